@@ -1,0 +1,165 @@
+/*
+ * tekubls.h -- C ABI of libtekubls_hip.so, the MI355X (gfx950) BLS12-381
+ * signature-verification backend for Teku.
+ *
+ * Drop-in boundary: a new implementation of Teku's SPI
+ *   tech.pegasys.teku.bls.impl.BLS12381
+ *   (infrastructure/bls/src/main/java/tech/pegasys/teku/bls/impl/BLS12381.java:34-157)
+ * next to BlstBLS12381 (impl/blst/BlstBLS12381.java), installed with
+ * BLS.setBlsImplementation (bls/BLS.java:51-53).  Each entry point below names
+ * the reference interface it replaces.  The JNI glue and the Java SPI classes a
+ * maintainer would add are shown in INTEGRATION.md.
+ *
+ * Conventions
+ *  - All points use the ZCash compressed encoding: G1 = 48 bytes, G2 = 96 bytes.
+ *  - Inputs are caller-owned host buffers, copied on entry; outputs go to
+ *    caller-provided buffers (SURVEY.md 8(b) "Ownership").
+ *  - Return value: a TBLS_* status.  Codes 0..7 mirror blst's BLST_ERROR enum
+ *    (the set jblst surfaces to BlstBLS12381); TBLS_DEVICE_ERROR is added.
+ *    The JNI layer maps them to BlsException / booleans exactly as
+ *    BlstBLS12381 does (BlstBLS12381.java:131-137, 169-188).
+ *  - Thread-safe and re-entrant: per-device submission lock, per-call staging.
+ *  - No CPU fallback: without a HIP device every call returns
+ *    TBLS_DEVICE_ERROR.
+ */
+#ifndef TEKUBLS_H
+#define TEKUBLS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+  TBLS_SUCCESS = 0,
+  TBLS_BAD_ENCODING = 1,
+  TBLS_POINT_NOT_ON_CURVE = 2,
+  TBLS_POINT_NOT_IN_GROUP = 3,
+  TBLS_AGGR_TYPE_MISMATCH = 4,
+  TBLS_VERIFY_FAIL = 5,
+  TBLS_PK_IS_INFINITY = 6,
+  TBLS_BAD_SCALAR = 7,
+  TBLS_DEVICE_ERROR = 8,
+  TBLS_BAD_ARGUMENT = 9, /* e.g. an empty public-key list inside a batch */
+};
+
+/* Library lifecycle.  n_devices = -1 uses every visible device.
+ * Replaces BlstLoader.INSTANCE (impl/blst/BlstLoader.java:32-51): a loader
+ * that gets an error here yields Optional.empty(). */
+int tbls_init(int n_devices, uint32_t flags);
+void tbls_shutdown(void);
+int tbls_device_count(void);
+
+/* BlstPublicKey.fromBytes + isValid (BlstPublicKey.java:38-45, 93-104):
+ * TBLS_SUCCESS iff the key decodes, is not infinity and is in G1. */
+int tbls_pk_validate(const uint8_t pk[48]);
+
+/* BlstSignature.fromBytes + isInGroup (BlstSignature.java:35-47, 147-149). */
+int tbls_sig_validate(const uint8_t sig[96], int* is_inf);
+
+/* BLS12381.aggregatePublicKeys -> BlstPublicKey.aggregate
+ * (BLS12381.java:95, BlstPublicKey.java:55-71): k >= 1; any invalid key makes
+ * the result the infinity key.  Decode failures -> TBLS_BAD_ENCODING etc. */
+int tbls_aggregate_pks(const uint8_t* pks, size_t k, uint8_t out[48]);
+
+/* BLS12381.aggregateSignatures -> BlstSignature.aggregate
+ * (BLS12381.java:105-106, BlstSignature.java:57-68): group check per input;
+ * k = 0 gives the infinity signature. */
+int tbls_aggregate_sigs(const uint8_t* sigs, size_t k, uint8_t out[96]);
+
+/* P2.hash_to (BlstBLS12381.java:59, HashToCurve.java:24-31). */
+int tbls_hash_to_g2(const uint8_t* msg, size_t len, const uint8_t* dst, size_t dlen, uint8_t out[96]);
+
+/* BlstBLS12381.sign (BlstBLS12381.java:48-63); sk big-endian, 0 < sk < r. */
+int tbls_sign(const uint8_t sk[32], const uint8_t* msg, size_t len, const uint8_t* dst, size_t dlen, uint8_t out[96]);
+
+/* BlstSecretKey.derivePublicKey (BlstSecretKey.java:75-78); sk = 0 -> infinity. */
+int tbls_sk_to_pk(const uint8_t sk[32], uint8_t out[48]);
+
+/* BlstBLS12381.verify -> blst core_verify(pk, hash=true)
+ * (BlstBLS12381.java:65-78).  *ok = 1 iff valid.  Decode errors are returned
+ * as codes (the facade turns them into false, BLS.java:99-101). */
+int tbls_verify(const uint8_t pk[48], const uint8_t* msg, size_t len, const uint8_t sig[96], const uint8_t* dst,
+                size_t dlen, int* ok);
+
+/* One signature set: n_pks keys (48 B each, contiguous), one message, one
+ * signature.  The unit of BLS.prepareBatchVerify (BLS.java:353-368). */
+typedef struct {
+  const uint8_t* pks;
+  uint32_t n_pks;
+  const uint8_t* msg;
+  uint32_t msg_len;
+  const uint8_t* sig;
+} tbls_set;
+
+typedef struct {
+  double total_ms;     /* API entry -> result, host clock */
+  double device_ms;    /* sum over devices of the kernel pipeline, HIP events */
+  uint32_t n_devices;  /* devices used */
+} tbls_timing;
+
+/* Randomized batch verification: BLS.batchVerify(pks, msgs, sigs) for n >= 2
+ * through prepareBatchVerify/completeBatchVerify (BLS.java:275-336,
+ * BlstBLS12381.java:112-189).  rand[i] in [1, 2^64] as BlstBLS12381
+ * .nextBatchRandomMultiplier (l.191-195) -- the caller owns the RNG.  n_gpus:
+ * shards sets over that many devices (0 = all initialised devices); each
+ * device produces one Fp12 partial product, gathered for one final
+ * exponentiation.  *ok = 1 iff every set is valid and the pairing product is
+ * 1.  n == 0 -> *ok = 0 (BLS.java:240-241).  A set with n_pks == 0 ->
+ * TBLS_BAD_ARGUMENT (BlstPublicKey.aggregate checkArgument, l.56). */
+int tbls_batch_verify(const tbls_set* sets, size_t n, const uint64_t* rand, int n_gpus, int* ok, tbls_timing* t);
+
+/* fastAggregateVerify per set (BLS.java:185-207, BlstSignature.java:125-129):
+ * ok_per_set[i] in {0,1}; an empty key list gives 0. */
+int tbls_fast_aggregate_verify_many(const tbls_set* sets, size_t n, int* ok_per_set);
+
+/* aggregateVerify (BLS.java:144-170, BlstSignature.java:104-122): n distinct
+ * (pk, msg) pairs against one aggregate signature. */
+int tbls_aggregate_verify(const uint8_t* pks, const uint8_t* const* msgs, const uint32_t* msg_lens, size_t n,
+                          const uint8_t sig[96], int* ok);
+
+/* ---- device-resident batch (inputs already in HBM; used by bench.py) ----
+ * All pointers are device pointers on `device`; `stream` is a hipStream_t (or
+ * NULL for the library's stream).  Produces the device's partial record
+ * (576-byte Fp12 product incl. the (-g1, sum r_i sig_i) pair, then a uint32
+ * count of invalid sets) at `partial_out` (580 bytes, device memory). */
+typedef struct {
+  const uint8_t* pks;      /* K * 48 */
+  const uint32_t* pk_off;  /* n + 1 offsets into pks (in keys) */
+  uint32_t n_keys;         /* K */
+  const uint8_t* msgs;     /* concatenated messages */
+  const uint32_t* msg_off; /* n + 1 byte offsets */
+  const uint8_t* sigs;     /* n * 96 */
+  const uint64_t* rand;    /* n */
+  uint32_t n;
+} tbls_dev_batch;
+
+#define TBLS_PARTIAL_BYTES 580
+
+int tbls_dev_batch_partial(int device, const tbls_dev_batch* b, void* stream, void* partial_out);
+
+/* Same as tbls_dev_batch_partial, also returning the per-stage device time
+ * (HIP events on `stream`) in stage_ms[7]: pk decompress, set pk
+ * aggregation+[r], signature decode+G2 check+[r], hash_to_G2, G2 sum, Miller
+ * loops, Fp12 product.  Blocks until the partial is ready. */
+int tbls_dev_batch_partial_timed(int device, const tbls_dev_batch* b, void* stream, void* partial_out, float* stage_ms);
+
+/* Multiply g partial records (device memory, contiguous) and run the final
+ * exponentiation: *ok = 1 iff no invalid set and the product is 1. */
+int tbls_dev_final_verify(int device, const void* partials, uint32_t g, void* stream, int* ok);
+
+/* ---- batched generation of synthetic workloads (sk big-endian, 32 B) ---- */
+int tbls_sk_to_pk_many(const uint8_t* sks, size_t n, uint8_t* out /* n*48 */);
+int tbls_sign_many(const uint8_t* sks, const uint8_t* msgs, const uint32_t* msg_off /* n+1 */, size_t n, const uint8_t* dst,
+                   size_t dlen, uint8_t* out /* n*96 */);
+
+/* ---- test hook: primitive ops (tb_testops.h records), run on the GPU ---- */
+int tbls_test_ops(int op, const uint8_t* in, uint8_t* out, size_t n);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* TEKUBLS_H */

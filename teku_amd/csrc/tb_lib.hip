@@ -1,0 +1,761 @@
+// libtekubls_hip.so: host side of the C ABI (include/tekubls.h).
+//
+// One HIP stream + workspace per device, guarded by a per-device mutex so the
+// library is thread-safe and re-entrant (prepareBatchVerify is called from
+// many ForkJoin / service threads in the reference: BLS.java:297-331,
+// AggregatingSignatureVerificationService.java:122-129).  Inputs are copied
+// into pinned staging on entry.  There is no CPU fallback.
+#include <chrono>
+#include <functional>
+#include <cstring>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "../../include/tekubls.h"
+#include "tb_kernels.hip"
+
+namespace {
+
+#define HIPCHK(x)                      \
+  do {                                 \
+    hipError_t e_ = (x);               \
+    if (e_ != hipSuccess) {            \
+      last_hip_error() = e_;           \
+      return TBLS_DEVICE_ERROR;        \
+    }                                  \
+  } while (0)
+
+hipError_t& last_hip_error() {
+  static thread_local hipError_t e = hipSuccess;
+  return e;
+}
+
+struct dbuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  int ensure(size_t bytes) {
+    if (bytes <= cap) return 0;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t nb = bytes < 4096 ? 4096 : bytes + bytes / 4;
+    if (hipMalloc(&p, nb) != hipSuccess) return -1;
+    cap = nb;
+    return 0;
+  }
+  template <typename T>
+  T* as(size_t off = 0) const {
+    return reinterpret_cast<T*>(static_cast<uint8_t*>(p) + off);
+  }
+};
+
+struct hbuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  int ensure(size_t bytes) {
+    if (bytes <= cap) return 0;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t nb = bytes < 4096 ? 4096 : bytes + bytes / 4;
+    if (hipHostMalloc(&p, nb, hipHostMallocDefault) != hipSuccess) return -1;
+    cap = nb;
+    return 0;
+  }
+  uint8_t* b() const { return static_cast<uint8_t*>(p); }
+};
+
+struct dev_ctx {
+  int dev = 0;
+  hipStream_t stream = nullptr;
+  std::mutex mu;
+  dbuf in, ws;  // device input staging, pipeline workspace
+  dbuf fin;     // final-exponentiation scratch
+  dbuf dstb;    // default DST for the device-resident API
+  hbuf hin, hout;
+};
+
+std::mutex g_mu;
+std::vector<dev_ctx*> g_ctx;
+bool g_inited = false;
+
+size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
+
+// --------------------------------------------------------------------------
+// workspace layout for one device pipeline over n sets / K keys
+// --------------------------------------------------------------------------
+struct ws_layout {
+  size_t pk_aff, pk_code, P, Q, skip, set_code, sig_code, rsig, f, gpart, fpart, fpart2, n_bad, result, total;
+  uint32_t nb_g2, nb_f;
+  ws_layout(uint32_t n, uint32_t K) {
+    const uint32_t np = n + 1;
+    nb_g2 = (n + TB_BLOCK - 1) / TB_BLOCK;
+    if (nb_g2 > 256) nb_g2 = 256;
+    if (nb_g2 == 0) nb_g2 = 1;
+    nb_f = (np + TB_BLOCK - 1) / TB_BLOCK;
+    if (nb_f > 256) nb_f = 256;
+    size_t o = 0;
+    pk_aff = o;   o = align_up(o + (size_t)K * sizeof(g1a));
+    pk_code = o;  o = align_up(o + K);
+    P = o;        o = align_up(o + (size_t)np * sizeof(g1a));
+    Q = o;        o = align_up(o + (size_t)np * sizeof(g2a));
+    skip = o;     o = align_up(o + np);
+    set_code = o; o = align_up(o + n);
+    sig_code = o; o = align_up(o + n);
+    rsig = o;     o = align_up(o + (size_t)n * sizeof(g2j));
+    f = o;        o = align_up(o + (size_t)np * sizeof(fp12));
+    gpart = o;    o = align_up(o + (size_t)nb_g2 * sizeof(g2j));
+    fpart = o;    o = align_up(o + (size_t)nb_f * sizeof(fp12));
+    fpart2 = o;   o = align_up(o + sizeof(fp12));
+    n_bad = o;    o = align_up(o + 4);
+    result = o;   o = align_up(o + 4);
+    total = o;
+  }
+};
+
+// Launch the partial pipeline for one device.  All pointers in `b` are
+// device pointers.  Writes the 580-byte partial record at `partial_out`.
+// Optionally leaves per-set codes in the workspace (set_code/sig_code).
+// stage events (optional): 0 start, 1 after k_pk_decompress, 2 after k_set_pk,
+// 3 after k_set_sig, 4 after k_set_hash, 5 after the G2 sum, 6 after k_miller,
+// 7 after the Fp12 product
+#define TB_NSTAGE_EV 8
+int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* partial_out, ws_layout& L,
+                   const uint8_t* dst, uint32_t dlen, bool keep_codes, hipEvent_t* ev = nullptr) {
+  const uint32_t n = b.n, K = b.n_keys;
+  L = ws_layout(n, K);
+  if (c.ws.ensure(L.total)) return TBLS_DEVICE_ERROR;
+  uint8_t* w = c.ws.as<uint8_t>();
+  HIPCHK(hipMemsetAsync(w + L.set_code, 0, n ? n : 1, s));
+  HIPCHK(hipMemsetAsync(w + L.n_bad, 0, 4, s));
+  (void)keep_codes;
+#define TB_EV(i) \
+  if (ev) HIPCHK(hipEventRecord(ev[i], s))
+  const dim3 blk(TB_BLOCK);
+  TB_EV(0);
+  if (K) hipLaunchKernelGGL(k_pk_decompress, dim3((K + TB_BLOCK - 1) / TB_BLOCK), blk, 0, s, b.pks, K, (g1a*)(w + L.pk_aff), w + L.pk_code);
+  TB_EV(1);
+  if (n) {
+    const dim3 g((n + TB_BLOCK - 1) / TB_BLOCK);
+    hipLaunchKernelGGL(k_set_pk, g, blk, 0, s, b.pk_off, (const g1a*)(w + L.pk_aff), w + L.pk_code, b.rand, n, (g1a*)(w + L.P),
+                       w + L.set_code, (uint32_t*)(w + L.n_bad));
+    TB_EV(2);
+    hipLaunchKernelGGL(k_set_sig, g, blk, 0, s, b.sigs, b.rand, n, (g2j*)(w + L.rsig), w + L.sig_code, (uint32_t*)(w + L.n_bad));
+    TB_EV(3);
+    hipLaunchKernelGGL(k_set_hash, g, blk, 0, s, b.msgs, b.msg_off, dst, dlen, n, (g2a*)(w + L.Q), w + L.skip);
+    TB_EV(4);
+    hipLaunchKernelGGL(k_g2_sum_partial, dim3(L.nb_g2), blk, 0, s, (const g2j*)(w + L.rsig), n, (g2j*)(w + L.gpart));
+  } else {
+    HIPCHK(hipMemsetAsync(w + L.gpart, 0, sizeof(g2j), s));  // z = 0 -> infinity
+    TB_EV(2);
+    TB_EV(3);
+    TB_EV(4);
+  }
+  hipLaunchKernelGGL(k_g2_sum_final, dim3(1), blk, 0, s, (const g2j*)(w + L.gpart), L.nb_g2, n, (g1a*)(w + L.P), (g2a*)(w + L.Q),
+                     w + L.skip);
+  TB_EV(5);
+  const uint32_t np = n + 1;
+  hipLaunchKernelGGL(k_miller, dim3((np + TB_BLOCK - 1) / TB_BLOCK), blk, 0, s, (const g1a*)(w + L.P), (const g2a*)(w + L.Q),
+                     w + L.skip, w + L.set_code, w + L.sig_code, n, np, (fp12*)(w + L.f));
+  TB_EV(6);
+  hipLaunchKernelGGL(k_fp12_prod, dim3(L.nb_f), blk, 0, s, (const fp12*)(w + L.f), np, (fp12*)(w + L.fpart));
+  hipLaunchKernelGGL(k_fp12_prod, dim3(1), blk, 0, s, (const fp12*)(w + L.fpart), L.nb_f, (fp12*)partial_out);
+  TB_EV(7);
+  HIPCHK(hipMemcpyAsync((uint8_t*)partial_out + sizeof(fp12), w + L.n_bad, 4, hipMemcpyDeviceToDevice, s));
+  HIPCHK(hipGetLastError());
+  return TBLS_SUCCESS;
+}
+
+// final: product of g partial records -> final exponentiation
+__global__ void k_gather_partials(const uint8_t* __restrict__ recs, uint32_t g, fp12* __restrict__ f, uint32_t* __restrict__ n_bad) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  uint32_t bad = 0;
+  for (uint32_t i = 0; i < g; i++) {
+    f[i] = *reinterpret_cast<const fp12*>(recs + (size_t)i * TBLS_PARTIAL_BYTES);
+    bad += *reinterpret_cast<const uint32_t*>(recs + (size_t)i * TBLS_PARTIAL_BYTES + sizeof(fp12));
+  }
+  n_bad[0] = bad;
+}
+
+int launch_final(dev_ctx& c, const void* recs, uint32_t g, hipStream_t s, int* result_host) {
+  const size_t need = align_up((size_t)g * sizeof(fp12)) + 2 * align_up(sizeof(fp12)) + 256;
+  if (c.fin.ensure(need)) return TBLS_DEVICE_ERROR;
+  uint8_t* w = c.fin.as<uint8_t>();
+  fp12* f = (fp12*)w;
+  fp12* prod = (fp12*)(w + align_up((size_t)g * sizeof(fp12)));
+  uint32_t* nbad = (uint32_t*)(w + align_up((size_t)g * sizeof(fp12)) + align_up(sizeof(fp12)));
+  int* res = (int*)(nbad + 1);
+  hipLaunchKernelGGL(k_gather_partials, dim3(1), dim3(64), 0, s, (const uint8_t*)recs, g, f, nbad);
+  hipLaunchKernelGGL(k_fp12_prod, dim3(1), dim3(TB_BLOCK), 0, s, (const fp12*)f, g, prod);
+  hipLaunchKernelGGL(k_final_verify, dim3(1), dim3(64), 0, s, (const fp12*)prod, (const uint32_t*)nbad, res);
+  HIPCHK(hipGetLastError());
+  if (c.hout.ensure(16)) return TBLS_DEVICE_ERROR;
+  HIPCHK(hipMemcpyAsync(c.hout.p, res, 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  *result_host = *(int*)c.hout.p;
+  return TBLS_SUCCESS;
+}
+
+int ensure_init() {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (g_inited) return g_ctx.empty() ? TBLS_DEVICE_ERROR : TBLS_SUCCESS;
+  return TBLS_DEVICE_ERROR;
+}
+
+dev_ctx* ctx_for(int d) {
+  if (d < 0 || d >= (int)g_ctx.size()) return nullptr;
+  return g_ctx[d];
+}
+
+// ---------------------------------------------------------------------------
+// host-side packing of tbls_set arrays into one contiguous staging image
+// ---------------------------------------------------------------------------
+struct packed {
+  size_t off_pks, off_pkoff, off_msgs, off_msgoff, off_sigs, off_rand, off_dst, total;
+  uint32_t n, K, M;
+};
+
+packed pack_layout(const tbls_set* sets, size_t lo, size_t hi, uint32_t dlen) {
+  packed p;
+  p.n = (uint32_t)(hi - lo);
+  uint64_t K = 0, M = 0;
+  for (size_t i = lo; i < hi; i++) {
+    K += sets[i].n_pks;
+    M += sets[i].msg_len;
+  }
+  p.K = (uint32_t)K;
+  p.M = (uint32_t)M;
+  size_t o = 0;
+  p.off_pks = o;    o = align_up(o + (size_t)K * 48);
+  p.off_pkoff = o;  o = align_up(o + ((size_t)p.n + 1) * 4);
+  p.off_msgs = o;   o = align_up(o + (M ? M : 1));
+  p.off_msgoff = o; o = align_up(o + ((size_t)p.n + 1) * 4);
+  p.off_sigs = o;   o = align_up(o + (size_t)p.n * 96);
+  p.off_rand = o;   o = align_up(o + (size_t)p.n * 8);
+  p.off_dst = o;    o = align_up(o + (dlen ? dlen : 1));
+  p.total = o;
+  return p;
+}
+
+void pack_fill(uint8_t* h, const packed& p, const tbls_set* sets, size_t lo, const uint64_t* rand, const uint8_t* dst, uint32_t dlen) {
+  uint32_t* pkoff = (uint32_t*)(h + p.off_pkoff);
+  uint32_t* moff = (uint32_t*)(h + p.off_msgoff);
+  uint64_t* rr = (uint64_t*)(h + p.off_rand);
+  uint32_t k = 0, m = 0;
+  for (uint32_t i = 0; i < p.n; i++) {
+    const tbls_set& s = sets[lo + i];
+    pkoff[i] = k;
+    moff[i] = m;
+    if (s.n_pks) memcpy(h + p.off_pks + (size_t)k * 48, s.pks, (size_t)s.n_pks * 48);
+    if (s.msg_len) memcpy(h + p.off_msgs + m, s.msg, s.msg_len);
+    memcpy(h + p.off_sigs + (size_t)i * 96, s.sig, 96);
+    rr[i] = rand ? rand[lo + i] : 1;
+    k += s.n_pks;
+    m += s.msg_len;
+  }
+  pkoff[p.n] = k;
+  moff[p.n] = m;
+  if (dlen) memcpy(h + p.off_dst, dst, dlen);
+}
+
+const uint8_t ETH2_DST[] = "BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_POP_";
+
+// Runs sets[lo, hi) on device d; produces the 580-byte partial record on the host.
+// Optionally returns per-set verdict codes (set_code | sig_code) on the host.
+int run_shard(int d, const tbls_set* sets, size_t lo, size_t hi, const uint64_t* rand, const uint8_t* dst, uint32_t dlen,
+              uint8_t* partial_host, uint8_t* codes_host, double* dev_ms) {
+  dev_ctx* c = ctx_for(d);
+  if (!c) return TBLS_DEVICE_ERROR;
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIPCHK(hipSetDevice(c->dev));
+  packed p = pack_layout(sets, lo, hi, dlen);
+  const size_t in_total = p.total + TBLS_PARTIAL_BYTES + 256;
+  if (c->hin.ensure(in_total) || c->in.ensure(in_total)) return TBLS_DEVICE_ERROR;
+  pack_fill(c->hin.b(), p, sets, lo, rand, dst, dlen);
+  hipStream_t s = c->stream;
+  hipEvent_t e0, e1;
+  HIPCHK(hipEventCreate(&e0));
+  HIPCHK(hipEventCreate(&e1));
+  HIPCHK(hipMemcpyAsync(c->in.p, c->hin.p, p.total, hipMemcpyHostToDevice, s));
+  uint8_t* di = c->in.as<uint8_t>();
+  tbls_dev_batch b;
+  b.pks = di + p.off_pks;
+  b.pk_off = (const uint32_t*)(di + p.off_pkoff);
+  b.n_keys = p.K;
+  b.msgs = di + p.off_msgs;
+  b.msg_off = (const uint32_t*)(di + p.off_msgoff);
+  b.sigs = di + p.off_sigs;
+  b.rand = (const uint64_t*)(di + p.off_rand);
+  b.n = p.n;
+  uint8_t* dpart = di + align_up(p.total);
+  ws_layout L(0, 0);
+  HIPCHK(hipEventRecord(e0, s));
+  int rc = launch_partial(*c, b, s, dpart, L, di + p.off_dst, dlen, codes_host != nullptr);
+  if (rc) return rc;
+  HIPCHK(hipEventRecord(e1, s));
+  const size_t outb = TBLS_PARTIAL_BYTES + (codes_host ? 2 * (size_t)p.n : 0);
+  if (c->hout.ensure(outb)) return TBLS_DEVICE_ERROR;
+  HIPCHK(hipMemcpyAsync(c->hout.p, dpart, TBLS_PARTIAL_BYTES, hipMemcpyDeviceToHost, s));
+  if (codes_host && p.n) {
+    HIPCHK(hipMemcpyAsync(c->hout.b() + TBLS_PARTIAL_BYTES, c->ws.as<uint8_t>(L.set_code), p.n, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(c->hout.b() + TBLS_PARTIAL_BYTES + p.n, c->ws.as<uint8_t>(L.sig_code), p.n, hipMemcpyDeviceToHost, s));
+  }
+  HIPCHK(hipStreamSynchronize(s));
+  float ms = 0;
+  (void)hipEventElapsedTime(&ms, e0, e1);
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  if (dev_ms) *dev_ms = ms;
+  memcpy(partial_host, c->hout.p, TBLS_PARTIAL_BYTES);
+  if (codes_host) {
+    for (uint32_t i = 0; i < p.n; i++) {
+      uint8_t a = c->hout.b()[TBLS_PARTIAL_BYTES + i], bb = c->hout.b()[TBLS_PARTIAL_BYTES + p.n + i];
+      codes_host[i] = bb ? bb : a;  // signature errors first (decode failures surface as BlsException)
+    }
+  }
+  return TBLS_SUCCESS;
+}
+
+int final_on_device0(const uint8_t* recs_host, uint32_t g, int* ok) {
+  dev_ctx* c = ctx_for(0);
+  if (!c) return TBLS_DEVICE_ERROR;
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIPCHK(hipSetDevice(c->dev));
+  // partial records go to a dedicated region past the final-exp scratch
+  dbuf recs;
+  if (recs.ensure((size_t)g * TBLS_PARTIAL_BYTES)) return TBLS_DEVICE_ERROR;
+  int rc = TBLS_SUCCESS;
+  if (hipMemcpyAsync(recs.p, recs_host, (size_t)g * TBLS_PARTIAL_BYTES, hipMemcpyHostToDevice, c->stream) != hipSuccess)
+    rc = TBLS_DEVICE_ERROR;
+  if (!rc) rc = launch_final(*c, recs.p, g, c->stream, ok);
+  (void)hipStreamSynchronize(c->stream);
+  (void)hipFree(recs.p);
+  return rc;
+}
+
+// generic single-kernel helpers: upload bytes, run, download
+struct upload {
+  std::vector<uint8_t> h;
+  size_t add(const void* src, size_t n) {
+    size_t o = align_up(h.size());
+    h.resize(o + (n ? n : 1));
+    if (n) memcpy(h.data() + o, src, n);
+    return o;
+  }
+};
+
+int with_device0(const std::function<int(dev_ctx&)>& fn) {
+  if (ensure_init()) return TBLS_DEVICE_ERROR;
+  dev_ctx* c = ctx_for(0);
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIPCHK(hipSetDevice(c->dev));
+  return fn(*c);
+}
+
+int stage_in(dev_ctx& c, const upload& u, uint8_t** d) {
+  if (c.in.ensure(u.h.size() + 4096)) return TBLS_DEVICE_ERROR;
+  HIPCHK(hipMemcpyAsync(c.in.p, u.h.data(), u.h.size(), hipMemcpyHostToDevice, c.stream));
+  *d = c.in.as<uint8_t>();
+  return TBLS_SUCCESS;
+}
+
+int fetch(dev_ctx& c, void* dst, const void* src, size_t n) {
+  HIPCHK(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, c.stream));
+  HIPCHK(hipStreamSynchronize(c.stream));
+  HIPCHK(hipGetLastError());
+  return TBLS_SUCCESS;
+}
+
+void sk_to_words(const uint8_t sk[32], uint64_t w[4]) {
+  for (int i = 0; i < 4; i++) {
+    uint64_t v = 0;
+    for (int j = 0; j < 8; j++) v = (v << 8) | sk[32 - 8 * (i + 1) + j];
+    w[i] = v;
+  }
+}
+
+// sk < r (BLSSecretKey.fromBytes range, BLSSecretKey.java:30-40)
+bool sk_in_range(const uint8_t sk[32]) {
+  static const uint8_t R_BE[32] = {0x73, 0xed, 0xa7, 0x53, 0x29, 0x9d, 0x7d, 0x48, 0x33, 0x39, 0xd8, 0x08, 0x09, 0xa1, 0xd8, 0x05,
+                                   0x53, 0xbd, 0xa4, 0x02, 0xff, 0xfe, 0x5b, 0xfe, 0xff, 0xff, 0xff, 0xff, 0x00, 0x00, 0x00, 0x01};
+  return memcmp(sk, R_BE, 32) < 0;
+}
+
+}  // namespace
+
+// ===========================================================================
+// C ABI
+// ===========================================================================
+extern "C" int tbls_init(int n_devices, uint32_t flags) {
+  (void)flags;
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (g_inited) return g_ctx.empty() ? TBLS_DEVICE_ERROR : TBLS_SUCCESS;
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) {
+    g_inited = true;
+    return TBLS_DEVICE_ERROR;
+  }
+  if (n_devices > 0 && n_devices < count) count = n_devices;
+  for (int d = 0; d < count; d++) {
+    dev_ctx* c = new dev_ctx();
+    c->dev = d;
+    if (hipSetDevice(d) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+      delete c;
+      break;
+    }
+    g_ctx.push_back(c);
+  }
+  g_inited = true;
+  return g_ctx.empty() ? TBLS_DEVICE_ERROR : TBLS_SUCCESS;
+}
+
+extern "C" void tbls_shutdown(void) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  for (dev_ctx* c : g_ctx) {
+    (void)hipSetDevice(c->dev);
+    if (c->in.p) (void)hipFree(c->in.p);
+    if (c->ws.p) (void)hipFree(c->ws.p);
+    if (c->fin.p) (void)hipFree(c->fin.p);
+    if (c->dstb.p) (void)hipFree(c->dstb.p);
+    if (c->hin.p) (void)hipHostFree(c->hin.p);
+    if (c->hout.p) (void)hipHostFree(c->hout.p);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+  }
+  g_ctx.clear();
+  g_inited = false;
+}
+
+extern "C" int tbls_device_count(void) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  return (int)g_ctx.size();
+}
+
+extern "C" int tbls_batch_verify(const tbls_set* sets, size_t n, const uint64_t* rand, int n_gpus, int* ok, tbls_timing* t) {
+  auto t0 = std::chrono::steady_clock::now();
+  *ok = 0;
+  if (ensure_init()) return TBLS_DEVICE_ERROR;
+  if (n == 0) return TBLS_SUCCESS;  // BLS.java:240-241
+  for (size_t i = 0; i < n; i++)
+    if (sets[i].n_pks == 0) return TBLS_BAD_ARGUMENT;
+  int G = (int)g_ctx.size();
+  if (n_gpus > 0 && n_gpus < G) G = n_gpus;
+  if ((size_t)G > n) G = (int)n;
+  // contiguous shards balanced by key count
+  uint64_t totalK = 0;
+  for (size_t i = 0; i < n; i++) totalK += sets[i].n_pks + 1;
+  std::vector<size_t> cut(G + 1, n);
+  cut[0] = 0;
+  {
+    uint64_t acc = 0;
+    int g = 1;
+    for (size_t i = 0; i < n && g < G; i++) {
+      acc += sets[i].n_pks + 1;
+      if (acc * G >= totalK * (uint64_t)g) cut[g++] = i + 1;
+    }
+  }
+  std::vector<uint8_t> recs((size_t)G * TBLS_PARTIAL_BYTES);
+  std::vector<int> rcs(G, 0);
+  std::vector<double> dms(G, 0);
+  if (G == 1) {
+    rcs[0] = run_shard(0, sets, 0, n, rand, ETH2_DST, 43, recs.data(), nullptr, &dms[0]);
+  } else {
+    std::vector<std::thread> th;
+    for (int g = 0; g < G; g++)
+      th.emplace_back([&, g] {
+        rcs[g] = run_shard(g, sets, cut[g], cut[g + 1], rand, ETH2_DST, 43, recs.data() + (size_t)g * TBLS_PARTIAL_BYTES, nullptr, &dms[g]);
+      });
+    for (auto& x : th) x.join();
+  }
+  for (int g = 0; g < G; g++)
+    if (rcs[g]) return rcs[g];
+  int rc = final_on_device0(recs.data(), (uint32_t)G, ok);
+  if (t) {
+    t->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    t->device_ms = 0;
+    for (double d : dms) t->device_ms += d;
+    t->n_devices = (uint32_t)G;
+  }
+  return rc;
+}
+
+// core_verify through the same pipeline with r = 1 (one set, no randomizer)
+static int verify_one(const uint8_t* pks, uint32_t n_pks, const uint8_t* msg, size_t len, const uint8_t sig[96], const uint8_t* dst,
+                      size_t dlen, int* ok, uint8_t* code_out) {
+  *ok = 0;
+  if (ensure_init()) return TBLS_DEVICE_ERROR;
+  if (dlen > 255) return TBLS_BAD_ARGUMENT;
+  tbls_set s = {pks, n_pks, msg, (uint32_t)len, sig};
+  uint8_t rec[TBLS_PARTIAL_BYTES];
+  uint8_t code = 0;
+  uint64_t one = 1;
+  int rc = run_shard(0, &s, 0, 1, &one, dst, (uint32_t)dlen, rec, &code, nullptr);
+  if (rc) return rc;
+  if (code_out) *code_out = code;
+  return final_on_device0(rec, 1, ok);
+}
+
+extern "C" int tbls_verify(const uint8_t pk[48], const uint8_t* msg, size_t len, const uint8_t sig[96], const uint8_t* dst, size_t dlen,
+                           int* ok) {
+  uint8_t code = 0;
+  int rc = verify_one(pk, 1, msg, len, sig, dst, dlen, ok, &code);
+  if (rc) return rc;
+  if (code == TB_BAD_ENCODING || code == TB_POINT_NOT_ON_CURVE) return code;  // decode failures are errors
+  return TBLS_SUCCESS;
+}
+
+extern "C" int tbls_fast_aggregate_verify_many(const tbls_set* sets, size_t n, int* ok_per_set) {
+  if (ensure_init()) return TBLS_DEVICE_ERROR;
+  for (size_t i = 0; i < n; i++) {
+    ok_per_set[i] = 0;
+    if (sets[i].n_pks == 0) continue;  // BLS.java:193-195
+    int ok = 0;
+    uint8_t code = 0;
+    int rc = verify_one(sets[i].pks, sets[i].n_pks, sets[i].msg, sets[i].msg_len, sets[i].sig, ETH2_DST, 43, &ok, &code);
+    if (rc) return rc;
+    ok_per_set[i] = ok;
+  }
+  return TBLS_SUCCESS;
+}
+
+extern "C" int tbls_aggregate_verify(const uint8_t* pks, const uint8_t* const* msgs, const uint32_t* msg_lens, size_t n, const uint8_t sig[96],
+                                     int* ok) {
+  *ok = 0;
+  if (ensure_init()) return TBLS_DEVICE_ERROR;
+  if (n == 0) return TBLS_SUCCESS;
+  static const uint8_t INF_SIG[96] = {0xc0};
+  std::vector<tbls_set> sets(n);
+  std::vector<uint64_t> ones(n, 1);
+  for (size_t i = 0; i < n; i++) sets[i] = {pks + 48 * i, 1, msgs[i], msg_lens[i], i == 0 ? sig : INF_SIG};
+  uint8_t rec[TBLS_PARTIAL_BYTES];
+  std::vector<uint8_t> codes(n);
+  int rc = run_shard(0, sets.data(), 0, n, ones.data(), ETH2_DST, 43, rec, codes.data(), nullptr);
+  if (rc) return rc;
+  return final_on_device0(rec, 1, ok);
+}
+
+extern "C" int tbls_pk_validate(const uint8_t pk[48]) {
+  return with_device0([&](dev_ctx& c) -> int {
+    upload u;
+    size_t o = u.add(pk, 48);
+    uint8_t* d;
+    int rc = stage_in(c, u, &d);
+    if (rc) return rc;
+    if (c.ws.ensure(4096)) return (int)TBLS_DEVICE_ERROR;
+    hipLaunchKernelGGL(k_pk_decompress, dim3(1), dim3(TB_BLOCK), 0, c.stream, d + o, 1u, c.ws.as<g1a>(0), c.ws.as<uint8_t>(1024));
+    uint8_t code = 0;
+    rc = fetch(c, &code, c.ws.as<uint8_t>(1024), 1);
+    return rc ? rc : (int)code;
+  });
+}
+
+extern "C" int tbls_sig_validate(const uint8_t sig[96], int* is_inf) {
+  return with_device0([&](dev_ctx& c) -> int {
+    upload u;
+    size_t o = u.add(sig, 96);
+    uint8_t* d;
+    int rc = stage_in(c, u, &d);
+    if (rc) return rc;
+    if (c.ws.ensure(4096)) return (int)TBLS_DEVICE_ERROR;
+    hipLaunchKernelGGL(k_sig_validate, dim3(1), dim3(TB_BLOCK), 0, c.stream, d + o, 1u, c.ws.as<uint32_t>(0));
+    uint32_t v = 0;
+    rc = fetch(c, &v, c.ws.as<uint32_t>(0), 4);
+    if (rc) return rc;
+    if (is_inf) *is_inf = (v >> 8) & 1;
+    return (int)(v & 0xff);
+  });
+}
+
+extern "C" int tbls_aggregate_pks(const uint8_t* pks, size_t k, uint8_t out[48]) {
+  if (k == 0) return TBLS_BAD_ARGUMENT;  // BlstPublicKey.java:56 checkArgument
+  return with_device0([&](dev_ctx& c) -> int {
+    upload u;
+    size_t o = u.add(pks, 48 * k);
+    uint8_t* d;
+    int rc = stage_in(c, u, &d);
+    if (rc) return rc;
+    const size_t aff = align_up(k * sizeof(g1a)), code = align_up(k);
+    if (c.ws.ensure(aff + code + 256)) return (int)TBLS_DEVICE_ERROR;
+    hipLaunchKernelGGL(k_pk_decompress, dim3((k + TB_BLOCK - 1) / TB_BLOCK), dim3(TB_BLOCK), 0, c.stream, d + o, (uint32_t)k, c.ws.as<g1a>(0),
+                       c.ws.as<uint8_t>(aff));
+    hipLaunchKernelGGL(k_aggregate_pks, dim3(1), dim3(TB_BLOCK), 0, c.stream, (const g1a*)c.ws.as<g1a>(0), (const uint8_t*)c.ws.as<uint8_t>(aff),
+                       (uint32_t)k, c.ws.as<uint8_t>(aff + code));
+    std::vector<uint8_t> codes(k);
+    rc = fetch(c, codes.data(), c.ws.as<uint8_t>(aff), k);
+    if (rc) return rc;
+    // decode failures throw in BlstPublicKey.fromBytes (BlstPublicKey.java:39-44)
+    for (size_t i = 0; i < k; i++)
+      if (codes[i] == TB_BAD_ENCODING || codes[i] == TB_POINT_NOT_ON_CURVE) return (int)codes[i];
+    return fetch(c, out, c.ws.as<uint8_t>(aff + code), 48);
+  });
+}
+
+extern "C" int tbls_aggregate_sigs(const uint8_t* sigs, size_t k, uint8_t out[96]) {
+  return with_device0([&](dev_ctx& c) -> int {
+    upload u;
+    size_t o = u.add(sigs, 96 * k);
+    uint8_t* d;
+    int rc = stage_in(c, u, &d);
+    if (rc) return rc;
+    if (c.ws.ensure(1024)) return (int)TBLS_DEVICE_ERROR;
+    hipLaunchKernelGGL(k_aggregate_sigs, dim3(1), dim3(TB_BLOCK), 0, c.stream, d + o, (uint32_t)k, c.ws.as<uint8_t>(0), c.ws.as<int>(512));
+    int status = 0;
+    rc = fetch(c, &status, c.ws.as<int>(512), 4);
+    if (rc) return rc;
+    if (status) return status;
+    return fetch(c, out, c.ws.as<uint8_t>(0), 96);
+  });
+}
+
+extern "C" int tbls_hash_to_g2(const uint8_t* msg, size_t len, const uint8_t* dst, size_t dlen, uint8_t out[96]) {
+  if (dlen > 255) return TBLS_BAD_ARGUMENT;
+  return with_device0([&](dev_ctx& c) -> int {
+    upload u;
+    uint32_t off[2] = {0, (uint32_t)len};
+    size_t om = u.add(msg, len), oo = u.add(off, 8), od = u.add(dst, dlen);
+    uint8_t* d;
+    int rc = stage_in(c, u, &d);
+    if (rc) return rc;
+    if (c.ws.ensure(1024)) return (int)TBLS_DEVICE_ERROR;
+    hipLaunchKernelGGL(k_hash_to_g2, dim3(1), dim3(TB_BLOCK), 0, c.stream, d + om, (const uint32_t*)(d + oo), d + od, (uint32_t)dlen, 1u,
+                       c.ws.as<uint8_t>(0));
+    return fetch(c, out, c.ws.as<uint8_t>(0), 96);
+  });
+}
+
+extern "C" int tbls_sign(const uint8_t sk[32], const uint8_t* msg, size_t len, const uint8_t* dst, size_t dlen, uint8_t out[96]) {
+  if (dlen > 255) return TBLS_BAD_ARGUMENT;
+  if (!sk_in_range(sk)) return TBLS_BAD_SCALAR;
+  bool zero = true;
+  for (int i = 0; i < 32; i++) zero = zero && sk[i] == 0;
+  if (zero) return TBLS_BAD_SCALAR;  // BlstBLS12381.java:54-56
+  return with_device0([&](dev_ctx& c) -> int {
+    upload u;
+    uint64_t w[4];
+    sk_to_words(sk, w);
+    uint32_t off[2] = {0, (uint32_t)len};
+    size_t ok_ = u.add(w, 32), om = u.add(msg, len), oo = u.add(off, 8), od = u.add(dst, dlen);
+    uint8_t* d;
+    int rc = stage_in(c, u, &d);
+    if (rc) return rc;
+    if (c.ws.ensure(1024)) return (int)TBLS_DEVICE_ERROR;
+    hipLaunchKernelGGL(k_sign, dim3(1), dim3(TB_BLOCK), 0, c.stream, (const uint64_t*)(d + ok_), d + om, (const uint32_t*)(d + oo), d + od,
+                       (uint32_t)dlen, 1u, c.ws.as<uint8_t>(0));
+    return fetch(c, out, c.ws.as<uint8_t>(0), 96);
+  });
+}
+
+extern "C" int tbls_sk_to_pk(const uint8_t sk[32], uint8_t out[48]) {
+  if (!sk_in_range(sk)) return TBLS_BAD_SCALAR;
+  return with_device0([&](dev_ctx& c) -> int {
+    upload u;
+    uint64_t w[4];
+    sk_to_words(sk, w);
+    size_t ok_ = u.add(w, 32);
+    uint8_t* d;
+    int rc = stage_in(c, u, &d);
+    if (rc) return rc;
+    if (c.ws.ensure(1024)) return (int)TBLS_DEVICE_ERROR;
+    hipLaunchKernelGGL(k_sk_to_pk, dim3(1), dim3(TB_BLOCK), 0, c.stream, (const uint64_t*)(d + ok_), 1u, c.ws.as<uint8_t>(0));
+    return fetch(c, out, c.ws.as<uint8_t>(0), 48);
+  });
+}
+
+extern "C" int tbls_dev_batch_partial(int device, const tbls_dev_batch* b, void* stream, void* partial_out) {
+  if (ensure_init()) return TBLS_DEVICE_ERROR;
+  dev_ctx* c = ctx_for(device);
+  if (!c) return TBLS_DEVICE_ERROR;
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIPCHK(hipSetDevice(c->dev));
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  if (!c->dstb.p) {
+    if (c->dstb.ensure(256)) return TBLS_DEVICE_ERROR;
+    HIPCHK(hipMemcpy(c->dstb.p, ETH2_DST, 43, hipMemcpyHostToDevice));
+  }
+  ws_layout L(0, 0);
+  return launch_partial(*c, *b, s, partial_out, L, c->dstb.as<uint8_t>(), 43, false);
+}
+
+extern "C" int tbls_dev_batch_partial_timed(int device, const tbls_dev_batch* b, void* stream, void* partial_out, float* stage_ms) {
+  if (ensure_init()) return TBLS_DEVICE_ERROR;
+  dev_ctx* c = ctx_for(device);
+  if (!c) return TBLS_DEVICE_ERROR;
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIPCHK(hipSetDevice(c->dev));
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  if (!c->dstb.p) {
+    if (c->dstb.ensure(256)) return TBLS_DEVICE_ERROR;
+    HIPCHK(hipMemcpy(c->dstb.p, ETH2_DST, 43, hipMemcpyHostToDevice));
+  }
+  hipEvent_t ev[TB_NSTAGE_EV];
+  for (int i = 0; i < TB_NSTAGE_EV; i++) HIPCHK(hipEventCreate(&ev[i]));
+  ws_layout L(0, 0);
+  int rc = launch_partial(*c, *b, s, partial_out, L, c->dstb.as<uint8_t>(), 43, false, ev);
+  if (!rc) {
+    HIPCHK(hipEventSynchronize(ev[TB_NSTAGE_EV - 1]));
+    for (int i = 0; i + 1 < TB_NSTAGE_EV; i++) {
+      float ms = 0;
+      (void)hipEventElapsedTime(&ms, ev[i], ev[i + 1]);
+      stage_ms[i] = ms;
+    }
+  }
+  for (int i = 0; i < TB_NSTAGE_EV; i++) (void)hipEventDestroy(ev[i]);
+  return rc;
+}
+
+// batched helpers for building synthetic workloads on the device
+extern "C" int tbls_sk_to_pk_many(const uint8_t* sks, size_t n, uint8_t* out) {
+  return with_device0([&](dev_ctx& c) -> int {
+    std::vector<uint64_t> w(4 * n);
+    for (size_t i = 0; i < n; i++) sk_to_words(sks + 32 * i, &w[4 * i]);
+    upload u;
+    size_t o = u.add(w.data(), 32 * n);
+    uint8_t* d;
+    int rc = stage_in(c, u, &d);
+    if (rc) return rc;
+    if (c.ws.ensure(48 * n + 256)) return (int)TBLS_DEVICE_ERROR;
+    hipLaunchKernelGGL(k_sk_to_pk, dim3((n + TB_BLOCK - 1) / TB_BLOCK), dim3(TB_BLOCK), 0, c.stream, (const uint64_t*)(d + o), (uint32_t)n,
+                       c.ws.as<uint8_t>(0));
+    return fetch(c, out, c.ws.p, 48 * n);
+  });
+}
+
+extern "C" int tbls_sign_many(const uint8_t* sks, const uint8_t* msgs, const uint32_t* msg_off, size_t n, const uint8_t* dst, size_t dlen,
+                              uint8_t* out) {
+  if (dlen > 255) return TBLS_BAD_ARGUMENT;
+  return with_device0([&](dev_ctx& c) -> int {
+    std::vector<uint64_t> w(4 * n);
+    for (size_t i = 0; i < n; i++) sk_to_words(sks + 32 * i, &w[4 * i]);
+    upload u;
+    size_t ok_ = u.add(w.data(), 32 * n), om = u.add(msgs, msg_off[n]), oo = u.add(msg_off, 4 * (n + 1)), od = u.add(dst, dlen);
+    uint8_t* d;
+    int rc = stage_in(c, u, &d);
+    if (rc) return rc;
+    if (c.ws.ensure(96 * n + 256)) return (int)TBLS_DEVICE_ERROR;
+    hipLaunchKernelGGL(k_sign, dim3((n + TB_BLOCK - 1) / TB_BLOCK), dim3(TB_BLOCK), 0, c.stream, (const uint64_t*)(d + ok_), d + om,
+                       (const uint32_t*)(d + oo), d + od, (uint32_t)dlen, (uint32_t)n, c.ws.as<uint8_t>(0));
+    return fetch(c, out, c.ws.p, 96 * n);
+  });
+}
+
+extern "C" int tbls_dev_final_verify(int device, const void* partials, uint32_t g, void* stream, int* ok) {
+  if (ensure_init()) return TBLS_DEVICE_ERROR;
+  dev_ctx* c = ctx_for(device);
+  if (!c) return TBLS_DEVICE_ERROR;
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIPCHK(hipSetDevice(c->dev));
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  return launch_final(*c, partials, g, s, ok);
+}
+
+extern "C" int tbls_test_ops(int op, const uint8_t* in, uint8_t* out, size_t n) {
+  return with_device0([&](dev_ctx& c) -> int {
+    if (c.in.ensure(n * TB_TEST_IN + 256) || c.ws.ensure(n * TB_TEST_OUT + 256)) return (int)TBLS_DEVICE_ERROR;
+    HIPCHK(hipMemcpyAsync(c.in.p, in, n * TB_TEST_IN, hipMemcpyHostToDevice, c.stream));
+    HIPCHK(hipMemsetAsync(c.ws.p, 0, n * TB_TEST_OUT, c.stream));
+    hipLaunchKernelGGL(k_test_ops, dim3((n + TB_BLOCK - 1) / TB_BLOCK), dim3(TB_BLOCK), 0, c.stream, op, c.in.as<uint8_t>(), c.ws.as<uint8_t>(),
+                       (uint32_t)n);
+    return fetch(c, out, c.ws.p, n * TB_TEST_OUT);
+  });
+}

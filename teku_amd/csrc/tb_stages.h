@@ -1,0 +1,72 @@
+// Per-item bodies of the batch-verification stages.  The kernels in
+// tb_kernels.hip call exactly these; tools/count_muls.py runs them on the host
+// build to count Fp multiplications per unit (the roofline's algorithmic work).
+#pragma once
+#include "tb_codec.h"
+#include "tb_h2c.h"
+#include "tb_pairing.h"
+
+namespace tb {
+
+// decode + !infinity + in G1  (BlstPublicKey.fromBytes / isValid)
+TB_HD TB_INLINE int stage_pk(const uint8_t* b48, g1a& a) {
+  bool inf;
+  int code = g1_decompress(a, inf, b48);
+  if (code == TB_SUCCESS && inf) code = TB_PK_IS_INFINITY;
+  if (code == TB_SUCCESS && !g1_in_group(jac_from_aff(a))) code = TB_POINT_NOT_IN_GROUP;
+  if (code != TB_SUCCESS) {
+    a.x = fp_zero();
+    a.y = fp_zero();
+  }
+  return code;
+}
+
+// aggregate keys [b, e) (any invalid -> PK_IS_INFINITY), P = [r] apk affine
+TB_HD TB_INLINE int stage_set_pk(const g1a* pk_aff, const uint8_t* pk_code, uint32_t b, uint32_t e, uint64_t r, g1a& P) {
+  int code = TB_SUCCESS;
+  P.x = fp_zero();
+  P.y = fp_zero();
+  if (e - b == 1) {
+    if (pk_code[b] != TB_SUCCESS) return TB_PK_IS_INFINITY;
+    g1j rp = jac_mul_u64_aff(pk_aff[b], r);
+    if (!jac_to_aff(P, rp)) code = TB_PK_IS_INFINITY;
+    return code;
+  }
+  g1j acc = jac_inf<fp>();
+  for (uint32_t k = b; k < e; k++) {
+    if (pk_code[k] != TB_SUCCESS) return TB_PK_IS_INFINITY;  // BlstPublicKey.java:58-65
+    acc = jac_add_aff(acc, pk_aff[k]);
+  }
+  if (jac_is_inf(acc)) return TB_PK_IS_INFINITY;
+  g1j rp = jac_mul_u64(acc, r);
+  if (!jac_to_aff(P, rp)) code = TB_PK_IS_INFINITY;
+  return code;
+}
+
+// decode signature, G2 check, [r] sig (infinity allowed and skipped)
+TB_HD TB_INLINE int stage_set_sig(const uint8_t* b96, uint64_t r, g2j& rs) {
+  g2a a;
+  bool inf;
+  int code = g2_decompress(a, inf, b96);
+  rs = jac_inf<fp2>();
+  if (code == TB_SUCCESS && !inf) {
+    if (!g2_in_group(jac_from_aff(a)))
+      code = TB_POINT_NOT_IN_GROUP;
+    else
+      rs = jac_mul_u64_aff(a, r);
+  }
+  return code;
+}
+
+// Q = hash_to_G2(m) affine; false for the (negligible) infinity case
+TB_HD TB_INLINE bool stage_set_hash(const xmd_ctx& c, g2a& Q) {
+  g2j h = hash_to_g2(c);
+  bool ok = jac_to_aff(Q, h);
+  if (!ok) {
+    Q.x = fp2_zero();
+    Q.y = fp2_zero();
+  }
+  return ok;
+}
+
+}  // namespace tb

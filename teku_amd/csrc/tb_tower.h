@@ -1,0 +1,239 @@
+// Extension tower: Fp2 = Fp[u]/(u^2+1), Fp6 = Fp2[v]/(v^3-xi), Fp12 = Fp6[w]/(w^2-v),
+// xi = 1+u.  Elements live in VGPRs (an Fp12 is 144 x 32-bit registers).
+#pragma once
+#include "tb_fp.h"
+
+namespace tb {
+
+struct fp2 {
+  fp c0, c1;
+};
+struct fp6 {
+  fp2 c0, c1, c2;
+};
+struct fp12 {
+  fp6 c0, c1;
+};
+
+// ---------------------------------------------------------------------------
+// Fp2
+// ---------------------------------------------------------------------------
+TB_HD TB_INLINE fp2 fp2_zero() { return {fp_zero(), fp_zero()}; }
+TB_HD TB_INLINE fp2 fp2_one() { return {fp_one(), fp_zero()}; }
+TB_HD TB_INLINE fp2 fp2_from_const(const uint32_t (&c)[2][12]) { return {fp_from_const(c[0]), fp_from_const(c[1])}; }
+TB_HD TB_INLINE fp2 fp2_add(const fp2& a, const fp2& b) { return {fp_add(a.c0, b.c0), fp_add(a.c1, b.c1)}; }
+TB_HD TB_INLINE fp2 fp2_sub(const fp2& a, const fp2& b) { return {fp_sub(a.c0, b.c0), fp_sub(a.c1, b.c1)}; }
+TB_HD TB_INLINE fp2 fp2_dbl(const fp2& a) { return {fp_dbl(a.c0), fp_dbl(a.c1)}; }
+TB_HD TB_INLINE fp2 fp2_neg(const fp2& a) { return {fp_neg(a.c0), fp_neg(a.c1)}; }
+TB_HD TB_INLINE fp2 fp2_conj(const fp2& a) { return {a.c0, fp_neg(a.c1)}; }
+TB_HD TB_INLINE bool fp2_is_zero(const fp2& a) { return fp_is_zero(a.c0) && fp_is_zero(a.c1); }
+TB_HD TB_INLINE bool fp2_eq(const fp2& a, const fp2& b) { return fp_eq(a.c0, b.c0) && fp_eq(a.c1, b.c1); }
+TB_HD TB_INLINE fp2 fp2_sel(bool c, const fp2& a, const fp2& b) { return {fp_sel(c, a.c0, b.c0), fp_sel(c, a.c1, b.c1)}; }
+TB_HD TB_INLINE fp2 fp2_mul_fp(const fp2& a, const fp& b) { return {fp_mul(a.c0, b), fp_mul(a.c1, b)}; }
+TB_HD TB_INLINE fp2 fp2_mul3(const fp2& a) { return {fp_mul3(a.c0), fp_mul3(a.c1)}; }
+TB_HD TB_INLINE fp2 fp2_half(const fp2& a) { return {fp_half(a.c0), fp_half(a.c1)}; }
+
+TB_HD TB_INLINE fp2 fp2_mul(const fp2& a, const fp2& b) {
+  fp t0 = fp_mul(a.c0, b.c0);
+  fp t1 = fp_mul(a.c1, b.c1);
+  fp t2 = fp_mul(fp_add(a.c0, a.c1), fp_add(b.c0, b.c1));
+  return {fp_sub(t0, t1), fp_sub(fp_sub(t2, t0), t1)};
+}
+
+TB_HD TB_INLINE fp2 fp2_sqr(const fp2& a) {
+  fp t = fp_mul(a.c0, a.c1);
+  return {fp_mul(fp_add(a.c0, a.c1), fp_sub(a.c0, a.c1)), fp_dbl(t)};
+}
+
+// multiply by xi = 1 + u
+TB_HD TB_INLINE fp2 fp2_mul_xi(const fp2& a) { return {fp_sub(a.c0, a.c1), fp_add(a.c0, a.c1)}; }
+
+TB_HD TB_NOINLINE fp2 fp2_inv(const fp2& a) {
+  fp n = fp_add(fp_sqr(a.c0), fp_sqr(a.c1));
+  fp t = fp_inv(n);
+  return {fp_mul(a.c0, t), fp_neg(fp_mul(a.c1, t))};
+}
+
+// RFC 9380 sgn0 (plain-value parity)
+TB_HD TB_INLINE uint32_t fp2_sgn0(const fp2& a) {
+  fp a0 = fp_from_mont(a.c0), a1 = fp_from_mont(a.c1);
+  uint32_t s0 = a0.l[0] & 1, z0 = fp_is_zero(a0) ? 1u : 0u, s1 = a1.l[0] & 1;
+  return s0 | (z0 & s1);
+}
+
+// ZCash lexicographic flag (c1 first)
+TB_HD TB_INLINE bool fp2_sign_zcash(const fp2& a) {
+  fp a0 = fp_from_mont(a.c0), a1 = fp_from_mont(a.c1);
+  bool g1 = fp_plain_gt(a1, P_MINUS_1_DIV_2), g0 = fp_plain_gt(a0, P_MINUS_1_DIV_2);
+  return fp_is_zero(a1) ? g0 : g1;
+}
+
+// Square root in Fp2 for p = 3 mod 4 (branch-free up to the final check).
+// gamma = sqrt(N(a)); delta = (a0 + gamma)/2 (or (a0 - gamma)/2 if that is 0);
+// s = delta^((p-3)/4); chi = s^2 delta = +-1;
+//   chi = +1:  x = s*delta + (a1 s/2) u
+//   chi = -1:  x = (-a1 s/2) + (s*delta) u
+// Returns false if a is not a square.  `norm_gamma` (optional) lets a caller
+// reuse sqrt(N(a)) (SSWU computes it to decide squareness).
+TB_HD TB_NOINLINE bool fp2_sqrt_with_gamma(fp2& out, const fp2& a, const fp& gamma) {
+  fp delta = fp_half(fp_add(a.c0, gamma));
+  delta = fp_sel(fp_is_zero(delta), fp_half(fp_sub(a.c0, gamma)), delta);
+  fp s = fp_pow_pm3d4(delta);
+  fp sd = fp_mul(s, delta);
+  fp chi = fp_mul(s, sd);
+  fp hs = fp_half(fp_mul(a.c1, s));
+  bool pos = fp_eq(chi, fp_one());
+  fp2 x;
+  x.c0 = fp_sel(pos, sd, fp_neg(hs));
+  x.c1 = fp_sel(pos, hs, sd);
+  out = x;
+  return fp2_eq(fp2_sqr(x), a);
+}
+
+TB_HD TB_INLINE fp fp2_norm(const fp2& a) { return fp_add(fp_sqr(a.c0), fp_sqr(a.c1)); }
+
+TB_HD TB_INLINE bool fp2_sqrt(fp2& out, const fp2& a) {
+  fp gamma = fp_sqrt_cand(fp2_norm(a));
+  return fp2_sqrt_with_gamma(out, a, gamma);
+}
+
+// ---------------------------------------------------------------------------
+// Fp6
+// ---------------------------------------------------------------------------
+TB_HD TB_INLINE fp6 fp6_zero() { return {fp2_zero(), fp2_zero(), fp2_zero()}; }
+TB_HD TB_INLINE fp6 fp6_one() { return {fp2_one(), fp2_zero(), fp2_zero()}; }
+TB_HD TB_INLINE fp6 fp6_add(const fp6& a, const fp6& b) { return {fp2_add(a.c0, b.c0), fp2_add(a.c1, b.c1), fp2_add(a.c2, b.c2)}; }
+TB_HD TB_INLINE fp6 fp6_sub(const fp6& a, const fp6& b) { return {fp2_sub(a.c0, b.c0), fp2_sub(a.c1, b.c1), fp2_sub(a.c2, b.c2)}; }
+TB_HD TB_INLINE fp6 fp6_neg(const fp6& a) { return {fp2_neg(a.c0), fp2_neg(a.c1), fp2_neg(a.c2)}; }
+TB_HD TB_INLINE fp6 fp6_mul_v(const fp6& a) { return {fp2_mul_xi(a.c2), a.c0, a.c1}; }
+TB_HD TB_INLINE bool fp6_is_zero(const fp6& a) { return fp2_is_zero(a.c0) && fp2_is_zero(a.c1) && fp2_is_zero(a.c2); }
+
+TB_HD TB_NOINLINE fp6 fp6_mul(const fp6& a, const fp6& b) {
+  fp2 t0 = fp2_mul(a.c0, b.c0);
+  fp2 t1 = fp2_mul(a.c1, b.c1);
+  fp2 t2 = fp2_mul(a.c2, b.c2);
+  fp2 c0 = fp2_add(t0, fp2_mul_xi(fp2_sub(fp2_mul(fp2_add(a.c1, a.c2), fp2_add(b.c1, b.c2)), fp2_add(t1, t2))));
+  fp2 c1 = fp2_add(fp2_sub(fp2_mul(fp2_add(a.c0, a.c1), fp2_add(b.c0, b.c1)), fp2_add(t0, t1)), fp2_mul_xi(t2));
+  fp2 c2 = fp2_add(fp2_sub(fp2_mul(fp2_add(a.c0, a.c2), fp2_add(b.c0, b.c2)), fp2_add(t0, t2)), t1);
+  return {c0, c1, c2};
+}
+
+// a * (b0 + b1 v)
+TB_HD TB_NOINLINE fp6 fp6_mul_by_01(const fp6& a, const fp2& b0, const fp2& b1) {
+  fp2 t0 = fp2_mul(a.c0, b0);
+  fp2 t1 = fp2_mul(a.c1, b1);
+  fp2 c0 = fp2_add(t0, fp2_mul_xi(fp2_mul(a.c2, b1)));
+  fp2 c1 = fp2_sub(fp2_sub(fp2_mul(fp2_add(a.c0, a.c1), fp2_add(b0, b1)), t0), t1);
+  fp2 c2 = fp2_add(t1, fp2_mul(a.c2, b0));
+  return {c0, c1, c2};
+}
+
+// a * (b1 v)
+TB_HD TB_INLINE fp6 fp6_mul_by_1(const fp6& a, const fp2& b1) {
+  return {fp2_mul_xi(fp2_mul(a.c2, b1)), fp2_mul(a.c0, b1), fp2_mul(a.c1, b1)};
+}
+
+TB_HD TB_NOINLINE fp6 fp6_inv(const fp6& a) {
+  fp2 t0 = fp2_sub(fp2_sqr(a.c0), fp2_mul_xi(fp2_mul(a.c1, a.c2)));
+  fp2 t1 = fp2_sub(fp2_mul_xi(fp2_sqr(a.c2)), fp2_mul(a.c0, a.c1));
+  fp2 t2 = fp2_sub(fp2_sqr(a.c1), fp2_mul(a.c0, a.c2));
+  fp2 d = fp2_add(fp2_mul(a.c0, t0), fp2_mul_xi(fp2_add(fp2_mul(a.c2, t1), fp2_mul(a.c1, t2))));
+  fp2 di = fp2_inv(d);
+  return {fp2_mul(t0, di), fp2_mul(t1, di), fp2_mul(t2, di)};
+}
+
+// ---------------------------------------------------------------------------
+// Fp12
+// ---------------------------------------------------------------------------
+TB_HD TB_INLINE fp12 fp12_one() { return {fp6_one(), fp6_zero()}; }
+TB_HD TB_INLINE fp12 fp12_conj(const fp12& a) { return {a.c0, fp6_neg(a.c1)}; }
+
+TB_HD TB_NOINLINE fp12 fp12_mul(const fp12& a, const fp12& b) {
+  fp6 t0 = fp6_mul(a.c0, b.c0);
+  fp6 t1 = fp6_mul(a.c1, b.c1);
+  fp6 c1 = fp6_sub(fp6_mul(fp6_add(a.c0, a.c1), fp6_add(b.c0, b.c1)), fp6_add(t0, t1));
+  fp6 c0 = fp6_add(t0, fp6_mul_v(t1));
+  return {c0, c1};
+}
+
+// complex squaring: (a0 + a1 w)^2 = (a0^2 + v a1^2) + 2 a0 a1 w
+TB_HD TB_NOINLINE fp12 fp12_sqr(const fp12& a) {
+  fp6 ab = fp6_mul(a.c0, a.c1);
+  fp6 t = fp6_mul(fp6_add(a.c0, a.c1), fp6_add(a.c0, fp6_mul_v(a.c1)));
+  fp6 c0 = fp6_sub(fp6_sub(t, ab), fp6_mul_v(ab));
+  fp6 c1 = fp6_add(ab, ab);
+  return {c0, c1};
+}
+
+// f * line, line = (A + B v) + (C v) w   (sparse positions 0, 1, 4)
+TB_HD TB_NOINLINE fp12 fp12_mul_by_line(const fp12& f, const fp2& A, const fp2& B, const fp2& C) {
+  fp6 t0 = fp6_mul_by_01(f.c0, A, B);
+  fp6 t1 = fp6_mul_by_1(f.c1, C);
+  fp6 c1 = fp6_sub(fp6_sub(fp6_mul_by_01(fp6_add(f.c0, f.c1), A, fp2_add(B, C)), t0), t1);
+  fp6 c0 = fp6_add(t0, fp6_mul_v(t1));
+  return {c0, c1};
+}
+
+TB_HD TB_NOINLINE fp12 fp12_inv(const fp12& a) {
+  fp6 t = fp6_sub(fp6_mul(a.c0, a.c0), fp6_mul_v(fp6_mul(a.c1, a.c1)));
+  fp6 ti = fp6_inv(t);
+  return {fp6_mul(a.c0, ti), fp6_neg(fp6_mul(a.c1, ti))};
+}
+
+TB_HD TB_INLINE bool fp12_is_one(const fp12& a) {
+  return fp_eq(a.c0.c0.c0, fp_one()) && fp_is_zero(a.c0.c0.c1) && fp2_is_zero(a.c0.c1) && fp2_is_zero(a.c0.c2) &&
+         fp6_is_zero(a.c1);
+}
+
+// Frobenius a^p:  coefficient of w^i -> conj(coef) * gamma_i,
+// w^0=c0.c0, w^1=c1.c0, w^2=c0.c1, w^3=c1.c1, w^4=c0.c2, w^5=c1.c2
+TB_HD TB_NOINLINE fp12 fp12_frob(const fp12& a) {
+  fp12 r;
+  r.c0.c0 = fp2_conj(a.c0.c0);
+  r.c1.c0 = fp2_mul(fp2_conj(a.c1.c0), fp2_from_const(FROB_G1));
+  r.c0.c1 = fp2_mul(fp2_conj(a.c0.c1), fp2_from_const(FROB_G2));
+  r.c1.c1 = fp2_mul(fp2_conj(a.c1.c1), fp2_from_const(FROB_G3));
+  r.c0.c2 = fp2_mul(fp2_conj(a.c0.c2), fp2_from_const(FROB_G4));
+  r.c1.c2 = fp2_mul(fp2_conj(a.c1.c2), fp2_from_const(FROB_G5));
+  return r;
+}
+
+// Granger-Scott squaring for elements of the cyclotomic subgroup.
+// Views Fp12 as Fp4^3 with Fp4 pairs (c0.c0, c1.c1), (c1.c0, c0.c2), (c0.c1, c1.c2).
+TB_HD TB_INLINE void fp4_sqr(fp2& r0, fp2& r1, const fp2& a, const fp2& b) {
+  fp2 t0 = fp2_sqr(a);
+  fp2 t1 = fp2_sqr(b);
+  r0 = fp2_add(fp2_mul_xi(t1), t0);
+  r1 = fp2_sub(fp2_sub(fp2_sqr(fp2_add(a, b)), t0), t1);
+}
+
+TB_HD TB_NOINLINE fp12 fp12_cyc_sqr(const fp12& f) {
+  fp2 z0 = f.c0.c0, z4 = f.c0.c1, z3 = f.c0.c2, z2 = f.c1.c0, z1 = f.c1.c1, z5 = f.c1.c2;
+  fp2 t0, t1, t2, t3;
+  fp4_sqr(t0, t1, z0, z1);
+  z0 = fp2_sub(t0, z0);
+  z0 = fp2_add(fp2_dbl(z0), t0);
+  z1 = fp2_add(t1, z1);
+  z1 = fp2_add(fp2_dbl(z1), t1);
+  fp4_sqr(t0, t1, z2, z3);
+  fp4_sqr(t2, t3, z4, z5);
+  z4 = fp2_sub(t0, z4);
+  z4 = fp2_add(fp2_dbl(z4), t0);
+  z5 = fp2_add(t1, z5);
+  z5 = fp2_add(fp2_dbl(z5), t1);
+  t0 = fp2_mul_xi(t3);
+  z2 = fp2_add(t0, z2);
+  z2 = fp2_add(fp2_dbl(z2), t0);
+  z3 = fp2_sub(t2, z3);
+  z3 = fp2_add(fp2_dbl(z3), t2);
+  fp12 r;
+  r.c0.c0 = z0;
+  r.c0.c1 = z4;
+  r.c0.c2 = z3;
+  r.c1.c0 = z2;
+  r.c1.c1 = z1;
+  r.c1.c2 = z5;
+  return r;
+}
+
+}  // namespace tb

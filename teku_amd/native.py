@@ -1,0 +1,162 @@
+"""ctypes binding of libtekubls_hip.so (include/tekubls.h).
+
+The product path: every call goes to the HIP library.  If the library or a
+HIP device is missing this module raises -- there is no CPU fallback.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libtekubls_hip.so")
+
+SUCCESS = 0
+BAD_ENCODING = 1
+POINT_NOT_ON_CURVE = 2
+POINT_NOT_IN_GROUP = 3
+AGGR_TYPE_MISMATCH = 4
+VERIFY_FAIL = 5
+PK_IS_INFINITY = 6
+BAD_SCALAR = 7
+DEVICE_ERROR = 8
+BAD_ARGUMENT = 9
+
+PARTIAL_BYTES = 580
+
+
+class TblsSet(ctypes.Structure):
+    _fields_ = [
+        ("pks", ctypes.c_void_p),
+        ("n_pks", ctypes.c_uint32),
+        ("msg", ctypes.c_void_p),
+        ("msg_len", ctypes.c_uint32),
+        ("sig", ctypes.c_void_p),
+    ]
+
+
+class TblsTiming(ctypes.Structure):
+    _fields_ = [("total_ms", ctypes.c_double), ("device_ms", ctypes.c_double), ("n_devices", ctypes.c_uint32)]
+
+
+class TblsDevBatch(ctypes.Structure):
+    _fields_ = [
+        ("pks", ctypes.c_void_p),
+        ("pk_off", ctypes.c_void_p),
+        ("n_keys", ctypes.c_uint32),
+        ("msgs", ctypes.c_void_p),
+        ("msg_off", ctypes.c_void_p),
+        ("sigs", ctypes.c_void_p),
+        ("rand", ctypes.c_void_p),
+        ("n", ctypes.c_uint32),
+    ]
+
+
+class NativeError(RuntimeError):
+    def __init__(self, code, what):
+        super().__init__(f"{what}: tbls status {code}")
+        self.code = code
+
+
+_lib = None
+_lock = threading.Lock()
+
+_SIGS = {
+    "tbls_init": (ctypes.c_int, [ctypes.c_int, ctypes.c_uint32]),
+    "tbls_shutdown": (None, []),
+    "tbls_device_count": (ctypes.c_int, []),
+    "tbls_pk_validate": (ctypes.c_int, [ctypes.c_char_p]),
+    "tbls_sig_validate": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int)]),
+    "tbls_aggregate_pks": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p]),
+    "tbls_aggregate_sigs": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p]),
+    "tbls_hash_to_g2": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p]),
+    "tbls_sign": (
+        ctypes.c_int,
+        [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p],
+    ),
+    "tbls_sk_to_pk": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p]),
+    "tbls_verify": (
+        ctypes.c_int,
+        [
+            ctypes.c_char_p,
+            ctypes.c_char_p,
+            ctypes.c_size_t,
+            ctypes.c_char_p,
+            ctypes.c_char_p,
+            ctypes.c_size_t,
+            ctypes.POINTER(ctypes.c_int),
+        ],
+    ),
+    "tbls_batch_verify": (
+        ctypes.c_int,
+        [
+            ctypes.POINTER(TblsSet),
+            ctypes.c_size_t,
+            ctypes.POINTER(ctypes.c_uint64),
+            ctypes.c_int,
+            ctypes.POINTER(ctypes.c_int),
+            ctypes.POINTER(TblsTiming),
+        ],
+    ),
+    "tbls_fast_aggregate_verify_many": (ctypes.c_int, [ctypes.POINTER(TblsSet), ctypes.c_size_t, ctypes.POINTER(ctypes.c_int)]),
+    "tbls_aggregate_verify": (
+        ctypes.c_int,
+        [
+            ctypes.c_char_p,
+            ctypes.POINTER(ctypes.c_char_p),
+            ctypes.POINTER(ctypes.c_uint32),
+            ctypes.c_size_t,
+            ctypes.c_char_p,
+            ctypes.POINTER(ctypes.c_int),
+        ],
+    ),
+    "tbls_dev_batch_partial": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(TblsDevBatch), ctypes.c_void_p, ctypes.c_void_p]),
+    "tbls_dev_final_verify": (
+        ctypes.c_int,
+        [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)],
+    ),
+    "tbls_dev_batch_partial_timed": (
+        ctypes.c_int,
+        [ctypes.c_int, ctypes.POINTER(TblsDevBatch), ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_float)],
+    ),
+    "tbls_sk_to_pk_many": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p]),
+    "tbls_sign_many": (
+        ctypes.c_int,
+        [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p],
+    ),
+    "tbls_test_ops": (ctypes.c_int, [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]),
+}
+
+EXPORTED = tuple(_SIGS)
+
+
+def load_library(path: str = LIB_PATH):
+    """dlopen the library and bind every entry point (no device initialisation)."""
+    if not os.path.exists(path):
+        raise NativeError(DEVICE_ERROR, f"HIP library not built: {path} (run __graft_entry__.build())")
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+def lib():
+    """The initialised library (raises NativeError when no HIP device is present)."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            L = load_library()
+            rc = L.tbls_init(-1, 0)
+            if rc != SUCCESS:
+                raise NativeError(rc, "tbls_init (no usable HIP device)")
+            _lib = L
+        return _lib
+
+
+def check(rc, what):
+    if rc != SUCCESS:
+        raise NativeError(rc, what)

@@ -1,0 +1,307 @@
+"""GPU parity of the BLS hot path through the C ABI / SPI mirror vs the oracle.
+
+Mirrors the reference's own tests:
+  infrastructure/bls/src/test/java/tech/pegasys/teku/bls/BLSTest.java
+  infrastructure/bls/src/test/java/tech/pegasys/teku/bls/impl/AbstractBLS12381Test.java
+  infrastructure/bls/src/test/java/tech/pegasys/teku/bls/BLSSecretKeyTest.java
+and the tampered-set list of SURVEY.md 8(d).
+"""
+
+import base64
+import ctypes
+import random
+
+import pytest
+
+from oracle import bls12_381 as O
+from oracle.keys import blstestutil_sk, interop_sk
+from tests.test_oracle_kats import (
+    KAT_AGGSLOT_SIG,
+    KAT_FAV4_MSG,
+    KAT_FAV4_PKS,
+    KAT_FAV4_SIG,
+    KAT_RANDAO_SIG,
+    KAT_REAL_PK,
+    KAT_REAL_ROOT,
+    KAT_REAL_SIG,
+    KAT_SK_PK,
+    local_signer_roots,
+)
+
+pytestmark = pytest.mark.gpu
+
+NOT_IN_G2 = bytes.fromhex("80" + "00" * 94 + "04")
+BAD_PK = bytes.fromhex("9378a6e3984e96d2cd50450c76ca14732f1300efa04aecdb805b22e6d6926a85ef409e8f3acf494a1481090bf32ce3bd")
+NUL_DST = b"BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_NUL_"
+
+
+@pytest.fixture(scope="module")
+def hip():
+    import torch  # noqa: F401
+
+    from teku_amd import bls, native
+
+    L = native.lib()
+    impl = bls.HipBLS12381()
+    bls.BLS.set_bls_implementation(impl)
+    return bls, native, L, impl
+
+
+@pytest.fixture(scope="module")
+def sets8():
+    sks = [interop_sk(i) for i in range(8)]
+    msgs = [bytes([i + 1]) * 32 for i in range(8)]
+    pks = [O.sk_to_pk(s) for s in sks]
+    sigs = [O.sign(s, m) for s, m in zip(sks, msgs)]
+    return sks, pks, msgs, sigs
+
+
+def _raw(bls, pks, msgs, sigs, rands=None, n_gpus=0):
+    sets = [(b"".join(p) if isinstance(p, list) else p, len(p) if isinstance(p, list) else 1, m, s) for p, m, s in zip(pks, msgs, sigs)]
+    rands = rands or [random.getrandbits(63) | 1 for _ in sets]
+    return bls.batch_verify_raw(sets, rands, n_gpus)
+
+
+def test_batch_valid_and_tampered(hip, sets8):
+    bls = hip[0]
+    sks, pks, msgs, sigs = sets8
+    assert _raw(bls, pks, msgs, sigs) is True
+    assert O.batch_verify([[p] for p in pks], msgs, sigs) is True
+    cases = {}
+    s2 = list(sigs)
+    s2[3] = O.sign(sks[3], bytes([msgs[3][0] ^ 1]) + msgs[3][1:])
+    cases["sig on m^1"] = (pks, msgs, s2)
+    m2 = list(msgs)
+    m2[1], m2[2] = m2[2], m2[1]
+    cases["swapped msgs"] = (pks, m2, sigs)
+    for name, bad in [("zero sig", bytes(96)), ("inf sig", O.INFINITY_G2), ("non-G2 sig", NOT_IN_G2)]:
+        s3 = list(sigs)
+        s3[5] = bad
+        cases[name] = (pks, msgs, s3)
+    for name, bad in [("inf pk", O.INFINITY_G1), ("0x9378 pk", BAD_PK), ("zero pk", bytes(48))]:
+        p3 = list(pks)
+        p3[6] = bad
+        cases[name] = (p3, msgs, sigs)
+    for name, (p, m, s) in cases.items():
+        got = _raw(bls, p, m, s)
+        exp = O.batch_verify([[x] for x in p], m, s)
+        assert got == exp is False, name
+
+
+def test_batch_multikey_sets(hip):
+    """fastAggregateVerify-style sets (configs 2/3 shape, scaled down)."""
+    bls = hip[0]
+    pks_l, msgs, sigs = [], [], []
+    for j in range(4):
+        sks = [interop_sk(10 * j + i) for i in range(5)]
+        m = bytes([0xA0 + j]) * 32
+        pks_l.append([O.sk_to_pk(s) for s in sks])
+        msgs.append(m)
+        sigs.append(O.aggregate_sigs([O.sign(s, m) for s in sks]))
+    assert _raw(bls, pks_l, msgs, sigs) is True
+    pks_l[2] = pks_l[2][:-1]
+    assert _raw(bls, pks_l, msgs, sigs) is False
+
+
+def test_simulated_shards_equal_single_device(hip, sets8):
+    """G logical shards on one GPU -> gather of partial records -> one final exp."""
+    import torch
+
+    bls, native, L, _ = hip
+    sks, pks, msgs, sigs = sets8
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    def shard(lo, hi):
+        n = hi - lo
+        u8 = lambda b: torch.frombuffer(bytearray(b), dtype=torch.uint8).to(dev)  # noqa: E731
+        t = dict(
+            pks=u8(b"".join(pks[lo:hi])),
+            msgs=u8(b"".join(msgs[lo:hi])),
+            sigs=u8(b"".join(sigs[lo:hi])),
+            pk_off=torch.arange(0, n + 1, dtype=torch.int32, device=dev),
+            msg_off=torch.arange(0, 32 * (n + 1), 32, dtype=torch.int32, device=dev),
+            rand=torch.randint(1, 1 << 62, (n,), dtype=torch.int64, device=dev),
+        )
+        d = native.TblsDevBatch(
+            t["pks"].data_ptr(), t["pk_off"].data_ptr(), n, t["msgs"].data_ptr(), t["msg_off"].data_ptr(), t["sigs"].data_ptr(), t["rand"].data_ptr(), n
+        )
+        out = torch.empty(native.PARTIAL_BYTES, dtype=torch.uint8, device=dev)
+        native.check(L.tbls_dev_batch_partial(0, ctypes.byref(d), stream, out.data_ptr()), "partial")
+        torch.cuda.synchronize()
+        return out
+
+    for G in (1, 2, 4):
+        cuts = [len(pks) * g // G for g in range(G + 1)]
+        recs = torch.cat([shard(cuts[g], cuts[g + 1]) for g in range(G)])
+        ok = ctypes.c_int(0)
+        native.check(L.tbls_dev_final_verify(0, recs.data_ptr(), G, stream, ctypes.byref(ok)), "final")
+        assert ok.value == 1, G
+    # one bad shard poisons the gathered result
+    sigs_bad = list(sigs)
+    sigs_bad[7] = sigs[6]
+    pks_bak = pks
+    recs = torch.cat([shard(0, 4)])
+    sigs[:] = sigs_bad
+    recs = torch.cat([recs, shard(4, 8)])
+    sigs[:] = [O.sign(s, m) for s, m in zip(sks, msgs)]
+    ok = ctypes.c_int(1)
+    native.check(L.tbls_dev_final_verify(0, recs.data_ptr(), 2, stream, ctypes.byref(ok)), "final")
+    assert ok.value == 0
+    assert pks_bak is pks
+
+
+def test_hash_sign_keys_bit_exact(hip):
+    bls, native, L, _ = hip
+    for msg, dst in [(b"", O.ETH2_DST), (b"abc", O.ETH2_DST), (b"\x42" * 32, O.ETH2_DST), (b"abc", NUL_DST), (bytes(range(200)), O.ETH2_DST)]:
+        out = ctypes.create_string_buffer(96)
+        native.check(L.tbls_hash_to_g2(msg, len(msg), dst, len(dst), out), "h2g")
+        assert out.raw == O.g2_compress(O.hash_to_g2(msg, dst))
+    for sk, pk in KAT_SK_PK:
+        out = ctypes.create_string_buffer(48)
+        native.check(L.tbls_sk_to_pk(sk.to_bytes(32, "big"), out), "sk2pk")
+        assert out.raw.hex() == pk
+    sk = blstestutil_sk(1234)
+    randao, aggslot = local_signer_roots()
+    for root, exp in [(randao, KAT_RANDAO_SIG), (aggslot, KAT_AGGSLOT_SIG)]:
+        out = ctypes.create_string_buffer(96)
+        native.check(L.tbls_sign(sk.to_bytes(32, "big"), root, 32, O.ETH2_DST, len(O.ETH2_DST), out), "sign")
+        assert out.raw == base64.b64decode(exp)
+    assert L.tbls_sign(bytes(32), b"x", 1, O.ETH2_DST, len(O.ETH2_DST), ctypes.create_string_buffer(96)) == native.BAD_SCALAR
+
+
+def test_aggregation_bit_exact(hip):
+    bls, native, L, impl = hip
+    sks = [interop_sk(i) for i in range(7)]
+    pks = [O.sk_to_pk(s) for s in sks]
+    sigs = [O.sign(s, b"agg") for s in sks]
+    assert impl.aggregate_public_keys([bls.HipPublicKey(p) for p in pks]).to_bytes_compressed() == O.aggregate_pks(pks)
+    assert impl.aggregate_signatures([bls.HipSignature(s) for s in sigs]).to_bytes_compressed() == O.aggregate_sigs(sigs)
+    # any invalid key -> infinity (BlstPublicKey.java:58-65)
+    assert impl.aggregate_public_keys([bls.HipPublicKey(p) for p in pks[:3] + [BAD_PK]]).to_bytes_compressed() == O.INFINITY_G1
+    # P + (-P) -> infinity; empty signature list -> infinity
+    assert impl.aggregate_signatures([]).to_bytes_compressed() == O.INFINITY_G2
+    with pytest.raises(bls.BlsException):
+        impl.aggregate_signatures([bls.HipSignature(sigs[0]), bls.HipSignature(NOT_IN_G2)])
+
+
+# ---- BLSTest.java mirrors (through the facade) -------------------------------
+def test_blstest_sign_verify(hip):
+    bls = hip[0]
+    B = bls.BLS
+    kp = bls.BLSKeyPair(bls.BLSSecretKey.from_bytes_mod_r(blstestutil_sk(42).to_bytes(32, "big")))
+    msg = b"Hello, world!"
+    sig = B.sign(kp.secret_key, msg)
+    assert B.verify(kp.public_key, msg, sig)
+    assert not B.verify(kp.public_key, msg, bls.BLSSignature.empty())  # l.43-51
+    # DST variants (l.375-391)
+    s2 = B.sign(kp.secret_key, msg, NUL_DST)
+    assert B.verify(kp.public_key, msg, s2, NUL_DST)
+    assert not B.verify(kp.public_key, msg, s2)
+
+
+def test_blstest_kats(hip):
+    bls = hip[0]
+    B = bls.BLS
+    pks = [bls.BLSPublicKey.from_bytes_compressed_validate(p) for p in KAT_FAV4_PKS]
+    assert B.fast_aggregate_verify(pks, KAT_FAV4_MSG, bls.BLSSignature.from_bytes_compressed(KAT_FAV4_SIG))  # l.106-126
+    assert B.verify(bls.BLSPublicKey(KAT_REAL_PK), KAT_REAL_ROOT, bls.BLSSignature(KAT_REAL_SIG))  # l.359-373
+
+
+def test_blstest_invalid_key_batches(hip):
+    """anyVerify_invalidPublicKeyShouldNotThrowAndReturnFalse (l.128-167)."""
+    bls = hip[0]
+    B = bls.BLS
+    kp = bls.BLSKeyPair(bls.BLSSecretKey.from_bytes_mod_r(blstestutil_sk(1).to_bytes(32, "big")))
+    msg = KAT_FAV4_MSG
+    invalid = bls.BLSPublicKey.from_bytes_compressed(bytes(48))
+    valid = bls.BLSPublicKey.from_bytes_compressed(kp.public_key.to_bytes_compressed())
+    sig = B.sign(kp.secret_key, msg)
+    assert not B.verify(invalid, msg, sig)
+    assert not B.aggregate_verify([invalid], [msg], sig)
+    assert not B.aggregate_verify([valid, invalid], [msg, msg], sig)
+    assert not B.fast_aggregate_verify([invalid], msg, sig)
+    assert not B.fast_aggregate_verify([valid, valid, invalid], msg, sig)
+    assert not B.batch_verify([[valid], [invalid]], [msg, msg], [sig, sig])
+    many = [[valid]] * 63 + [[invalid]]
+    assert not B.batch_verify(many, [msg] * 64, [sig] * 64)
+    assert B.batch_verify([[valid]] * 64, [msg] * 64, [sig] * 64)
+
+
+def test_blstest_infinity_and_aggregate(hip):
+    bls = hip[0]
+    B = bls.BLS
+    inf_pk = bls.BLSPublicKey.from_bytes_compressed(O.INFINITY_G1)
+    inf_sig = bls.BLSSignature.from_bytes_compressed(O.INFINITY_G2)
+    assert not B.verify(inf_pk, b"Hello, world!", inf_sig)  # l.262-266
+    zero = bls.BLSSecretKey.from_bytes(bytes(32))
+    assert zero.to_public_key().to_bytes_compressed() == O.INFINITY_G1  # l.268-271
+    with pytest.raises(ValueError):
+        B.sign(zero, b"Hello, world!")  # l.273-277
+    kp1 = bls.BLSKeyPair(bls.BLSSecretKey.from_bytes_mod_r(blstestutil_sk(1).to_bytes(32, "big")))
+    sig1 = B.sign(kp1.secret_key, b"Hello, world!")
+    agg_pk = bls.BLSPublicKey.aggregate([kp1.public_key, zero.to_public_key()])
+    agg_sig = B.aggregate([sig1, inf_sig])
+    assert not B.verify(agg_pk, b"Hello, world!", agg_sig)  # l.279-292
+    with pytest.raises(ValueError):
+        B.aggregate([bls.BLSSignature(NOT_IN_G2)])  # l.294-297
+    with pytest.raises(ValueError):
+        B.aggregate([])  # l.212-216
+    with pytest.raises(ValueError):
+        B.aggregate([sig1, bls.BLSSignature.empty(), sig1])  # l.76-85
+    assert B.aggregate([sig1]) == sig1  # l.69-73
+    # prepare(inf pk, inf sig) x2 -> complete false (l.299-312); valid + inf (l.342-357)
+    a = B.prepare_batch_verify(0, [zero.to_public_key()], b"Hello, world!", inf_sig)
+    b = B.prepare_batch_verify(1, [zero.to_public_key()], b"Hello, world!", inf_sig)
+    assert not B.complete_batch_verify([a, b])
+    c = B.prepare_batch_verify(0, [kp1.public_key], b"Hello, world!", sig1)
+    assert not B.complete_batch_verify([c, b])
+    assert B.complete_batch_verify([c])
+    assert not B.fast_aggregate_verify([], b"", bls.BLSSignature.empty())  # l.218-228
+    assert not B.aggregate_verify([], [], bls.BLSSignature.empty())
+
+
+def test_blstest_odd_double_pairing(hip):
+    """batchVerifyWithPairingOddNumberOfVerifications (l.314-340)."""
+    bls = hip[0]
+    B = bls.BLS
+    kp = bls.BLSKeyPair(bls.BLSSecretKey.from_bytes_mod_r(blstestutil_sk(1).to_bytes(32, "big")))
+    m = [b"Hello, 1!", b"Hello, 2!", b"Hello, 3!"]
+    s = [B.sign(kp.secret_key, x) for x in m]
+    bad = B.sign(kp.secret_key, m[1])
+    pks = [[kp.public_key]] * 3
+    assert not B.batch_verify(pks, m, [s[0], s[1], bad], True, False)
+    assert B.batch_verify(pks, m, s, True, False)
+
+
+def test_aggregate_verify_distinct(hip):
+    """succeedsWhenAggregateVerifyWithDistinctMessagesReturnsTrue (l.170-189) and the infinite-pair case (l.191-210)."""
+    bls = hip[0]
+    B = bls.BLS
+    kps = [bls.BLSKeyPair(bls.BLSSecretKey.from_bytes_mod_r(blstestutil_sk(i).to_bytes(32, "big"))) for i in (1, 2, 3)]
+    msgs = [b"Hello, world 1!", b"Hello, world 2!", b"Hello, world 3!"]
+    sigs = [B.sign(k.secret_key, m) for k, m in zip(kps, msgs)]
+    agg = B.aggregate(sigs)
+    assert B.aggregate_verify([k.public_key for k in kps], msgs, agg)
+    inf = bls.BLSPublicKey.from_bytes_compressed(O.INFINITY_G1)
+    agg2 = B.aggregate(sigs[:2] + [bls.BLSSignature.infinity()])
+    assert not B.aggregate_verify([kps[0].public_key, kps[1].public_key, inf], msgs, agg2)
+
+
+def test_spi_prepare_complete_combinatorics(hip):
+    """AbstractBLS12381Test.java:189-229: n = 0..7 positive; one invalid at each position."""
+    bls, native, L, impl = hip
+    sks = [interop_sk(100 + i) for i in range(7)]
+    pks = [bls.HipPublicKey(O.sk_to_pk(s)) for s in sks]
+    msgs = [bytes([i]) * 32 for i in range(7)]
+    sigs = [bls.HipSignature(O.sign(s, m)) for s, m in zip(sks, msgs)]
+    for n in range(0, 8):
+        prep = [impl.prepare_batch_verify(i, [pks[i]], msgs[i], sigs[i]) for i in range(n)]
+        assert impl.complete_batch_verify(prep) is True
+    for bad in range(6):
+        prep = [impl.prepare_batch_verify(i, [pks[i]], msgs[i], sigs[(i + 1) % 6 if i == bad else i]) for i in range(6)]
+        assert impl.complete_batch_verify(prep) is False
+    assert impl.complete_batch_verify([object()]) is False  # ClassCastException path (BlstBLS12381.java:185-188)
+    eager = bls.HipBLS12381(eager=True)
+    with pytest.raises(ValueError):  # BlstTest.succeedsWhenPrepareBatchVerifyNotInG2ThrowsException
+        eager.prepare_batch_verify(0, [pks[0]], msgs[0], bls.HipSignature(NOT_IN_G2))

@@ -1,0 +1,121 @@
+"""GPU parity of the primitive kernels (tb_testops.h via tbls_test_ops) against the oracle."""
+
+import random
+
+import pytest
+
+from oracle import bls12_381 as O
+from oracle.keys import interop_sk
+from tests.opcodec import *  # noqa: F401,F403
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def run():
+    from teku_amd import native
+
+    L = native.lib()
+    return lambda op, recs: run_ops(L.tbls_test_ops, op, recs)
+
+
+def _rng():
+    return random.Random(1234)
+
+
+def test_fp_ops(run):
+    rng = _rng()
+    A = [rng.randrange(O.P) for _ in range(200)] + [0, 1, O.P - 1]
+    B = [rng.randrange(O.P) for _ in range(200)] + [O.P - 1, O.P - 1, O.P - 1]
+    recs = [enc_fp(a) + enc_fp(b) for a, b in zip(A, B)]
+    assert [dec_fp(x) for x in run("FP_MUL", recs)] == [a * b % O.P for a, b in zip(A, B)]
+    assert [dec_fp(x) for x in run("FP_ADD", recs)] == [(a + b) % O.P for a, b in zip(A, B)]
+    assert [dec_fp(x) for x in run("FP_SUB", recs)] == [(a - b) % O.P for a, b in zip(A, B)]
+    out = run("FP_INV", [enc_fp(a) for a in A[:16]])
+    assert all(dec_fp(x) * a % O.P == 1 for x, a in zip(out, A[:16]) if a)
+
+
+def test_fp2_fp12(run):
+    rng = _rng()
+    rf2 = lambda: (rng.randrange(O.P), rng.randrange(O.P))  # noqa: E731
+    X = [rf2() for _ in range(64)]
+    Y = [rf2() for _ in range(64)]
+    out = run("FP2_MUL", [enc_fp2(a) + enc_fp2(b) for a, b in zip(X, Y)])
+    assert [dec_fp2(x) for x in out] == [O.f2_mul(a, b) for a, b in zip(X, Y)]
+    sq = [O.f2_sqr(x) for x in X[:8]] + X[8:16] + [(0, 0), (5, 0), (O.P - 5, 0), (0, 7)]
+    out = run("FP2_SQRT", [enc_fp2(a) for a in sq])
+    for x, a in zip(out, sq):
+        exp = O.f2_sqrt(a) is not None
+        assert u32(x) == exp
+        if exp:
+            assert O.f2_sqr(dec_fp2(x[4:])) == a
+    rf12 = lambda: tuple(tuple(rf2() for _ in range(3)) for _ in range(2))  # noqa: E731
+    F = [rf12() for _ in range(4)]
+    G = [rf12() for _ in range(4)]
+    assert [dec_fp12(x) for x in run("FP12_MUL", [enc_fp12(a) + enc_fp12(b) for a, b in zip(F, G)])] == [
+        O.f12_mul(a, b) for a, b in zip(F, G)
+    ]
+    assert [dec_fp12(x) for x in run("FP12_SQR", [enc_fp12(a) for a in F])] == [O.f12_mul(a, a) for a in F]
+    cyc = []
+    for a in F:
+        t = O.f12_mul(O.f12_conj(a), O.f12_inv(a))
+        cyc.append(O.f12_mul(O.f12_pow(t, O.P * O.P), t))
+    assert [dec_fp12(x) for x in run("FP12_CYC_SQR", [enc_fp12(a) for a in cyc])] == [O.f12_mul(a, a) for a in cyc]
+    out = run("FP12_INV", [enc_fp12(a) for a in F[:2]])
+    assert all(O.f12_mul(dec_fp12(x), a) == O.F12_ONE for x, a in zip(out, F[:2]))
+
+
+def test_decompress_and_groups(run):
+    sks = [interop_sk(i) for i in range(6)]
+    pks = [O.sk_to_pk(s) for s in sks] + [
+        O.INFINITY_G1,
+        bytes(48),
+        bytes.fromhex("9378a6e3984e96d2cd50450c76ca14732f1300efa04aecdb805b22e6d6926a85ef409e8f3acf494a1481090bf32ce3bd"),
+        bytes([0x80]) + bytes(47),
+        bytes([0xC0]) + bytes(46) + b"\x01",
+        bytes([0x9F]) + b"\xff" * 47,
+    ]
+    for x, b in zip(run("G1_DECOMP", pks), pks):
+        code, a = O.g1_decompress(b)
+        c = u32(x)
+        assert c & 0xFF == code
+        assert bool(c & 0x100) == (code == O.SUCCESS and a is None)
+        if code == O.SUCCESS and a is not None:
+            assert (dec_fp(x[4:]), dec_fp(x[52:])) == a
+    sigs = [O.sign(s, b"m%d" % i) for i, s in enumerate(sks[:3])] + [
+        O.INFINITY_G2,
+        bytes(96),
+        bytes.fromhex("80" + "00" * 94 + "04"),
+        bytes([0xA0]) + bytes(95),
+    ]
+    for x, b in zip(run("G2_DECOMP", sigs), sigs):
+        code, a = O.g2_decompress(b)
+        c = u32(x)
+        assert c & 0xFF == code
+        if code == O.SUCCESS and a is not None:
+            assert (dec_fp2(x[4:100]), dec_fp2(x[100:196])) == a
+    pts = [O.g1_decompress(b)[1] for b in pks[:4]] + [O.g1_decompress(pks[8])[1]]
+    got = [u32(x) for x in run("G1_IN_GROUP", [enc_fp(a[0]) + enc_fp(a[1]) for a in pts])]
+    assert got == [1, 1, 1, 1, 0]
+    p2 = [O.g2_decompress(s)[1] for s in sigs[:3]] + [O.g2_decompress(sigs[5])[1]]
+    got = [u32(x) for x in run("G2_IN_GROUP", [enc_fp2(a[0]) + enc_fp2(a[1]) for a in p2])]
+    assert got == [1, 1, 1, 0]
+
+
+def test_hash_to_g2(run):
+    msgs = [b"", b"abc", b"\x99" * 32, bytes(range(256)) * 2, b"Hello, world!"]
+    recs = [enc_h2c(m) for m in msgs] + [enc_h2c(b"abc", b"BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_NUL_")]
+    exp = [O.g2_compress(O.hash_to_g2(m)) for m in msgs] + [
+        O.g2_compress(O.hash_to_g2(b"abc", b"BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_NUL_"))
+    ]
+    assert [x[:96] for x in run("HASH_TO_G2", recs)] == exp
+
+
+def test_pairing_pieces(run):
+    P1, Q1 = O.G1_GEN, O.G2_GEN
+    out = run("MILLER", [enc_fp(P1[0]) + enc_fp(P1[1]) + enc_fp2(Q1[0]) + enc_fp2(Q1[1])])
+    f = dec_fp12(out[0])
+    assert O.final_exponentiation(f) == O.pairing(P1, Q1)
+    g = dec_fp12(run("FINAL_EXP", [enc_fp12(f)])[0])
+    e = O.pairing(P1, Q1)
+    assert g == O.f12_mul(O.f12_mul(e, e), e)
