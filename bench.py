@@ -195,8 +195,9 @@ def main():
         return
 
     stage_ms = [a / args.steps for a in stage_acc]
-    # dominant kernel and its integer-VALU roofline
-    dom = max(range(len(STAGES)), key=lambda i: stage_ms[i])
+    # integer-VALU roofline of the dominant kernel: k_miller (largest single
+    # kernel; it runs alone after the three concurrent per-set stages join)
+    dom = STAGES.index("miller")
     props = torch.cuda.get_device_properties(device)
     cus = props.multi_processor_count
     peak_tmacs = cus * 128 * 2.4e9 / 1e12  # v_mad_u64_u32: full rate, 4 SIMD32 per CU, 2.4 GHz max clock
@@ -217,20 +218,27 @@ def main():
         "macs_per_m": MACS_PER_M,
         "units_per_launch": units,
         "kernel_ms": stage_ms[dom],
+        "stage_tmacs": {
+            STAGES[i]: (M_PER_UNIT[STAGES[i]] * MACS_PER_M * (S + 1 if STAGES[i] == "miller" else S) / (stage_ms[i] * 1e-3) / 1e12)
+            if M_PER_UNIT.get(STAGES[i]) and stage_ms[i] > 0 else None
+            for i in range(len(STAGES))
+        },
     }
 
     # p50 latency of a 128-set batchVerify through the host C ABI (config 1 shape)
     from teku_amd import bls
 
     lat = []
+    if args.lat_reps <= 0:
+        lat = [float("nan")]
     sets128 = [(pks[48 * j : 48 * j + 48], 1, msgs[32 * j : 32 * j + 32], sigs[96 * j : 96 * j + 96]) for j in range(128)]
-    for _ in range(args.lat_reps + 3):
+    for _ in range(args.lat_reps + 3 if args.lat_reps > 0 else 0):
         rr = [secrets.randbits(64) | 1 for _ in range(128)]
         t1 = time.perf_counter()
         good = bls.batch_verify_raw(sets128, rr, n_gpus=1)
         lat.append((time.perf_counter() - t1) * 1e3)
         assert good
-    lat = sorted(lat[3:])
+    lat = sorted(lat[3:]) if args.lat_reps > 0 else lat
 
     cpu = None if args.no_cpu_baseline else cpu_baseline_oracle()
     line = {

@@ -177,33 +177,55 @@ TB_HD TB_INLINE fp fp_cneg(const fp& a, bool c) { return fp_sel(c, fp_neg(a), a)
 // ---------------------------------------------------------------------------
 // Montgomery multiplication (FIPS)
 // ---------------------------------------------------------------------------
-TB_HD TB_NOINLINE fp fp_mul(fp a, fp b) {
-  TB_COUNT_MUL();
+// Two-chain variant for a lone product: the a*b terms and the m*p reduction
+// terms of a column go to independent accumulators (halving the dependent
+// v_mad_u64_u32 chain), merged once per column.
+TB_HD TB_INLINE void mac_ab_mp(uint64_t& A, uint32_t& EA, uint64_t& M, uint32_t& EM, uint32_t a, uint32_t b, uint32_t m,
+                               uint32_t pc) {
+#if TB_DEVICE_PASS
+  uint64_t c0, c1;
+  asm("v_mad_u64_u32 %0, %4, %6, %7, %0\n\t"
+      "v_mad_u64_u32 %2, %5, %8, %9, %2\n\t"
+      "v_addc_co_u32_e64 %1, %4, %1, 0, %4\n\t"
+      "v_addc_co_u32_e64 %3, %5, %3, 0, %5"
+      : "+v"(A), "+v"(EA), "+v"(M), "+v"(EM), "=&s"(c0), "=&s"(c1)
+      : "v"(a), "v"(b), "v"(m), "s"(pc));
+#else
+  mac1(A, EA, a, b);
+  mac1(M, EM, m, pc);
+#endif
+}
+
+TB_HD TB_INLINE void acc_merge(uint64_t& A, uint32_t& EA, uint64_t& M, uint32_t& EM) {
+  uint64_t s = A + M;
+  EA += EM + (s < A ? 1u : 0u);
+  A = s;
+  M = 0;
+  EM = 0;
+}
+
+TB_HD TB_INLINE fp fp_mul_body(const fp& a, const fp& b) {
   uint32_t m[12];
   fp t;
-  uint64_t acc = 0;
-  uint32_t ext = 0;
+  uint64_t A = 0, M = 0;
+  uint32_t EA = 0, EM = 0;
   TB_UNROLL for (int k = 0; k < 12; k++) {
-    int i = 0;
-    TB_UNROLL for (; i + 1 < k; i += 2)
-      mac4s(acc, ext, a.l[i], b.l[k - i], m[i], P_MOD[k - i], a.l[i + 1], b.l[k - i - 1], m[i + 1], P_MOD[k - i - 1]);
-    TB_UNROLL for (; i < k; i++) mac2s(acc, ext, a.l[i], b.l[k - i], m[i], P_MOD[k - i]);
-    mac1(acc, ext, a.l[k], b.l[0]);
-    m[k] = (uint32_t)acc * N0;
-    mac1s(acc, ext, m[k], P_MOD[0]);
-    acc = (acc >> 32) | ((uint64_t)ext << 32);
-    ext = 0;
+    TB_UNROLL for (int i = 0; i < k; i++) mac_ab_mp(A, EA, M, EM, a.l[i], b.l[k - i], m[i], P_MOD[k - i]);
+    mac1(A, EA, a.l[k], b.l[0]);
+    acc_merge(A, EA, M, EM);
+    m[k] = (uint32_t)A * N0;
+    mac1s(A, EA, m[k], P_MOD[0]);
+    A = (A >> 32) | ((uint64_t)EA << 32);
+    EA = 0;
   }
   TB_UNROLL for (int k = 12; k < 23; k++) {
-    int i = k - 11;
-    TB_UNROLL for (; i + 1 < 12; i += 2)
-      mac4s(acc, ext, a.l[i], b.l[k - i], m[i], P_MOD[k - i], a.l[i + 1], b.l[k - i - 1], m[i + 1], P_MOD[k - i - 1]);
-    TB_UNROLL for (; i < 12; i++) mac2s(acc, ext, a.l[i], b.l[k - i], m[i], P_MOD[k - i]);
-    t.l[k - 12] = (uint32_t)acc;
-    acc = (acc >> 32) | ((uint64_t)ext << 32);
-    ext = 0;
+    TB_UNROLL for (int i = k - 11; i < 12; i++) mac_ab_mp(A, EA, M, EM, a.l[i], b.l[k - i], m[i], P_MOD[k - i]);
+    acc_merge(A, EA, M, EM);
+    t.l[k - 12] = (uint32_t)A;
+    A = (A >> 32) | ((uint64_t)EA << 32);
+    EA = 0;
   }
-  t.l[11] = (uint32_t)acc;
+  t.l[11] = (uint32_t)A;
   // t < 2p: one conditional subtraction
   fp d;
   uint32_t br = 0;
@@ -211,7 +233,123 @@ TB_HD TB_NOINLINE fp fp_mul(fp a, fp b) {
   return fp_sel(br != 0, t, d);
 }
 
+TB_HD TB_NOINLINE fp fp_mul(fp a, fp b) {
+  TB_COUNT_MUL();
+  return fp_mul_body(a, b);
+}
+
 TB_HD TB_INLINE fp fp_sqr(const fp& a) { return fp_mul(a, a); }
+
+// N independent products interleaved in program order (one accumulator chain
+// each): the ILP a lone FIPS chain lacks.  Used by fp2_mul (N=3) and fp2_sqr (N=2).
+template <int N>
+TB_HD TB_INLINE void mac_n(uint64_t (&A)[N], uint32_t (&E)[N], const uint32_t (&x)[N], const uint32_t (&y)[N]) {
+#if TB_DEVICE_PASS
+  if constexpr (N == 3) {
+    uint64_t c0, c1, c2;
+    asm("v_mad_u64_u32 %0, %6, %9, %10, %0\n\t"
+        "v_mad_u64_u32 %1, %7, %11, %12, %1\n\t"
+        "v_mad_u64_u32 %2, %8, %13, %14, %2\n\t"
+        "v_addc_co_u32_e64 %3, %6, %3, 0, %6\n\t"
+        "v_addc_co_u32_e64 %4, %7, %4, 0, %7\n\t"
+        "v_addc_co_u32_e64 %5, %8, %5, 0, %8"
+        : "+v"(A[0]), "+v"(A[1]), "+v"(A[2]), "+v"(E[0]), "+v"(E[1]), "+v"(E[2]), "=&s"(c0), "=&s"(c1), "=&s"(c2)
+        : "v"(x[0]), "v"(y[0]), "v"(x[1]), "v"(y[1]), "v"(x[2]), "v"(y[2]));
+  } else if constexpr (N == 2) {
+    uint64_t c0, c1;
+    asm("v_mad_u64_u32 %0, %4, %6, %7, %0\n\t"
+        "v_mad_u64_u32 %1, %5, %8, %9, %1\n\t"
+        "v_addc_co_u32_e64 %2, %4, %2, 0, %4\n\t"
+        "v_addc_co_u32_e64 %3, %5, %3, 0, %5"
+        : "+v"(A[0]), "+v"(A[1]), "+v"(E[0]), "+v"(E[1]), "=&s"(c0), "=&s"(c1)
+        : "v"(x[0]), "v"(y[0]), "v"(x[1]), "v"(y[1]));
+  } else {
+    TB_UNROLL for (int j = 0; j < N; j++) mac1(A[j], E[j], x[j], y[j]);
+  }
+#else
+  TB_UNROLL for (int j = 0; j < N; j++) mac1(A[j], E[j], x[j], y[j]);
+#endif
+}
+
+template <int N>
+TB_HD TB_INLINE void macs_n(uint64_t (&A)[N], uint32_t (&E)[N], const uint32_t (&x)[N], uint32_t pc) {
+#if TB_DEVICE_PASS
+  if constexpr (N == 3) {
+    uint64_t c0, c1, c2;
+    asm("v_mad_u64_u32 %0, %6, %9, %12, %0\n\t"
+        "v_mad_u64_u32 %1, %7, %10, %12, %1\n\t"
+        "v_mad_u64_u32 %2, %8, %11, %12, %2\n\t"
+        "v_addc_co_u32_e64 %3, %6, %3, 0, %6\n\t"
+        "v_addc_co_u32_e64 %4, %7, %4, 0, %7\n\t"
+        "v_addc_co_u32_e64 %5, %8, %5, 0, %8"
+        : "+v"(A[0]), "+v"(A[1]), "+v"(A[2]), "+v"(E[0]), "+v"(E[1]), "+v"(E[2]), "=&s"(c0), "=&s"(c1), "=&s"(c2)
+        : "v"(x[0]), "v"(x[1]), "v"(x[2]), "s"(pc));
+  } else if constexpr (N == 2) {
+    uint64_t c0, c1;
+    asm("v_mad_u64_u32 %0, %4, %6, %8, %0\n\t"
+        "v_mad_u64_u32 %1, %5, %7, %8, %1\n\t"
+        "v_addc_co_u32_e64 %2, %4, %2, 0, %4\n\t"
+        "v_addc_co_u32_e64 %3, %5, %3, 0, %5"
+        : "+v"(A[0]), "+v"(A[1]), "+v"(E[0]), "+v"(E[1]), "=&s"(c0), "=&s"(c1)
+        : "v"(x[0]), "v"(x[1]), "s"(pc));
+  } else {
+    TB_UNROLL for (int j = 0; j < N; j++) mac1s(A[j], E[j], x[j], pc);
+  }
+#else
+  TB_UNROLL for (int j = 0; j < N; j++) mac1(A[j], E[j], x[j], pc);
+#endif
+}
+
+// r[j] = a[j] * b[j] (Montgomery), j < N, interleaved
+template <int N>
+TB_HD TB_INLINE void fp_mul_n(fp (&r)[N], const fp (&a)[N], const fp (&b)[N]) {
+  uint32_t m[N][12];
+  uint64_t A[N];
+  uint32_t E[N];
+  TB_UNROLL for (int j = 0; j < N; j++) {
+    A[j] = 0;
+    E[j] = 0;
+  }
+  TB_UNROLL for (int k = 0; k < 23; k++) {
+    const int lo = k < 12 ? 0 : k - 11;
+    const int hi = k < 12 ? k : 11;
+    TB_UNROLL for (int i = lo; i <= hi; i++) {
+      uint32_t x[N], y[N];
+      TB_UNROLL for (int j = 0; j < N; j++) {
+        x[j] = a[j].l[i];
+        y[j] = b[j].l[k - i];
+      }
+      mac_n<N>(A, E, x, y);
+      if (i < k && i < 12 && k - i < 12 && !(k < 12 && i == k)) {
+        // reduction term m_i * p_{k-i} (i < k, both in range)
+        uint32_t xm[N];
+        TB_UNROLL for (int j = 0; j < N; j++) xm[j] = m[j][i];
+        macs_n<N>(A, E, xm, P_MOD[k - i]);
+      }
+    }
+    if (k < 12) {
+      uint32_t xm[N];
+      TB_UNROLL for (int j = 0; j < N; j++) {
+        m[j][k] = (uint32_t)A[j] * N0;
+        xm[j] = m[j][k];
+      }
+      macs_n<N>(A, E, xm, P_MOD[0]);
+    } else {
+      TB_UNROLL for (int j = 0; j < N; j++) r[j].l[k - 12] = (uint32_t)A[j];
+    }
+    TB_UNROLL for (int j = 0; j < N; j++) {
+      A[j] = (A[j] >> 32) | ((uint64_t)E[j] << 32);
+      E[j] = 0;
+    }
+  }
+  TB_UNROLL for (int j = 0; j < N; j++) {
+    r[j].l[11] = (uint32_t)A[j];
+    fp d;
+    uint32_t br = 0;
+    TB_UNROLL for (int i = 0; i < 12; i++) d.l[i] = subc32(r[j].l[i], P_MOD[i], br, &br);
+    r[j] = fp_sel(br != 0, r[j], d);
+  }
+}
 
 // multiply by small constants via additions
 TB_HD TB_INLINE fp fp_mul3(const fp& a) { return fp_add(fp_dbl(a), a); }
@@ -248,7 +386,153 @@ TB_HD TB_NOINLINE fp fp_pow(const fp& a, const uint32_t (&e)[12], int top) {
   return r;
 }
 
-TB_HD TB_INLINE fp fp_inv(const fp& a) { return fp_pow(a, E_P_MINUS_2, 380); }           // 0 -> 0
+TB_HD TB_INLINE fp fp_inv_fermat(const fp& a) { return fp_pow(a, E_P_MINUS_2, 380); }  // 0 -> 0
+
+// ---------------------------------------------------------------------------
+// Inversion by Pornin's optimized binary GCD ("Optimized Binary GCD for Modular
+// Inversion", 2020): 26 outer iterations; each runs 30 divsteps on 62-bit
+// approximations of (a, b) (low 30 bits exact + top 32 bits), accumulating a
+// 2x2 matrix with |entries| <= 2^30, then applies it to the full a, b and to
+// the Bezout coefficients u, v (mod p, with a 2^-32 word reduction).  ~65 Fp
+// multiplication-equivalents of instructions vs ~570 for Fermat; variable
+// time (verification inputs are public).  Prototype: tools/ (see DESIGN.md).
+// ---------------------------------------------------------------------------
+// out[0..12] = x*f + y*g (two's complement, 13 limbs); f, g in [-2^30, 2^30]
+TB_HD TB_INLINE void lincomb13(uint32_t (&out)[13], const uint32_t (&x)[12], int32_t f, const uint32_t (&y)[12], int32_t g) {
+  const uint32_t fa = f < 0 ? (uint32_t)(-(int64_t)f) : (uint32_t)f;
+  const uint32_t ga = g < 0 ? (uint32_t)(-(int64_t)g) : (uint32_t)g;
+  const uint32_t fm = f < 0 ? 0xffffffffu : 0u, gm = g < 0 ? 0xffffffffu : 0u;
+  uint32_t p1[13], p2[13];
+  uint64_t c1 = 0, c2 = 0;
+  TB_UNROLL for (int i = 0; i < 12; i++) {
+    c1 = (uint64_t)x[i] * fa + (c1 >> 32);
+    c2 = (uint64_t)y[i] * ga + (c2 >> 32);
+    p1[i] = (uint32_t)c1;
+    p2[i] = (uint32_t)c2;
+  }
+  p1[12] = (uint32_t)(c1 >> 32);
+  p2[12] = (uint32_t)(c2 >> 32);
+  // conditional two's complement negation: (p ^ m) + (m & 1)
+  uint32_t k1 = fm & 1u, k2 = gm & 1u, cc = 0;
+  TB_UNROLL for (int i = 0; i < 13; i++) {
+    uint32_t a1 = addc32(p1[i] ^ fm, 0, k1, &k1);
+    uint32_t a2 = addc32(p2[i] ^ gm, 0, k2, &k2);
+    out[i] = addc32(a1, a2, cc, &cc);
+  }
+}
+
+TB_HD TB_INLINE bool neg13(uint32_t (&v)[13]) {
+  const bool neg = (v[12] >> 31) != 0;
+  const uint32_t m = neg ? 0xffffffffu : 0u;
+  uint32_t k = m & 1u;
+  TB_UNROLL for (int i = 0; i < 13; i++) v[i] = addc32(v[i] ^ m, 0, k, &k);
+  return neg;
+}
+
+// (x*f + y*g) * 2^-32 mod p, x, y in [0, p)
+TB_HD TB_INLINE fp bez_update(const fp& x, int32_t f, const fp& y, int32_t g) {
+  uint32_t w[13];
+  lincomb13(w, x.l, f, y.l, g);
+  const uint32_t q = w[0] * N0;
+  // w + q*p  (w signed 13 limbs; q*p < 2^413): then drop the low word
+  uint64_t c = 0;
+  uint32_t s[14];
+  TB_UNROLL for (int i = 0; i < 12; i++) {
+    c = (uint64_t)q * P_MOD[i] + w[i] + (c >> 32);
+    s[i] = (uint32_t)c;
+  }
+  c = (uint64_t)w[12] + (c >> 32);
+  s[12] = (uint32_t)c;
+  s[13] = (uint32_t)(c >> 32) + ((w[12] >> 31) ? 0xffffffffu : 0u);  // sign extension of w
+  // r = s >> 32 is in (-2p, 2p): 13 limbs signed (s[1..13])
+  fp r;
+  TB_UNROLL for (int i = 0; i < 12; i++) r.l[i] = s[i + 1];
+  const bool neg = (s[13] >> 31) != 0;
+  // bring to [0, p): if negative add p (up to twice), else subtract p (up to twice)
+  TB_UNROLL for (int rep = 0; rep < 2; rep++) {
+    fp t;
+    uint32_t cy = 0;
+    if (neg) {
+      TB_UNROLL for (int i = 0; i < 12; i++) t.l[i] = addc32(r.l[i], P_MOD[i], cy, &cy);
+      // still negative unless the 384-bit add overflowed past the sign
+      const bool done = cy != 0 || rep == 1;
+      r = t;
+      if (done) break;
+    } else {
+      TB_UNROLL for (int i = 0; i < 12; i++) t.l[i] = subc32(r.l[i], P_MOD[i], cy, &cy);
+      if (!cy) r = t;
+    }
+  }
+  return r;
+}
+
+TB_HD TB_NOINLINE fp fp_inv(fp A) {
+  uint32_t a[12], b[12];
+  TB_UNROLL for (int i = 0; i < 12; i++) {
+    a[i] = A.l[i];
+    b[i] = P_MOD[i];
+  }
+  fp u = fp_zero(), v = fp_zero();
+  u.l[0] = 1;
+  const bool zero = fp_is_zero(A);
+  TB_NOUNROLL for (int it = 0; it < 26; it++) {
+    // n = max(bitlen(a), bitlen(b), 62); approximations: low 30 bits + bits [n-32, n)
+    uint32_t hi = 0, top = 0;
+    TB_UNROLL for (int i = 0; i < 12; i++) {
+      const uint32_t o = a[i] | b[i];
+      if (o) {
+        hi = i;
+        top = o;
+      }
+    }
+    int n = 32 * (int)hi + (top ? 32 - __builtin_clz(top) : 0);
+    if (n < 62) n = 62;
+    const int sh = n - 32, wi = sh >> 5, bo = sh & 31;
+    uint32_t a0 = 0, a1 = 0, b0 = 0, b1 = 0;
+    TB_UNROLL for (int i = 0; i < 12; i++) {
+      if (i == wi) {
+        a0 = a[i];
+        b0 = b[i];
+      }
+      if (i == wi + 1) {
+        a1 = a[i];
+        b1 = b[i];
+      }
+    }
+    const uint64_t at = ((((uint64_t)a1 << 32) | a0) >> bo) & 0xffffffffull;
+    const uint64_t bt = ((((uint64_t)b1 << 32) | b0) >> bo) & 0xffffffffull;
+    uint64_t xa = (a[0] & 0x3fffffffu) | (at << 30);
+    uint64_t xb = (b[0] & 0x3fffffffu) | (bt << 30);
+    int32_t f0 = 1, g0 = 0, f1 = 0, g1 = 1;
+    TB_UNROLL for (int j = 0; j < 30; j++) {
+      const bool odd = (xa & 1) != 0;
+      const bool sw = odd && xa < xb;
+      const uint64_t ta = sw ? xb : xa, tb = sw ? xa : xb;
+      int32_t tf0 = sw ? f1 : f0, tg0 = sw ? g1 : g0, tf1 = sw ? f0 : f1, tg1 = sw ? g0 : g1;
+      xa = odd ? ta - tb : ta;
+      xb = tb;
+      f0 = odd ? tf0 - tf1 : tf0;
+      g0 = odd ? tg0 - tg1 : tg0;
+      f1 = tf1 * 2;
+      g1 = tg1 * 2;
+      xa >>= 1;
+    }
+    uint32_t na[13], nb[13];
+    lincomb13(na, a, f0, b, g0);
+    lincomb13(nb, a, f1, b, g1);
+    const bool nega = neg13(na), negb = neg13(nb);
+    TB_UNROLL for (int i = 0; i < 12; i++) {
+      a[i] = (na[i] >> 30) | (na[i + 1] << 2);
+      b[i] = (nb[i] >> 30) | (nb[i + 1] << 2);
+    }
+    fp nu = bez_update(u, f0, v, g0);
+    fp nv = bez_update(u, f1, v, g1);
+    u = fp_cneg(nu, nega);
+    v = fp_cneg(nv, negb);
+  }
+  fp r = fp_mul(v, fp_from_const(INV_CORR));
+  return zero ? fp_zero() : r;
+}
 TB_HD TB_INLINE fp fp_sqrt_cand(const fp& a) { return fp_pow(a, E_P_PLUS_1_DIV_4, 378); }  // a^((p+1)/4)
 TB_HD TB_INLINE fp fp_pow_pm3d4(const fp& a) { return fp_pow(a, E_P_MINUS_3_DIV_4, 378); } // a^((p-3)/4)
 

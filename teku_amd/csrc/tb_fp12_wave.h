@@ -1,0 +1,196 @@
+// Wave-parallel Fp12 arithmetic for the latency-critical, once-per-batch final
+// exponentiation (BlstBLS12381.completeBatchVerify -> finalverify,
+// BlstBLS12381.java:184).  One 64-lane workgroup owns the Fp12 values, which
+// live in LDS as 12 Fp coordinates.  A multiplication is
+//   pre-combination (lane j forms its two Karatsuba operands)
+//   -> 54 independent Fp products, one per lane
+//   -> post-combination split over 48 lanes (4 partial sums per coordinate)
+// using the tables of tools/gen_fp12_wave.py, derived from the exact
+// tb_tower.h formulas.  The sequential chain per Fp12 multiply drops from 54
+// Fp multiplications to ~1 multiplication plus ~30 additions.
+#pragma once
+#include "tb_fp12_wave_tables.h"
+#include "tb_pairing.h"
+
+namespace tb {
+
+// LDS scratch for the wave ops
+struct wave12_scratch {
+  fp prod[64];
+  fp part[48];
+};
+
+__device__ TB_INLINE fp w_sparse_sum(const fp* src, const uint16_t* ent, int b, int e) {
+  fp acc = fp_zero();
+  for (int t = b; t < e; t++) {
+    const uint32_t x = ent[t];
+    const int idx = (int)(x >> 4);
+    int c = (int)(x & 15u);
+    if (c >= 8) c -= 16;
+    fp v = src[idx];
+    if (c < 0) {
+      c = -c;
+      v = fp_neg(v);
+    }
+    for (int k = 0; k < c; k++) acc = fp_add(acc, v);
+  }
+  return acc;
+}
+
+// generic bilinear op: dst = POST(prod(A x, B y)) + LIN x
+template <int NPROD>
+__device__ TB_INLINE void w_bilinear(fp* dst, const fp* x, const fp* y, wave12_scratch& s, const uint16_t* aoff,
+                                     const uint16_t* aent, const uint16_t* boff, const uint16_t* bent, const uint16_t* poff,
+                                     const uint16_t* pent, const uint16_t* loff, const uint16_t* lent) {
+  const int l = threadIdx.x;
+  if (l < NPROD) {
+    fp a = w_sparse_sum(x, aent, aoff[l], aoff[l + 1]);
+    fp b = w_sparse_sum(y, bent, boff[l], boff[l + 1]);
+    s.prod[l] = fp_mul(a, b);
+  }
+  __syncthreads();
+  if (l < 48) {
+    const int i = l >> 2, q = l & 3;
+    const int b0 = poff[i], e0 = poff[i + 1];
+    const int chunk = (e0 - b0 + 3) >> 2;
+    int lo = b0 + q * chunk, hi = lo + chunk;
+    if (hi > e0) hi = e0;
+    if (lo > e0) lo = e0;
+    s.part[l] = w_sparse_sum(s.prod, pent, lo, hi);
+  }
+  __syncthreads();
+  fp r;
+  if (l < 12) {
+    r = fp_add(fp_add(s.part[4 * l], s.part[4 * l + 1]), fp_add(s.part[4 * l + 2], s.part[4 * l + 3]));
+    r = fp_add(r, w_sparse_sum(x, lent, loff[l], loff[l + 1]));
+  }
+  __syncthreads();
+  if (l < 12) dst[l] = r;
+  __syncthreads();
+}
+
+__device__ TB_INLINE void w_mul(fp* dst, const fp* x, const fp* y, wave12_scratch& s) {
+  w_bilinear<W12M_NPROD>(dst, x, y, s, W12M_A_OFF, W12M_A_ENT, W12M_B_OFF, W12M_B_ENT, W12M_POST_OFF, W12M_POST_ENT, W12M_LIN_OFF,
+                         W12M_LIN_ENT);
+}
+
+__device__ TB_INLINE void w_cyc_sqr(fp* dst, const fp* x, wave12_scratch& s) {
+  w_bilinear<W12C_NPROD>(dst, x, x, s, W12C_A_OFF, W12C_A_ENT, W12C_B_OFF, W12C_B_ENT, W12C_POST_OFF, W12C_POST_ENT, W12C_LIN_OFF,
+                         W12C_LIN_ENT);
+}
+
+__device__ TB_INLINE void w_copy(fp* dst, const fp* x) {
+  const int l = threadIdx.x;
+  fp v;
+  if (l < 12) v = x[l];
+  __syncthreads();
+  if (l < 12) dst[l] = v;
+  __syncthreads();
+}
+
+__device__ TB_INLINE void w_conj(fp* dst, const fp* x) {
+  const int l = threadIdx.x;
+  fp v;
+  if (l < 12) v = l >= 6 ? fp_neg(x[l]) : x[l];
+  __syncthreads();
+  if (l < 12) dst[l] = v;
+  __syncthreads();
+}
+
+// Frobenius: Fp2 coefficient at coordinates (2j, 2j+1); its w-power is
+// j = 0,1,2 -> w^0, w^2, w^4 ; j = 3,4,5 -> w^1, w^3, w^5
+__device__ TB_INLINE void w_frob(fp* dst, const fp* x) {
+  const int l = threadIdx.x;
+  fp2 v;
+  if (l < 6) {
+    fp2 c = {x[2 * l], fp_neg(x[2 * l + 1])};
+    const int wp = l < 3 ? 2 * l : 2 * (l - 3) + 1;
+    switch (wp) {
+      case 1: c = fp2_mul(c, fp2_from_const(FROB_G1)); break;
+      case 2: c = fp2_mul(c, fp2_from_const(FROB_G2)); break;
+      case 3: c = fp2_mul(c, fp2_from_const(FROB_G3)); break;
+      case 4: c = fp2_mul(c, fp2_from_const(FROB_G4)); break;
+      case 5: c = fp2_mul(c, fp2_from_const(FROB_G5)); break;
+      default: break;
+    }
+    v = c;
+  }
+  __syncthreads();
+  if (l < 6) {
+    dst[2 * l] = v.c0;
+    dst[2 * l + 1] = v.c1;
+  }
+  __syncthreads();
+}
+
+__device__ TB_INLINE void fp12_to_coords(fp* dst, const fp12& a) {
+  const fp2* c[6] = {&a.c0.c0, &a.c0.c1, &a.c0.c2, &a.c1.c0, &a.c1.c1, &a.c1.c2};
+  for (int j = 0; j < 6; j++) {
+    dst[2 * j] = c[j]->c0;
+    dst[2 * j + 1] = c[j]->c1;
+  }
+}
+
+__device__ TB_INLINE fp12 fp12_from_coords(const fp* s) {
+  fp12 a;
+  a.c0.c0 = {s[0], s[1]};
+  a.c0.c1 = {s[2], s[3]};
+  a.c0.c2 = {s[4], s[5]};
+  a.c1.c0 = {s[6], s[7]};
+  a.c1.c1 = {s[8], s[9]};
+  a.c1.c2 = {s[10], s[11]};
+  return a;
+}
+
+// dst = conj(src^|x|) = src^x for src in the cyclotomic subgroup (dst != src)
+__device__ TB_INLINE void w_cyc_exp_x(fp* dst, const fp* src, wave12_scratch& s) {
+  w_copy(dst, src);
+  for (int i = 62; i >= 0; --i) {
+    w_cyc_sqr(dst, dst, s);
+    if ((X_ABS >> i) & 1) w_mul(dst, dst, src, s);
+  }
+  w_conj(dst, dst);
+}
+
+struct final_exp_lds {
+  fp F[12], T[12], A[12], B[12], C[12], E[12], X[12], Y[12];
+  wave12_scratch s;
+};
+
+// result = final_exp(F) via the same chain as tb_pairing.h final_exp; whole block (64 lanes) participates.
+__device__ TB_INLINE void final_exp_wave(final_exp_lds& L) {
+  const int l = threadIdx.x;
+  // easy part: t = conj(f) / f  (the inversion runs on lane 0)
+  if (l == 0) {
+    fp12 inv = fp12_inv(fp12_from_coords(L.F));
+    fp12_to_coords(L.X, inv);
+  }
+  __syncthreads();
+  w_conj(L.Y, L.F);
+  w_mul(L.T, L.Y, L.X, L.s);
+  w_frob(L.X, L.T);
+  w_frob(L.X, L.X);
+  w_mul(L.T, L.X, L.T, L.s);  // t = f^((p^6-1)(p^2+1))
+  // hard part (x3)
+  w_cyc_exp_x(L.E, L.T, L.s);
+  w_conj(L.X, L.T);
+  w_mul(L.A, L.E, L.X, L.s);  // a = t^(x-1)
+  w_cyc_exp_x(L.E, L.A, L.s);
+  w_conj(L.X, L.A);
+  w_mul(L.A, L.E, L.X, L.s);  // a = t^((x-1)^2)
+  w_cyc_exp_x(L.E, L.A, L.s);
+  w_frob(L.X, L.A);
+  w_mul(L.B, L.E, L.X, L.s);  // b = a^(x+p)
+  w_cyc_exp_x(L.E, L.B, L.s);
+  w_cyc_exp_x(L.C, L.E, L.s);
+  w_frob(L.X, L.B);
+  w_frob(L.X, L.X);
+  w_mul(L.C, L.C, L.X, L.s);
+  w_conj(L.X, L.B);
+  w_mul(L.C, L.C, L.X, L.s);  // c = b^(x^2+p^2-1)
+  w_cyc_sqr(L.X, L.T, L.s);
+  w_mul(L.X, L.X, L.T, L.s);  // t^3
+  w_mul(L.F, L.C, L.X, L.s);
+}
+
+}  // namespace tb

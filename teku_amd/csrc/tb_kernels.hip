@@ -18,6 +18,7 @@
 // in LDS, then one block over the block partials).
 #include "tb_stages.h"
 #include "tb_testops.h"
+#include "tb_fp12_wave.h"
 
 using namespace tb;
 
@@ -184,7 +185,26 @@ extern "C" __global__ void __launch_bounds__(TB_BLOCK)
   if (threadIdx.x == 0) part[blockIdx.x] = acc;
 }
 
-// result[0] = 1 iff no set is invalid and final_exp(prod f) == 1
+// result[0] = 1 iff no set is invalid and final_exp(prod f) == 1 (one 64-lane wave)
+extern "C" __global__ void __launch_bounds__(64) k_final_verify_wave(const fp12* __restrict__ f, const uint32_t* __restrict__ n_bad,
+                                                                     int* __restrict__ result) {
+  __shared__ final_exp_lds L;
+  if (threadIdx.x == 0) fp12_to_coords(L.F, f[0]);
+  __syncthreads();
+  final_exp_wave(L);
+  if (threadIdx.x == 0) result[0] = (n_bad[0] == 0 && fp12_is_one(fp12_from_coords(L.F))) ? 1 : 0;
+}
+
+// test hook: one final exponentiation per 64-lane block (tb_testops.h record layout)
+extern "C" __global__ void __launch_bounds__(64) k_test_final_exp_wave(const uint8_t* in, uint8_t* out) {
+  __shared__ final_exp_lds L;
+  if (threadIdx.x == 0) fp12_to_coords(L.F, tio_fp12(in + (size_t)blockIdx.x * TB_TEST_IN));
+  __syncthreads();
+  final_exp_wave(L);
+  if (threadIdx.x == 0) tio_put_fp12(out + (size_t)blockIdx.x * TB_TEST_OUT, fp12_from_coords(L.F));
+}
+
+// single-lane reference version (kept for A/B timing)
 extern "C" __global__ void k_final_verify(const fp12* __restrict__ f, const uint32_t* __restrict__ n_bad, int* __restrict__ result) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   fp12 g = final_exp(f[0]);

@@ -73,6 +73,8 @@ struct dev_ctx {
   dbuf in, ws;  // device input staging, pipeline workspace
   dbuf fin;     // final-exponentiation scratch
   dbuf dstb;    // default DST for the device-resident API
+  hipStream_t aux[2] = {nullptr, nullptr};  // concurrent per-set stages
+  hipEvent_t e_fork = nullptr, e_join[2] = {nullptr, nullptr};
   hbuf hin, hout;
 };
 
@@ -117,51 +119,69 @@ struct ws_layout {
 // Launch the partial pipeline for one device.  All pointers in `b` are
 // device pointers.  Writes the 580-byte partial record at `partial_out`.
 // Optionally leaves per-set codes in the workspace (set_code/sig_code).
-// stage events (optional): 0 start, 1 after k_pk_decompress, 2 after k_set_pk,
-// 3 after k_set_sig, 4 after k_set_hash, 5 after the G2 sum, 6 after k_miller,
-// 7 after the Fp12 product
-#define TB_NSTAGE_EV 8
+// Per-stage timing (optional): ev[2*i] / ev[2*i+1] bracket stage i on the
+// stream that runs it.  Stages: 0 pk decompress, 1 set pk, 2 set sig, 3 set
+// hash, 4 G2 sum, 5 Miller, 6 Fp12 product.
+#define TB_NSTAGE 7
+#define TB_NSTAGE_EV (2 * TB_NSTAGE)
+// The three per-set stages are independent (keys / signatures / messages), so
+// they run concurrently on three streams forked from the caller's stream `s`
+// and joined before the Miller loops.
 int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* partial_out, ws_layout& L,
                    const uint8_t* dst, uint32_t dlen, bool keep_codes, hipEvent_t* ev = nullptr) {
   const uint32_t n = b.n, K = b.n_keys;
   L = ws_layout(n, K);
   if (c.ws.ensure(L.total)) return TBLS_DEVICE_ERROR;
   uint8_t* w = c.ws.as<uint8_t>();
+  (void)keep_codes;
+  hipStream_t sa = c.aux[0], sb = c.aux[1];
+#define TB_EV(i, st) \
+  if (ev) HIPCHK(hipEventRecord(ev[i], st))
   HIPCHK(hipMemsetAsync(w + L.set_code, 0, n ? n : 1, s));
   HIPCHK(hipMemsetAsync(w + L.n_bad, 0, 4, s));
-  (void)keep_codes;
-#define TB_EV(i) \
-  if (ev) HIPCHK(hipEventRecord(ev[i], s))
+  HIPCHK(hipEventRecord(c.e_fork, s));
+  HIPCHK(hipStreamWaitEvent(sa, c.e_fork, 0));
+  HIPCHK(hipStreamWaitEvent(sb, c.e_fork, 0));
   const dim3 blk(TB_BLOCK);
-  TB_EV(0);
+  const dim3 g((n + TB_BLOCK - 1) / TB_BLOCK);
+  // stream a: hash_to_G2 per set
+  TB_EV(6, sa);
+  if (n) hipLaunchKernelGGL(k_set_hash, g, blk, 0, sa, b.msgs, b.msg_off, dst, dlen, n, (g2a*)(w + L.Q), w + L.skip);
+  TB_EV(7, sa);
+  HIPCHK(hipEventRecord(c.e_join[0], sa));
+  // stream b: signatures, then the G2 sum
+  TB_EV(4, sb);
+  if (n) hipLaunchKernelGGL(k_set_sig, g, blk, 0, sb, b.sigs, b.rand, n, (g2j*)(w + L.rsig), w + L.sig_code, (uint32_t*)(w + L.n_bad));
+  TB_EV(5, sb);
+  TB_EV(8, sb);
+  if (n)
+    hipLaunchKernelGGL(k_g2_sum_partial, dim3(L.nb_g2), blk, 0, sb, (const g2j*)(w + L.rsig), n, (g2j*)(w + L.gpart));
+  else
+    HIPCHK(hipMemsetAsync(w + L.gpart, 0, sizeof(g2j), sb));  // z = 0 -> infinity
+  hipLaunchKernelGGL(k_g2_sum_final, dim3(1), blk, 0, sb, (const g2j*)(w + L.gpart), L.nb_g2, n, (g1a*)(w + L.P), (g2a*)(w + L.Q),
+                     w + L.skip);
+  TB_EV(9, sb);
+  HIPCHK(hipEventRecord(c.e_join[1], sb));
+  // caller's stream: public keys
+  TB_EV(0, s);
   if (K) hipLaunchKernelGGL(k_pk_decompress, dim3((K + TB_BLOCK - 1) / TB_BLOCK), blk, 0, s, b.pks, K, (g1a*)(w + L.pk_aff), w + L.pk_code);
-  TB_EV(1);
-  if (n) {
-    const dim3 g((n + TB_BLOCK - 1) / TB_BLOCK);
+  TB_EV(1, s);
+  TB_EV(2, s);
+  if (n)
     hipLaunchKernelGGL(k_set_pk, g, blk, 0, s, b.pk_off, (const g1a*)(w + L.pk_aff), w + L.pk_code, b.rand, n, (g1a*)(w + L.P),
                        w + L.set_code, (uint32_t*)(w + L.n_bad));
-    TB_EV(2);
-    hipLaunchKernelGGL(k_set_sig, g, blk, 0, s, b.sigs, b.rand, n, (g2j*)(w + L.rsig), w + L.sig_code, (uint32_t*)(w + L.n_bad));
-    TB_EV(3);
-    hipLaunchKernelGGL(k_set_hash, g, blk, 0, s, b.msgs, b.msg_off, dst, dlen, n, (g2a*)(w + L.Q), w + L.skip);
-    TB_EV(4);
-    hipLaunchKernelGGL(k_g2_sum_partial, dim3(L.nb_g2), blk, 0, s, (const g2j*)(w + L.rsig), n, (g2j*)(w + L.gpart));
-  } else {
-    HIPCHK(hipMemsetAsync(w + L.gpart, 0, sizeof(g2j), s));  // z = 0 -> infinity
-    TB_EV(2);
-    TB_EV(3);
-    TB_EV(4);
-  }
-  hipLaunchKernelGGL(k_g2_sum_final, dim3(1), blk, 0, s, (const g2j*)(w + L.gpart), L.nb_g2, n, (g1a*)(w + L.P), (g2a*)(w + L.Q),
-                     w + L.skip);
-  TB_EV(5);
+  TB_EV(3, s);
+  HIPCHK(hipStreamWaitEvent(s, c.e_join[0], 0));
+  HIPCHK(hipStreamWaitEvent(s, c.e_join[1], 0));
   const uint32_t np = n + 1;
+  TB_EV(10, s);
   hipLaunchKernelGGL(k_miller, dim3((np + TB_BLOCK - 1) / TB_BLOCK), blk, 0, s, (const g1a*)(w + L.P), (const g2a*)(w + L.Q),
                      w + L.skip, w + L.set_code, w + L.sig_code, n, np, (fp12*)(w + L.f));
-  TB_EV(6);
+  TB_EV(11, s);
+  TB_EV(12, s);
   hipLaunchKernelGGL(k_fp12_prod, dim3(L.nb_f), blk, 0, s, (const fp12*)(w + L.f), np, (fp12*)(w + L.fpart));
   hipLaunchKernelGGL(k_fp12_prod, dim3(1), blk, 0, s, (const fp12*)(w + L.fpart), L.nb_f, (fp12*)partial_out);
-  TB_EV(7);
+  TB_EV(13, s);
   HIPCHK(hipMemcpyAsync((uint8_t*)partial_out + sizeof(fp12), w + L.n_bad, 4, hipMemcpyDeviceToDevice, s));
   HIPCHK(hipGetLastError());
   return TBLS_SUCCESS;
@@ -188,7 +208,7 @@ int launch_final(dev_ctx& c, const void* recs, uint32_t g, hipStream_t s, int* r
   int* res = (int*)(nbad + 1);
   hipLaunchKernelGGL(k_gather_partials, dim3(1), dim3(64), 0, s, (const uint8_t*)recs, g, f, nbad);
   hipLaunchKernelGGL(k_fp12_prod, dim3(1), dim3(TB_BLOCK), 0, s, (const fp12*)f, g, prod);
-  hipLaunchKernelGGL(k_final_verify, dim3(1), dim3(64), 0, s, (const fp12*)prod, (const uint32_t*)nbad, res);
+  hipLaunchKernelGGL(k_final_verify_wave, dim3(1), dim3(64), 0, s, (const fp12*)prod, (const uint32_t*)nbad, res);
   HIPCHK(hipGetLastError());
   if (c.hout.ensure(16)) return TBLS_DEVICE_ERROR;
   HIPCHK(hipMemcpyAsync(c.hout.p, res, 4, hipMemcpyDeviceToHost, s));
@@ -400,7 +420,12 @@ extern "C" int tbls_init(int n_devices, uint32_t flags) {
   for (int d = 0; d < count; d++) {
     dev_ctx* c = new dev_ctx();
     c->dev = d;
-    if (hipSetDevice(d) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    if (hipSetDevice(d) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->aux[0], hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->aux[1], hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&c->e_fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->e_join[0], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->e_join[1], hipEventDisableTiming) != hipSuccess) {
       delete c;
       break;
     }
@@ -421,6 +446,11 @@ extern "C" void tbls_shutdown(void) {
     if (c->hin.p) (void)hipHostFree(c->hin.p);
     if (c->hout.p) (void)hipHostFree(c->hout.p);
     if (c->stream) (void)hipStreamDestroy(c->stream);
+    for (int i = 0; i < 2; i++)
+      if (c->aux[i]) (void)hipStreamDestroy(c->aux[i]);
+    if (c->e_fork) (void)hipEventDestroy(c->e_fork);
+    for (int i = 0; i < 2; i++)
+      if (c->e_join[i]) (void)hipEventDestroy(c->e_join[i]);
     delete c;
   }
   g_ctx.clear();
@@ -694,9 +724,11 @@ extern "C" int tbls_dev_batch_partial_timed(int device, const tbls_dev_batch* b,
   int rc = launch_partial(*c, *b, s, partial_out, L, c->dstb.as<uint8_t>(), 43, false, ev);
   if (!rc) {
     HIPCHK(hipEventSynchronize(ev[TB_NSTAGE_EV - 1]));
-    for (int i = 0; i + 1 < TB_NSTAGE_EV; i++) {
+    static const int order[TB_NSTAGE] = {0, 1, 2, 3, 4, 5, 6};  // pk, set_pk, set_sig, set_hash, g2_sum, miller, prod
+    const int evi[TB_NSTAGE] = {0, 2, 4, 6, 8, 10, 12};
+    for (int i = 0; i < TB_NSTAGE; i++) {
       float ms = 0;
-      (void)hipEventElapsedTime(&ms, ev[i], ev[i + 1]);
+      (void)hipEventElapsedTime(&ms, ev[evi[order[i]]], ev[evi[order[i]] + 1]);
       stage_ms[i] = ms;
     }
   }
@@ -754,6 +786,10 @@ extern "C" int tbls_test_ops(int op, const uint8_t* in, uint8_t* out, size_t n) 
     if (c.in.ensure(n * TB_TEST_IN + 256) || c.ws.ensure(n * TB_TEST_OUT + 256)) return (int)TBLS_DEVICE_ERROR;
     HIPCHK(hipMemcpyAsync(c.in.p, in, n * TB_TEST_IN, hipMemcpyHostToDevice, c.stream));
     HIPCHK(hipMemsetAsync(c.ws.p, 0, n * TB_TEST_OUT, c.stream));
+    if (op == 29) {  // TOP_FINAL_EXP_WAVE: one 64-lane block per record
+      hipLaunchKernelGGL(k_test_final_exp_wave, dim3(n), dim3(64), 0, c.stream, c.in.as<uint8_t>(), c.ws.as<uint8_t>());
+      return fetch(c, out, c.ws.p, n * TB_TEST_OUT);
+    }
     hipLaunchKernelGGL(k_test_ops, dim3((n + TB_BLOCK - 1) / TB_BLOCK), dim3(TB_BLOCK), 0, c.stream, op, c.in.as<uint8_t>(), c.ws.as<uint8_t>(),
                        (uint32_t)n);
     return fetch(c, out, c.ws.p, n * TB_TEST_OUT);

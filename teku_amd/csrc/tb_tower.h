@@ -33,16 +33,27 @@ TB_HD TB_INLINE fp2 fp2_mul_fp(const fp2& a, const fp& b) { return {fp_mul(a.c0,
 TB_HD TB_INLINE fp2 fp2_mul3(const fp2& a) { return {fp_mul3(a.c0), fp_mul3(a.c1)}; }
 TB_HD TB_INLINE fp2 fp2_half(const fp2& a) { return {fp_half(a.c0), fp_half(a.c1)}; }
 
-TB_HD TB_INLINE fp2 fp2_mul(const fp2& a, const fp2& b) {
-  fp t0 = fp_mul(a.c0, b.c0);
-  fp t1 = fp_mul(a.c1, b.c1);
-  fp t2 = fp_mul(fp_add(a.c0, a.c1), fp_add(b.c0, b.c1));
-  return {fp_sub(t0, t1), fp_sub(fp_sub(t2, t0), t1)};
+// Karatsuba: the three Fp products are independent and run interleaved in one call
+TB_HD TB_NOINLINE fp2 fp2_mul(fp2 a, fp2 b) {
+#if !TB_DEVICE_PASS && defined(TB_COUNT_MULS)
+  tb_mul_count += 3;
+#endif
+  fp t[3];
+  const fp x[3] = {a.c0, a.c1, fp_add(a.c0, a.c1)};
+  const fp y[3] = {b.c0, b.c1, fp_add(b.c0, b.c1)};
+  fp_mul_n<3>(t, x, y);
+  return {fp_sub(t[0], t[1]), fp_sub(fp_sub(t[2], t[0]), t[1])};
 }
 
-TB_HD TB_INLINE fp2 fp2_sqr(const fp2& a) {
-  fp t = fp_mul(a.c0, a.c1);
-  return {fp_mul(fp_add(a.c0, a.c1), fp_sub(a.c0, a.c1)), fp_dbl(t)};
+TB_HD TB_NOINLINE fp2 fp2_sqr(fp2 a) {
+#if !TB_DEVICE_PASS && defined(TB_COUNT_MULS)
+  tb_mul_count += 2;
+#endif
+  fp t[2];
+  const fp x[2] = {a.c0, fp_add(a.c0, a.c1)};
+  const fp y[2] = {a.c1, fp_sub(a.c0, a.c1)};
+  fp_mul_n<2>(t, x, y);
+  return {t[1], fp_dbl(t[0])};
 }
 
 // multiply by xi = 1 + u

@@ -11,7 +11,7 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libtekubls_hip.so")
+LIB_PATH = os.environ.get("TBLS_LIB") or os.path.join(_HERE, "lib", "libtekubls_hip.so")
 
 SUCCESS = 0
 BAD_ENCODING = 1

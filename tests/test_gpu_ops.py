@@ -119,3 +119,9 @@ def test_pairing_pieces(run):
     g = dec_fp12(run("FINAL_EXP", [enc_fp12(f)])[0])
     e = O.pairing(P1, Q1)
     assert g == O.f12_mul(O.f12_mul(e, e), e)
+    # wave-parallel final exponentiation == single-lane version, bit for bit
+    rng = _rng()
+    fs = [f] + [tuple(tuple((rng.randrange(O.P), rng.randrange(O.P)) for _ in range(3)) for _ in range(2)) for _ in range(2)]
+    single = [dec_fp12(x) for x in run("FINAL_EXP", [enc_fp12(x) for x in fs])]
+    wave = [dec_fp12(x) for x in run("FINAL_EXP_WAVE", [enc_fp12(x) for x in fs])]
+    assert wave == single
