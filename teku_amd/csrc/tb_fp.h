@@ -1,12 +1,12 @@
-// Fp: the BLS12-381 base field, 381-bit modulus, on 12 x 32-bit limbs in
-// Montgomery form (R = 2^384), always fully reduced to [0, p).
+// Fp: the BLS12-381 base field, 381-bit modulus.  Elements are stored on
+// 12 x 32-bit limbs in Montgomery form with R = 2^406 and are WEAKLY reduced:
+// every operation returns a value in [0, 2p) (fp_canon gives [0, p)).
+// Equality / zero tests and encodings canonicalize; everything else works on
+// the redundant form.
 //
-// Multiplication is the finely-integrated product-scanning (FIPS) Montgomery
-// method: each output column is accumulated in a 64-bit register pair with
-// v_mad_u64_u32 whose carry-out (SDST) is folded into a third word with
-// v_addc_co_u32.  Two instructions per 32x32 MAC, no per-MAC carry chain across
-// limbs.  On gfx950 v_mad_u64_u32 issues at the full VALU rate (measured,
-// tools/microbench/int_rates.hip), so instruction count is the cost model.
+// Multiplication converts to 14 x 29-bit limbs and runs product-scanning
+// Montgomery with one v_mad_u64_u32 per multiply-accumulate (see the core
+// below); additions use the 32-bit hardware carry chain.
 #pragma once
 #include "tb_common.h"
 #include "tb_consts.h"
@@ -25,70 +25,137 @@ extern "C" unsigned long long tb_mul_count;  // host instrumentation (tools/coun
 #endif
 
 // ---------------------------------------------------------------------------
-// multiply-accumulate primitives: (ext:acc) += a*b [+ c*d ...]
+// Radix-2^29 Montgomery core (R = 2^406)
+//
+// Storage stays 12 x 32-bit (cheap add/sub with the hardware carry chain), but
+// a product is formed on 14 x 29-bit limbs: every column of a x b plus m x p
+// holds <= 28 products < 2^58, so it fits ONE 64-bit accumulator and every
+// multiply-accumulate is a single v_mad_u64_u32 (no carry word, no SGPR carry
+// hazard).  Measured on MI355X (tools/microbench/fp_rates.hip): 78 G mul/s
+// (3 interleaved products) vs 61 G mul/s for 12 x 32 product scanning.
+// Inputs may be any values < 2^393 (several multiples of p); the output is
+// < 2p, so results stay "weakly reduced" in [0, 2p) without a final
+// conditional subtraction.
 // ---------------------------------------------------------------------------
-TB_HD TB_INLINE void mac1(uint64_t& acc, uint32_t& ext, uint32_t a, uint32_t b) {
-#if TB_DEVICE_PASS
-  uint64_t c;
-  asm("v_mad_u64_u32 %0, %2, %3, %4, %0\n\t"
-      "v_addc_co_u32_e64 %1, %2, %1, 0, %2"
-      : "+v"(acc), "+v"(ext), "=&s"(c)
-      : "v"(a), "v"(b));
-#else
-  unsigned __int128 s = (unsigned __int128)acc + (uint64_t)a * b;
-  acc = (uint64_t)s;
-  ext += (uint32_t)(s >> 64);
-#endif
+TB_CONST uint32_t M29 = 0x1fffffffu;
+
+TB_HD TB_INLINE void to29(uint32_t (&x)[14], const fp& a) {
+  TB_UNROLL for (int i = 0; i < 14; i++) {
+    const int o = 29 * i, w = o >> 5, s = o & 31;
+    uint32_t v = a.l[w] >> s;
+    if (s + 29 > 32 && w + 1 < 12) v |= a.l[w + 1] << (32 - s);
+    x[i] = v & M29;
+  }
 }
 
-// two products, the second with a scalar (SGPR) constant operand
-TB_HD TB_INLINE void mac2s(uint64_t& acc, uint32_t& ext, uint32_t a, uint32_t b, uint32_t m, uint32_t pc) {
-#if TB_DEVICE_PASS
-  uint64_t c;
-  asm("v_mad_u64_u32 %0, %2, %3, %4, %0\n\t"
-      "v_addc_co_u32_e64 %1, %2, %1, 0, %2\n\t"
-      "v_mad_u64_u32 %0, %2, %5, %6, %0\n\t"
-      "v_addc_co_u32_e64 %1, %2, %1, 0, %2"
-      : "+v"(acc), "+v"(ext), "=&s"(c)
-      : "v"(a), "v"(b), "v"(m), "s"(pc));
-#else
-  mac1(acc, ext, a, b);
-  mac1(acc, ext, m, pc);
-#endif
+// 14 normalized limbs (value < 2^384) -> 12 words
+TB_HD TB_INLINE void from29(fp& r, const uint32_t (&x)[14]) {
+  TB_UNROLL for (int j = 0; j < 12; j++) {
+    const int i = (32 * j) / 29, s = 32 * j - 29 * i;
+    uint32_t v = x[i] >> s;
+    if (i + 1 < 14) v |= x[i + 1] << (29 - s);
+    if (s > 26 && i + 2 < 14) v |= x[i + 2] << (58 - s);
+    r.l[j] = v;
+  }
 }
 
-TB_HD TB_INLINE void mac4s(uint64_t& acc, uint32_t& ext, uint32_t a0, uint32_t b0, uint32_t m0, uint32_t p0,
-                           uint32_t a1, uint32_t b1, uint32_t m1, uint32_t p1) {
-#if TB_DEVICE_PASS
-  uint64_t c;
-  asm("v_mad_u64_u32 %0, %2, %3, %4, %0\n\t"
-      "v_addc_co_u32_e64 %1, %2, %1, 0, %2\n\t"
-      "v_mad_u64_u32 %0, %2, %5, %6, %0\n\t"
-      "v_addc_co_u32_e64 %1, %2, %1, 0, %2\n\t"
-      "v_mad_u64_u32 %0, %2, %7, %8, %0\n\t"
-      "v_addc_co_u32_e64 %1, %2, %1, 0, %2\n\t"
-      "v_mad_u64_u32 %0, %2, %9, %10, %0\n\t"
-      "v_addc_co_u32_e64 %1, %2, %1, 0, %2"
-      : "+v"(acc), "+v"(ext), "=&s"(c)
-      : "v"(a0), "v"(b0), "v"(m0), "s"(p0), "v"(a1), "v"(b1), "v"(m1), "s"(p1));
-#else
-  mac2s(acc, ext, a0, b0, m0, p0);
-  mac2s(acc, ext, a1, b1, m1, p1);
-#endif
+TB_HD TB_INLINE void mad29(uint64_t& acc, uint32_t a, uint32_t b) { acc += (uint64_t)a * b; }
+
+// N independent Montgomery products r[j] = a[j] b[j] / 2^406 (mod p), interleaved
+// column by column.  N == 1 splits a column over two accumulators (a x b and
+// m x p) for instruction-level parallelism inside the lone product.
+template <int N, bool SQR>
+TB_HD TB_INLINE void mont29(uint32_t (&r)[N][14], const uint32_t (&a)[N][14], const uint32_t (&b)[N][14]) {
+  uint64_t A[N], M[N];
+  uint32_t m[N][14];
+  uint32_t a2[N][14];
+  if (SQR) {
+    TB_UNROLL for (int j = 0; j < N; j++) TB_UNROLL for (int i = 0; i < 14; i++) a2[j][i] = a[j][i] << 1;
+  }
+  TB_UNROLL for (int j = 0; j < N; j++) {
+    A[j] = 0;
+    M[j] = 0;
+  }
+  TB_UNROLL for (int k = 0; k < 27; k++) {
+    const int lo = k < 14 ? 0 : k - 13;
+    const int hi = k < 14 ? k : 13;
+    if (SQR) {
+      // 2 a_i a_{k-i} for i < k - i, plus a_{k/2}^2
+      TB_UNROLL for (int i = lo; i <= hi; i++) {
+        if (i < k - i) {
+          TB_UNROLL for (int j = 0; j < N; j++) mad29(A[j], a2[j][i], a[j][k - i]);
+        } else if (i == k - i) {
+          TB_UNROLL for (int j = 0; j < N; j++) mad29(A[j], a[j][i], a[j][i]);
+        }
+      }
+    } else {
+      TB_UNROLL for (int i = lo; i <= hi; i++) TB_UNROLL for (int j = 0; j < N; j++) mad29(A[j], a[j][i], b[j][k - i]);
+    }
+    const int mhi = k < 14 ? k - 1 : 13;  // m_k is formed at the end of column k
+    TB_UNROLL for (int i = lo; i <= mhi; i++) {
+      TB_UNROLL for (int j = 0; j < N; j++) {
+        if (N == 1)
+          mad29(M[j], m[j][i], P29[k - i]);
+        else
+          mad29(A[j], m[j][i], P29[k - i]);
+      }
+    }
+    if (N == 1) {
+      A[0] += M[0];
+      M[0] = 0;
+    }
+    if (k < 14) {
+      TB_UNROLL for (int j = 0; j < N; j++) {
+        m[j][k] = ((uint32_t)A[j] * N0_29) & M29;
+        mad29(A[j], m[j][k], P29[0]);
+      }
+    } else {
+      TB_UNROLL for (int j = 0; j < N; j++) r[j][k - 14] = (uint32_t)A[j] & M29;
+    }
+    TB_UNROLL for (int j = 0; j < N; j++) A[j] >>= 29;
+  }
+  TB_UNROLL for (int j = 0; j < N; j++) r[j][13] = (uint32_t)A[j];
 }
 
-TB_HD TB_INLINE void mac1s(uint64_t& acc, uint32_t& ext, uint32_t m, uint32_t pc) {
-#if TB_DEVICE_PASS
-  uint64_t c;
-  asm("v_mad_u64_u32 %0, %2, %3, %4, %0\n\t"
-      "v_addc_co_u32_e64 %1, %2, %1, 0, %2"
-      : "+v"(acc), "+v"(ext), "=&s"(c)
-      : "v"(m), "s"(pc));
-#else
-  mac1(acc, ext, m, pc);
-#endif
+// r[j] = a[j] * b[j] (Montgomery), j < N, interleaved
+template <int N>
+TB_HD TB_INLINE void fp_mul_n(fp (&r)[N], const fp (&a)[N], const fp (&b)[N]) {
+  uint32_t x[N][14], y[N][14], z[N][14];
+  TB_UNROLL for (int j = 0; j < N; j++) {
+    to29(x[j], a[j]);
+    to29(y[j], b[j]);
+  }
+  mont29<N, false>(z, x, y);
+  TB_UNROLL for (int j = 0; j < N; j++) from29(r[j], z[j]);
 }
 
+template <int N>
+TB_HD TB_INLINE void fp_sqr_n(fp (&r)[N], const fp (&a)[N]) {
+  uint32_t x[N][14], z[N][14];
+  TB_UNROLL for (int j = 0; j < N; j++) to29(x[j], a[j]);
+  mont29<N, true>(z, x, x);
+  TB_UNROLL for (int j = 0; j < N; j++) from29(r[j], z[j]);
+}
+
+TB_HD TB_NOINLINE fp fp_mul(fp a, fp b) {
+  TB_COUNT_MUL();
+  fp r[1];
+  const fp x[1] = {a}, y[1] = {b};
+  fp_mul_n<1>(r, x, y);
+  return r[0];
+}
+
+TB_HD TB_NOINLINE fp fp_sqr(fp a) {
+  TB_COUNT_MUL();
+  fp r[1];
+  const fp x[1] = {a};
+  fp_sqr_n<1>(r, x);
+  return r[0];
+}
+
+// ---------------------------------------------------------------------------
+// addition-type ops on [0, 2p) values (12-limb hardware carry chains)
+// ---------------------------------------------------------------------------
 TB_HD TB_INLINE uint32_t addc32(uint32_t a, uint32_t b, uint32_t cin, uint32_t* cout) {
 #if defined(__clang__)
   return __builtin_addc(a, b, cin, cout);
@@ -109,9 +176,6 @@ TB_HD TB_INLINE uint32_t subc32(uint32_t a, uint32_t b, uint32_t bin, uint32_t* 
 #endif
 }
 
-// ---------------------------------------------------------------------------
-// basic ops
-// ---------------------------------------------------------------------------
 TB_HD TB_INLINE fp fp_zero() {
   fp r;
   TB_UNROLL for (int i = 0; i < 12; i++) r.l[i] = 0;
@@ -126,18 +190,6 @@ TB_HD TB_INLINE fp fp_from_const(const uint32_t (&c)[12]) {
 
 TB_HD TB_INLINE fp fp_one() { return fp_from_const(R1); }
 
-TB_HD TB_INLINE bool fp_is_zero(const fp& a) {
-  uint32_t t = 0;
-  TB_UNROLL for (int i = 0; i < 12; i++) t |= a.l[i];
-  return t == 0;
-}
-
-TB_HD TB_INLINE bool fp_eq(const fp& a, const fp& b) {
-  uint32_t t = 0;
-  TB_UNROLL for (int i = 0; i < 12; i++) t |= a.l[i] ^ b.l[i];
-  return t == 0;
-}
-
 // r = c ? a : b
 TB_HD TB_INLINE fp fp_sel(bool c, const fp& a, const fp& b) {
   fp r;
@@ -145,11 +197,18 @@ TB_HD TB_INLINE fp fp_sel(bool c, const fp& a, const fp& b) {
   return r;
 }
 
-TB_HD TB_INLINE fp fp_add(const fp& a, const fp& b) {
-  fp s, d;
-  uint32_t c = 0, br = 0;
+// a + b without reduction (a, b < 2p -> < 4p < 2^383): a multiplication operand
+TB_HD TB_INLINE fp fp_add_nr(const fp& a, const fp& b) {
+  fp s;
+  uint32_t c = 0;
   TB_UNROLL for (int i = 0; i < 12; i++) s.l[i] = addc32(a.l[i], b.l[i], c, &c);
-  TB_UNROLL for (int i = 0; i < 12; i++) d.l[i] = subc32(s.l[i], P_MOD[i], br, &br);
+  return s;
+}
+
+TB_HD TB_INLINE fp fp_add(const fp& a, const fp& b) {
+  fp s = fp_add_nr(a, b), d;
+  uint32_t br = 0;
+  TB_UNROLL for (int i = 0; i < 12; i++) d.l[i] = subc32(s.l[i], P2_MOD[i], br, &br);
   return fp_sel(br != 0, s, d);
 }
 
@@ -158,198 +217,36 @@ TB_HD TB_INLINE fp fp_sub(const fp& a, const fp& b) {
   uint32_t br = 0, c = 0;
   TB_UNROLL for (int i = 0; i < 12; i++) d.l[i] = subc32(a.l[i], b.l[i], br, &br);
   const uint32_t mask = 0u - br;
-  TB_UNROLL for (int i = 0; i < 12; i++) d.l[i] = addc32(d.l[i], P_MOD[i] & mask, c, &c);
+  TB_UNROLL for (int i = 0; i < 12; i++) d.l[i] = addc32(d.l[i], P2_MOD[i] & mask, c, &c);
   return d;
 }
 
 TB_HD TB_INLINE fp fp_dbl(const fp& a) { return fp_add(a, a); }
 
-TB_HD TB_INLINE fp fp_neg(const fp& a) {
-  fp d;
-  uint32_t br = 0;
-  TB_UNROLL for (int i = 0; i < 12; i++) d.l[i] = subc32(P_MOD[i], a.l[i], br, &br);
-  return fp_sel(fp_is_zero(a), a, d);
-}
+TB_HD TB_INLINE fp fp_neg(const fp& a) { return fp_sub(fp_zero(), a); }
 
 // conditional negate
 TB_HD TB_INLINE fp fp_cneg(const fp& a, bool c) { return fp_sel(c, fp_neg(a), a); }
 
-// ---------------------------------------------------------------------------
-// Montgomery multiplication (FIPS)
-// ---------------------------------------------------------------------------
-// Two-chain variant for a lone product: the a*b terms and the m*p reduction
-// terms of a column go to independent accumulators (halving the dependent
-// v_mad_u64_u32 chain), merged once per column.
-TB_HD TB_INLINE void mac_ab_mp(uint64_t& A, uint32_t& EA, uint64_t& M, uint32_t& EM, uint32_t a, uint32_t b, uint32_t m,
-                               uint32_t pc) {
-#if TB_DEVICE_PASS
-  uint64_t c0, c1;
-  asm("v_mad_u64_u32 %0, %4, %6, %7, %0\n\t"
-      "v_mad_u64_u32 %2, %5, %8, %9, %2\n\t"
-      "v_addc_co_u32_e64 %1, %4, %1, 0, %4\n\t"
-      "v_addc_co_u32_e64 %3, %5, %3, 0, %5"
-      : "+v"(A), "+v"(EA), "+v"(M), "+v"(EM), "=&s"(c0), "=&s"(c1)
-      : "v"(a), "v"(b), "v"(m), "s"(pc));
-#else
-  mac1(A, EA, a, b);
-  mac1(M, EM, m, pc);
-#endif
-}
-
-TB_HD TB_INLINE void acc_merge(uint64_t& A, uint32_t& EA, uint64_t& M, uint32_t& EM) {
-  uint64_t s = A + M;
-  EA += EM + (s < A ? 1u : 0u);
-  A = s;
-  M = 0;
-  EM = 0;
-}
-
-TB_HD TB_INLINE fp fp_mul_body(const fp& a, const fp& b) {
-  uint32_t m[12];
-  fp t;
-  uint64_t A = 0, M = 0;
-  uint32_t EA = 0, EM = 0;
-  TB_UNROLL for (int k = 0; k < 12; k++) {
-    TB_UNROLL for (int i = 0; i < k; i++) mac_ab_mp(A, EA, M, EM, a.l[i], b.l[k - i], m[i], P_MOD[k - i]);
-    mac1(A, EA, a.l[k], b.l[0]);
-    acc_merge(A, EA, M, EM);
-    m[k] = (uint32_t)A * N0;
-    mac1s(A, EA, m[k], P_MOD[0]);
-    A = (A >> 32) | ((uint64_t)EA << 32);
-    EA = 0;
-  }
-  TB_UNROLL for (int k = 12; k < 23; k++) {
-    TB_UNROLL for (int i = k - 11; i < 12; i++) mac_ab_mp(A, EA, M, EM, a.l[i], b.l[k - i], m[i], P_MOD[k - i]);
-    acc_merge(A, EA, M, EM);
-    t.l[k - 12] = (uint32_t)A;
-    A = (A >> 32) | ((uint64_t)EA << 32);
-    EA = 0;
-  }
-  t.l[11] = (uint32_t)A;
-  // t < 2p: one conditional subtraction
+// canonical representative in [0, p)
+TB_HD TB_INLINE fp fp_canon(const fp& a) {
   fp d;
   uint32_t br = 0;
-  TB_UNROLL for (int i = 0; i < 12; i++) d.l[i] = subc32(t.l[i], P_MOD[i], br, &br);
-  return fp_sel(br != 0, t, d);
+  TB_UNROLL for (int i = 0; i < 12; i++) d.l[i] = subc32(a.l[i], P_MOD[i], br, &br);
+  return fp_sel(br != 0, a, d);
 }
 
-TB_HD TB_NOINLINE fp fp_mul(fp a, fp b) {
-  TB_COUNT_MUL();
-  return fp_mul_body(a, b);
+// a == 0 (mod p) for a in [0, 2p): a is 0 or p
+TB_HD TB_INLINE bool fp_is_zero(const fp& a) {
+  uint32_t z = 0, q = 0;
+  TB_UNROLL for (int i = 0; i < 12; i++) {
+    z |= a.l[i];
+    q |= a.l[i] ^ P_MOD[i];
+  }
+  return z == 0 || q == 0;
 }
 
-TB_HD TB_INLINE fp fp_sqr(const fp& a) { return fp_mul(a, a); }
-
-// N independent products interleaved in program order (one accumulator chain
-// each): the ILP a lone FIPS chain lacks.  Used by fp2_mul (N=3) and fp2_sqr (N=2).
-template <int N>
-TB_HD TB_INLINE void mac_n(uint64_t (&A)[N], uint32_t (&E)[N], const uint32_t (&x)[N], const uint32_t (&y)[N]) {
-#if TB_DEVICE_PASS
-  if constexpr (N == 3) {
-    uint64_t c0, c1, c2;
-    asm("v_mad_u64_u32 %0, %6, %9, %10, %0\n\t"
-        "v_mad_u64_u32 %1, %7, %11, %12, %1\n\t"
-        "v_mad_u64_u32 %2, %8, %13, %14, %2\n\t"
-        "v_addc_co_u32_e64 %3, %6, %3, 0, %6\n\t"
-        "v_addc_co_u32_e64 %4, %7, %4, 0, %7\n\t"
-        "v_addc_co_u32_e64 %5, %8, %5, 0, %8"
-        : "+v"(A[0]), "+v"(A[1]), "+v"(A[2]), "+v"(E[0]), "+v"(E[1]), "+v"(E[2]), "=&s"(c0), "=&s"(c1), "=&s"(c2)
-        : "v"(x[0]), "v"(y[0]), "v"(x[1]), "v"(y[1]), "v"(x[2]), "v"(y[2]));
-  } else if constexpr (N == 2) {
-    uint64_t c0, c1;
-    asm("v_mad_u64_u32 %0, %4, %6, %7, %0\n\t"
-        "v_mad_u64_u32 %1, %5, %8, %9, %1\n\t"
-        "v_addc_co_u32_e64 %2, %4, %2, 0, %4\n\t"
-        "v_addc_co_u32_e64 %3, %5, %3, 0, %5"
-        : "+v"(A[0]), "+v"(A[1]), "+v"(E[0]), "+v"(E[1]), "=&s"(c0), "=&s"(c1)
-        : "v"(x[0]), "v"(y[0]), "v"(x[1]), "v"(y[1]));
-  } else {
-    TB_UNROLL for (int j = 0; j < N; j++) mac1(A[j], E[j], x[j], y[j]);
-  }
-#else
-  TB_UNROLL for (int j = 0; j < N; j++) mac1(A[j], E[j], x[j], y[j]);
-#endif
-}
-
-template <int N>
-TB_HD TB_INLINE void macs_n(uint64_t (&A)[N], uint32_t (&E)[N], const uint32_t (&x)[N], uint32_t pc) {
-#if TB_DEVICE_PASS
-  if constexpr (N == 3) {
-    uint64_t c0, c1, c2;
-    asm("v_mad_u64_u32 %0, %6, %9, %12, %0\n\t"
-        "v_mad_u64_u32 %1, %7, %10, %12, %1\n\t"
-        "v_mad_u64_u32 %2, %8, %11, %12, %2\n\t"
-        "v_addc_co_u32_e64 %3, %6, %3, 0, %6\n\t"
-        "v_addc_co_u32_e64 %4, %7, %4, 0, %7\n\t"
-        "v_addc_co_u32_e64 %5, %8, %5, 0, %8"
-        : "+v"(A[0]), "+v"(A[1]), "+v"(A[2]), "+v"(E[0]), "+v"(E[1]), "+v"(E[2]), "=&s"(c0), "=&s"(c1), "=&s"(c2)
-        : "v"(x[0]), "v"(x[1]), "v"(x[2]), "s"(pc));
-  } else if constexpr (N == 2) {
-    uint64_t c0, c1;
-    asm("v_mad_u64_u32 %0, %4, %6, %8, %0\n\t"
-        "v_mad_u64_u32 %1, %5, %7, %8, %1\n\t"
-        "v_addc_co_u32_e64 %2, %4, %2, 0, %4\n\t"
-        "v_addc_co_u32_e64 %3, %5, %3, 0, %5"
-        : "+v"(A[0]), "+v"(A[1]), "+v"(E[0]), "+v"(E[1]), "=&s"(c0), "=&s"(c1)
-        : "v"(x[0]), "v"(x[1]), "s"(pc));
-  } else {
-    TB_UNROLL for (int j = 0; j < N; j++) mac1s(A[j], E[j], x[j], pc);
-  }
-#else
-  TB_UNROLL for (int j = 0; j < N; j++) mac1(A[j], E[j], x[j], pc);
-#endif
-}
-
-// r[j] = a[j] * b[j] (Montgomery), j < N, interleaved
-template <int N>
-TB_HD TB_INLINE void fp_mul_n(fp (&r)[N], const fp (&a)[N], const fp (&b)[N]) {
-  uint32_t m[N][12];
-  uint64_t A[N];
-  uint32_t E[N];
-  TB_UNROLL for (int j = 0; j < N; j++) {
-    A[j] = 0;
-    E[j] = 0;
-  }
-  TB_UNROLL for (int k = 0; k < 23; k++) {
-    const int lo = k < 12 ? 0 : k - 11;
-    const int hi = k < 12 ? k : 11;
-    TB_UNROLL for (int i = lo; i <= hi; i++) {
-      uint32_t x[N], y[N];
-      TB_UNROLL for (int j = 0; j < N; j++) {
-        x[j] = a[j].l[i];
-        y[j] = b[j].l[k - i];
-      }
-      mac_n<N>(A, E, x, y);
-      if (i < k && i < 12 && k - i < 12 && !(k < 12 && i == k)) {
-        // reduction term m_i * p_{k-i} (i < k, both in range)
-        uint32_t xm[N];
-        TB_UNROLL for (int j = 0; j < N; j++) xm[j] = m[j][i];
-        macs_n<N>(A, E, xm, P_MOD[k - i]);
-      }
-    }
-    if (k < 12) {
-      uint32_t xm[N];
-      TB_UNROLL for (int j = 0; j < N; j++) {
-        m[j][k] = (uint32_t)A[j] * N0;
-        xm[j] = m[j][k];
-      }
-      macs_n<N>(A, E, xm, P_MOD[0]);
-    } else {
-      TB_UNROLL for (int j = 0; j < N; j++) r[j].l[k - 12] = (uint32_t)A[j];
-    }
-    TB_UNROLL for (int j = 0; j < N; j++) {
-      A[j] = (A[j] >> 32) | ((uint64_t)E[j] << 32);
-      E[j] = 0;
-    }
-  }
-  TB_UNROLL for (int j = 0; j < N; j++) {
-    r[j].l[11] = (uint32_t)A[j];
-    fp d;
-    uint32_t br = 0;
-    TB_UNROLL for (int i = 0; i < 12; i++) d.l[i] = subc32(r[j].l[i], P_MOD[i], br, &br);
-    r[j] = fp_sel(br != 0, r[j], d);
-  }
-}
+TB_HD TB_INLINE bool fp_eq(const fp& a, const fp& b) { return fp_is_zero(fp_sub(a, b)); }
 
 // multiply by small constants via additions
 TB_HD TB_INLINE fp fp_mul3(const fp& a) { return fp_add(fp_dbl(a), a); }
@@ -370,10 +267,11 @@ TB_HD TB_INLINE fp fp_half(const fp& a) {
 
 TB_HD TB_INLINE fp fp_to_mont(const fp& a) { return fp_mul(a, fp_from_const(R2)); }
 
+// Montgomery -> plain integer, canonical in [0, p)
 TB_HD TB_INLINE fp fp_from_mont(const fp& a) {
   fp one = fp_zero();
   one.l[0] = 1;
-  return fp_mul(a, one);
+  return fp_canon(fp_mul(a, one));
 }
 
 // a^e for a compile-time-sized exponent given as 12 limbs (top bit index `top`)
@@ -467,6 +365,7 @@ TB_HD TB_INLINE fp bez_update(const fp& x, int32_t f, const fp& y, int32_t g) {
 }
 
 TB_HD TB_NOINLINE fp fp_inv(fp A) {
+  A = fp_canon(A);
   uint32_t a[12], b[12];
   TB_UNROLL for (int i = 0; i < 12; i++) {
     a[i] = A.l[i];

@@ -39,8 +39,8 @@ TB_HD TB_NOINLINE fp2 fp2_mul(fp2 a, fp2 b) {
   tb_mul_count += 3;
 #endif
   fp t[3];
-  const fp x[3] = {a.c0, a.c1, fp_add(a.c0, a.c1)};
-  const fp y[3] = {b.c0, b.c1, fp_add(b.c0, b.c1)};
+  const fp x[3] = {a.c0, a.c1, fp_add_nr(a.c0, a.c1)};
+  const fp y[3] = {b.c0, b.c1, fp_add_nr(b.c0, b.c1)};
   fp_mul_n<3>(t, x, y);
   return {fp_sub(t[0], t[1]), fp_sub(fp_sub(t[2], t[0]), t[1])};
 }
@@ -50,7 +50,7 @@ TB_HD TB_NOINLINE fp2 fp2_sqr(fp2 a) {
   tb_mul_count += 2;
 #endif
   fp t[2];
-  const fp x[2] = {a.c0, fp_add(a.c0, a.c1)};
+  const fp x[2] = {a.c0, fp_add_nr(a.c0, a.c1)};
   const fp y[2] = {a.c1, fp_sub(a.c0, a.c1)};
   fp_mul_n<2>(t, x, y);
   return {t[1], fp_dbl(t[0])};
