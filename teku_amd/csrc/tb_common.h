@@ -18,7 +18,7 @@
 #include <hip/hip_runtime.h>
 #define TB_HD __host__ __device__
 #define TB_INLINE __forceinline__
-#define TB_NOINLINE __noinline__
+#define TB_NOINLINE inline __attribute__((noinline))  // inline: one definition across TUs
 #define TB_CONST static constexpr
 #else
 #define TB_HD

@@ -201,7 +201,7 @@ TB_HD TB_NOINLINE jac<F> jac_mul_u64(const jac<F>& P, uint64_t k) {
 // endomorphisms and subgroup checks
 // ---------------------------------------------------------------------------
 // psi(X, Y, Z) = (conj(X) cx, conj(Y) cy, conj(Z))
-TB_HD TB_NOINLINE g2j g2_psi(const g2j& p) {
+TB_HD TB_INLINE g2j g2_psi(const g2j& p) {
   return {fp2_mul(fp2_conj(p.x), fp2_from_const(PSI_CX)), fp2_mul(fp2_conj(p.y), fp2_from_const(PSI_CY)), fp2_conj(p.z)};
 }
 TB_HD TB_INLINE g2j g2_psi2(const g2j& p) {

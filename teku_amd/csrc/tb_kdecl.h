@@ -1,0 +1,63 @@
+// gfx950 kernels for the BLS12-381 verification hot path: shared declarations.
+//
+// Randomized batch verification (BLS.batchVerify -> BlstBLS12381
+// .prepareBatchVerify/completeBatchVerify, BLS.java:275-336,
+// BlstBLS12381.java:112-189) is split into per-stage kernels, one thread per
+// public key / signature set / pairing:
+//
+//   k_pk_decompress   48-B key -> affine G1 + validity (decode, !inf, in G1)
+//   k_set_pk          per set: sum keys (any invalid -> set invalid), [r]apk -> affine P_i
+//   k_set_sig         per set: decode sig, G2 check, [r]sig (Jacobian)
+//   k_set_hash        per set: H(m_i) = hash_to_G2 -> affine Q_i
+//   k_g2_sum_*        S = sum [r_i]sig_i ; pair n = (-g1, S)
+//   k_miller2         per 2 pairs: f_t = Miller(P_2t, Q_2t) Miller(P_2t+1, Q_2t+1)
+//   k_miller_one      the (-g1, S) pair
+//   k_fp12_prod_*     F = prod f_i  (the per-GPU partial, 576 B)
+//   k_final_verify    final_exp(F) == 1 && no invalid set
+//
+// Every thread's work is independent; reductions are two-level (block tree
+// in LDS, then one block over the block partials).
+#pragma once
+#include "tb_stages.h"
+#include "tb_testops.h"
+#include "tb_fp12_wave.h"
+
+using namespace tb;
+
+#define TB_BLOCK 64
+
+// [k]P for a 256-bit scalar (4 little-endian u64 words), MSB first
+template <typename F>
+__device__ TB_INLINE jac<F> jac_mul_u256(const jac<F>& P, const uint64_t* k) {
+  jac<F> r = jac_inf<F>();
+  for (int w = 3; w >= 0; --w) {
+    uint64_t kw = k[w];
+    TB_NOUNROLL for (int b = 63; b >= 0; --b) {
+      r = jac_dbl(r);
+      if ((kw >> b) & 1) r = jac_add(r, P);
+    }
+  }
+  return r;
+}
+
+// Kernel declarations (definitions in k_keys / k_sigs / k_hash / k_pair / k_test .hip),
+// for the host code in tb_lib.hip.
+extern "C" __global__ void k_pk_decompress(const uint8_t* __restrict__ pks, uint32_t K, g1a* __restrict__ pk_aff, uint8_t* __restrict__ pk_code);
+extern "C" __global__ void k_set_pk(const uint32_t* __restrict__ pk_off, const g1a* __restrict__ pk_aff, const uint8_t* __restrict__ pk_code, const uint64_t* __restrict__ rand, uint32_t n, g1a* __restrict__ P, uint8_t* __restrict__ set_code, uint32_t* __restrict__ n_bad);
+extern "C" __global__ void k_aggregate_pks(const g1a* __restrict__ pk_aff, const uint8_t* __restrict__ pk_code, uint32_t K, uint8_t* __restrict__ out);
+extern "C" __global__ void k_sk_to_pk(const uint64_t* __restrict__ sks, uint32_t n, uint8_t* __restrict__ out);
+extern "C" __global__ void k_set_sig(const uint8_t* __restrict__ sigs, const uint64_t* __restrict__ rand, uint32_t n, g2j* __restrict__ rsig, uint8_t* __restrict__ sig_code, uint32_t* __restrict__ n_bad);
+extern "C" __global__ void k_g2_sum_partial(const g2j* __restrict__ in, uint32_t n, g2j* __restrict__ part);
+extern "C" __global__ void k_g2_sum_final(const g2j* __restrict__ part, uint32_t nparts, uint32_t slot, g1a* __restrict__ P, g2a* __restrict__ Q, uint8_t* __restrict__ skip);
+extern "C" __global__ void k_aggregate_sigs(const uint8_t* __restrict__ sigs, uint32_t K, uint8_t* __restrict__ out, int* __restrict__ status);
+extern "C" __global__ void k_sig_validate(const uint8_t* __restrict__ sigs, uint32_t n, uint32_t* __restrict__ out);
+extern "C" __global__ void k_set_hash(const uint8_t* __restrict__ msgs, const uint32_t* __restrict__ msg_off, const uint8_t* __restrict__ dst, uint32_t dlen, uint32_t n, g2a* __restrict__ Q, uint8_t* __restrict__ skip);
+extern "C" __global__ void k_hash_to_g2(const uint8_t* __restrict__ msgs, const uint32_t* __restrict__ msg_off, const uint8_t* __restrict__ dst, uint32_t dlen, uint32_t n, uint8_t* __restrict__ out);
+extern "C" __global__ void k_sign(const uint64_t* __restrict__ sks, const uint8_t* __restrict__ msgs, const uint32_t* __restrict__ msg_off, const uint8_t* __restrict__ dst, uint32_t dlen, uint32_t n, uint8_t* __restrict__ out);
+extern "C" __global__ void k_miller2(const g1a* __restrict__ P, const g2a* __restrict__ Q, const uint8_t* __restrict__ skip, const uint8_t* __restrict__ code_a, const uint8_t* __restrict__ code_b, uint32_t n, fp12* __restrict__ f);
+extern "C" __global__ void k_miller_one(const g1a* __restrict__ P, const g2a* __restrict__ Q, const uint8_t* __restrict__ skip, uint32_t slot, fp12* __restrict__ f);
+extern "C" __global__ void k_fp12_prod(const fp12* __restrict__ in, uint32_t n, fp12* __restrict__ part);
+extern "C" __global__ void k_final_verify_wave(const fp12* __restrict__ f, const uint32_t* __restrict__ n_bad, int* __restrict__ result);
+extern "C" __global__ void k_final_verify(const fp12* __restrict__ f, const uint32_t* __restrict__ n_bad, int* __restrict__ result);
+extern "C" __global__ void k_test_ops(int op, const uint8_t* in, uint8_t* out, uint32_t n);
+extern "C" __global__ void k_test_final_exp_wave(const uint8_t* in, uint8_t* out);

@@ -13,7 +13,7 @@
 #include <vector>
 
 #include "../../include/tekubls.h"
-#include "tb_kernels.hip"
+#include "tb_kdecl.h"
 
 namespace {
 
@@ -161,6 +161,10 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
   hipLaunchKernelGGL(k_g2_sum_final, dim3(1), blk, 0, sb, (const g2j*)(w + L.gpart), L.nb_g2, n, (g1a*)(w + L.P), (g2a*)(w + L.Q),
                      w + L.skip);
   TB_EV(9, sb);
+  // Miller loop of the (-g1, S) pair, overlapping the per-set stages
+  const uint32_t nthr = (n + 1) / 2;
+  hipLaunchKernelGGL(k_miller_one, dim3(1), dim3(64), 0, sb, (const g1a*)(w + L.P), (const g2a*)(w + L.Q), w + L.skip, n,
+                     (fp12*)(w + L.f) + nthr);
   HIPCHK(hipEventRecord(c.e_join[1], sb));
   // caller's stream: public keys
   TB_EV(0, s);
@@ -173,13 +177,13 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
   TB_EV(3, s);
   HIPCHK(hipStreamWaitEvent(s, c.e_join[0], 0));
   HIPCHK(hipStreamWaitEvent(s, c.e_join[1], 0));
-  const uint32_t np = n + 1;
   TB_EV(10, s);
-  hipLaunchKernelGGL(k_miller, dim3((np + TB_BLOCK - 1) / TB_BLOCK), blk, 0, s, (const g1a*)(w + L.P), (const g2a*)(w + L.Q),
-                     w + L.skip, w + L.set_code, w + L.sig_code, n, np, (fp12*)(w + L.f));
+  if (nthr)
+    hipLaunchKernelGGL(k_miller2, dim3((nthr + TB_BLOCK - 1) / TB_BLOCK), blk, 0, s, (const g1a*)(w + L.P), (const g2a*)(w + L.Q),
+                       w + L.skip, w + L.set_code, w + L.sig_code, n, (fp12*)(w + L.f));
   TB_EV(11, s);
   TB_EV(12, s);
-  hipLaunchKernelGGL(k_fp12_prod, dim3(L.nb_f), blk, 0, s, (const fp12*)(w + L.f), np, (fp12*)(w + L.fpart));
+  hipLaunchKernelGGL(k_fp12_prod, dim3(L.nb_f), blk, 0, s, (const fp12*)(w + L.f), nthr + 1, (fp12*)(w + L.fpart));
   hipLaunchKernelGGL(k_fp12_prod, dim3(1), blk, 0, s, (const fp12*)(w + L.fpart), L.nb_f, (fp12*)partial_out);
   TB_EV(13, s);
   HIPCHK(hipMemcpyAsync((uint8_t*)partial_out + sizeof(fp12), w + L.n_bad, 4, hipMemcpyDeviceToDevice, s));

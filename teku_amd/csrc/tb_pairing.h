@@ -1,5 +1,6 @@
 // Optimal ate pairing on BLS12-381: Miller loop over |x| = 0xd201000000010000
-// with Jacobian twist-point arithmetic and sparse line multiplication, and the
+// with homogeneous projective twist-point arithmetic and sparse line
+// multiplication (two pairs per accumulator), and the
 // final exponentiation (p^12-1)/r as easy part * (3 x hard part) using
 //   3 (p^4 - p^2 + 1)/r = (x-1)^2 (x+p) (x^2+p^2-1) + 3
 // (f^(3d) == 1 <=> f^d == 1 since gcd(3, r) = 1).
@@ -14,66 +15,97 @@ struct line3 {
   fp2 a, b, c;
 };
 
-// T <- 2T; line through T tangent, evaluated at P, scaled by 2YZ^3:
-//   A = 3X^3 - 2Y^2, B = -3X^2 Z^2 xP, C = 2 Y Z^3 yP
-TB_HD TB_NOINLINE line3 miller_dbl_step(g2j& T, const g1a& P) {
-  fp2 A = fp2_sqr(T.x);
-  fp2 B = fp2_sqr(T.y);
-  fp2 C = fp2_sqr(B);
-  fp2 D = fp2_dbl(fp2_sub(fp2_sub(fp2_sqr(fp2_add(T.x, B)), A), C));
-  fp2 E = fp2_mul3(A);
-  fp2 ZZ = fp2_sqr(T.z);
+// Twist point in homogeneous projective coordinates (x = X/Z, y = Y/Z).
+struct g2p {
+  fp2 x, y, z;
+};
+
+// 3 b' c with b' = 4(1 + u): 12 xi c, by additions
+TB_HD TB_INLINE fp2 fp2_mul_3b(const fp2& c) {
+  fp2 t = fp2_mul_xi(c);
+  t = fp2_add(fp2_dbl(t), t);
+  return fp2_dbl(fp2_dbl(t));
+}
+
+// T <- 2T with the tangent line at P (Costello-Lange-Naehrig / Aranha et al.
+// 2011 homogeneous formulas for the M-type twist; 3 Fp2 mul + 6 Fp2 sqr +
+// 4 Fp mul).  Line = I + (3 X^2 xP) v - (2YZ yP) v w, an Fp2 multiple of the
+// affine tangent (the factor is killed by the final exponentiation).
+TB_HD TB_NOINLINE line3 miller_dbl_step(g2p& T, const g1a& P) {
+  const fp2 A = fp2_half(fp2_mul(T.x, T.y));
+  const fp2 B = fp2_sqr(T.y);
+  const fp2 C = fp2_sqr(T.z);
+  const fp2 E = fp2_mul_3b(C);
+  const fp2 F = fp2_add(fp2_dbl(E), E);
+  const fp2 G = fp2_half(fp2_add(B, F));
+  const fp2 H = fp2_sub(fp2_sqr(fp2_add(T.y, T.z)), fp2_add(B, C));
+  const fp2 J = fp2_sqr(T.x);
+  const fp2 EE = fp2_sqr(E);
   line3 l;
-  l.a = fp2_sub(fp2_mul(E, T.x), fp2_dbl(B));
-  l.b = fp2_mul_fp(fp2_neg(fp2_mul(E, ZZ)), P.x);
-  fp2 Z3 = fp2_mul(fp2_dbl(T.y), T.z);
-  l.c = fp2_mul_fp(fp2_mul(Z3, ZZ), P.y);
-  fp2 X3 = fp2_sub(fp2_sqr(E), fp2_dbl(D));
-  T.y = fp2_sub(fp2_mul(E, fp2_sub(D, X3)), fp2_dbl(fp2_dbl(fp2_dbl(C))));
-  T.x = X3;
-  T.z = Z3;
+  l.a = fp2_sub(E, B);
+  l.b = fp2_mul_fp(fp2_add(fp2_dbl(J), J), P.x);
+  l.c = fp2_neg(fp2_mul_fp(H, P.y));
+  T.x = fp2_mul(A, fp2_sub(B, F));
+  T.y = fp2_sub(fp2_sqr(G), fp2_add(fp2_dbl(EE), EE));
+  T.z = fp2_mul(B, H);
   return l;
 }
 
-// T <- T + Q (Q affine); line through T and Q at P, scaled by 2HZ:
-//   A = rr xQ - yQ Z3, B = -rr xP, C = Z3 yP
-TB_HD TB_NOINLINE line3 miller_add_step(g2j& T, const g2a& Q, const g1a& P) {
-  fp2 Z1Z1 = fp2_sqr(T.z);
-  fp2 U2 = fp2_mul(Q.x, Z1Z1);
-  fp2 S2 = fp2_mul(fp2_mul(Q.y, T.z), Z1Z1);
-  fp2 H = fp2_sub(U2, T.x);
-  fp2 rr = fp2_dbl(fp2_sub(S2, T.y));
-  fp2 HH = fp2_sqr(H);
-  fp2 I = fp2_dbl(fp2_dbl(HH));
-  fp2 J = fp2_mul(H, I);
-  fp2 V = fp2_mul(T.x, I);
-  fp2 X3 = fp2_sub(fp2_sub(fp2_sqr(rr), J), fp2_dbl(V));
-  fp2 Y3 = fp2_sub(fp2_mul(rr, fp2_sub(V, X3)), fp2_dbl(fp2_mul(T.y, J)));
-  fp2 Z3 = fp2_sub(fp2_sub(fp2_sqr(fp2_add(T.z, H)), Z1Z1), HH);
+// T <- T + Q (Q affine) with the chord line at P (mixed homogeneous addition).
+// Line = (theta xQ - lambda yQ) - (theta xP) v + (lambda yP) v w.
+TB_HD TB_NOINLINE line3 miller_add_step(g2p& T, const g2a& Q, const g1a& P) {
+  const fp2 theta = fp2_sub(T.y, fp2_mul(Q.y, T.z));
+  const fp2 lambda = fp2_sub(T.x, fp2_mul(Q.x, T.z));
+  const fp2 c = fp2_sqr(theta);
+  const fp2 d = fp2_sqr(lambda);
+  const fp2 e = fp2_mul(lambda, d);
+  const fp2 f = fp2_mul(T.z, c);
+  const fp2 g = fp2_mul(T.x, d);
+  const fp2 h = fp2_sub(fp2_add(e, f), fp2_dbl(g));
   line3 l;
-  l.a = fp2_sub(fp2_mul(rr, Q.x), fp2_mul(Q.y, Z3));
-  l.b = fp2_mul_fp(fp2_neg(rr), P.x);
-  l.c = fp2_mul_fp(Z3, P.y);
-  T.x = X3;
-  T.y = Y3;
-  T.z = Z3;
+  l.a = fp2_sub(fp2_mul(theta, Q.x), fp2_mul(lambda, Q.y));
+  l.b = fp2_neg(fp2_mul_fp(theta, P.x));
+  l.c = fp2_mul_fp(lambda, P.y);
+  T.y = fp2_sub(fp2_mul(theta, fp2_sub(g, h)), fp2_mul(e, T.y));
+  T.x = fp2_mul(lambda, h);
+  T.z = fp2_mul(T.z, e);
   return l;
 }
 
-// f_{|x|,Q}(P), conjugated (x < 0).  P, Q finite affine points.
-TB_HD TB_NOINLINE fp12 miller_loop(const g1a& P, const g2a& Q) {
-  g2j T = jac_from_aff(Q);
+// Two Miller loops sharing one accumulator:
+//   f = f_{|x|,Q0}(P0) * f_{|x|,Q1}(P1), conjugated (x < 0).
+// The per-step Fp12 squaring -- the part of a step that does not depend on
+// the pair -- is paid once for both pairs.  s0 / s1 drop a pair (it then
+// contributes 1).  P, Q finite affine points.
+TB_HD TB_NOINLINE fp12 miller_loop2(const g1a& P0, const g2a& Q0, bool s0, const g1a& P1, const g2a& Q1, bool s1) {
+  g2p T0 = {Q0.x, Q0.y, fp2_one()}, T1 = {Q1.x, Q1.y, fp2_one()};
   fp12 f = fp12_one();
   TB_NOUNROLL for (int i = 62; i >= 0; --i) {
-    line3 l = miller_dbl_step(T, P);
-    f = fp12_mul_by_line(fp12_sqr(f), l.a, l.b, l.c);
-    if ((X_ABS >> i) & 1) {
-      l = miller_add_step(T, Q, P);
+    if (i != 62) f = fp12_sqr(f);
+    if (!s0) {
+      const line3 l = miller_dbl_step(T0, P0);
       f = fp12_mul_by_line(f, l.a, l.b, l.c);
+    }
+    if (!s1) {
+      const line3 l = miller_dbl_step(T1, P1);
+      f = fp12_mul_by_line(f, l.a, l.b, l.c);
+    }
+    if ((X_ABS >> i) & 1) {
+      if (!s0) {
+        const line3 l = miller_add_step(T0, Q0, P0);
+        f = fp12_mul_by_line(f, l.a, l.b, l.c);
+      }
+      if (!s1) {
+        const line3 l = miller_add_step(T1, Q1, P1);
+        f = fp12_mul_by_line(f, l.a, l.b, l.c);
+      }
     }
   }
   return fp12_conj(f);
 }
+
+// f_{|x|,Q}(P), conjugated (x < 0).
+TB_HD TB_INLINE fp12 miller_loop(const g1a& P, const g2a& Q) { return miller_loop2(P, Q, false, P, Q, true); }
 
 // a^|x| for a in the cyclotomic subgroup
 TB_HD TB_NOINLINE fp12 cyc_exp_xabs(const fp12& a) {

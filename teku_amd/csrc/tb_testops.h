@@ -40,6 +40,7 @@ enum {
   TOP_STAGE_SET_SIG = 26,
   TOP_STAGE_SET_HASH = 27,
   TOP_G2_JADD = 28,
+  TOP_MILLER2 = 30,
 };
 
 #define TB_TEST_IN 1536
@@ -138,6 +139,14 @@ TB_HD TB_NOINLINE void test_op(int op, const uint8_t* in, uint8_t* out) {
       g1a P = {tio_fp(in), tio_fp(in + 48)};
       g2a Q = {tio_fp2(in + 96), tio_fp2(in + 192)};
       tio_put_fp12(out, miller_loop(P, Q));
+      break;
+    }
+    case TOP_MILLER2: {
+      g1a P0 = {tio_fp(in), tio_fp(in + 48)};
+      g2a Q0 = {tio_fp2(in + 96), tio_fp2(in + 192)};
+      g1a P1 = {tio_fp(in + 288), tio_fp(in + 336)};
+      g2a Q1 = {tio_fp2(in + 384), tio_fp2(in + 480)};
+      tio_put_fp12(out, miller_loop2(P0, Q0, false, P1, Q1, false));
       break;
     }
     case TOP_G1_DECOMP: {

@@ -34,7 +34,7 @@ TB_HD TB_INLINE fp2 fp2_mul3(const fp2& a) { return {fp_mul3(a.c0), fp_mul3(a.c1
 TB_HD TB_INLINE fp2 fp2_half(const fp2& a) { return {fp_half(a.c0), fp_half(a.c1)}; }
 
 // Karatsuba: the three Fp products are independent and run interleaved in one call
-TB_HD TB_NOINLINE fp2 fp2_mul(fp2 a, fp2 b) {
+TB_HD TB_INLINE fp2 fp2_mul(fp2 a, fp2 b) {
 #if !TB_DEVICE_PASS && defined(TB_COUNT_MULS)
   tb_mul_count += 3;
 #endif
@@ -45,7 +45,7 @@ TB_HD TB_NOINLINE fp2 fp2_mul(fp2 a, fp2 b) {
   return {fp_sub(t[0], t[1]), fp_sub(fp_sub(t[2], t[0]), t[1])};
 }
 
-TB_HD TB_NOINLINE fp2 fp2_sqr(fp2 a) {
+TB_HD TB_INLINE fp2 fp2_sqr(fp2 a) {
 #if !TB_DEVICE_PASS && defined(TB_COUNT_MULS)
   tb_mul_count += 2;
 #endif

@@ -125,3 +125,12 @@ def test_pairing_pieces(run):
     single = [dec_fp12(x) for x in run("FINAL_EXP", [enc_fp12(x) for x in fs])]
     wave = [dec_fp12(x) for x in run("FINAL_EXP_WAVE", [enc_fp12(x) for x in fs])]
     assert wave == single
+
+
+def test_miller2_shared_accumulator(run):
+    P0, Q0 = O.G1_GEN, O.G2_GEN
+    P1 = O.jac_to_affine(O.FP, O.jac_mul(O.FP, O.jac_from_affine(O.FP, O.G1_GEN), 7))
+    Q1 = O.hash_to_g2(b"second pair")
+    rec = enc_fp(P0[0]) + enc_fp(P0[1]) + enc_fp2(Q0[0]) + enc_fp2(Q0[1]) + enc_fp(P1[0]) + enc_fp(P1[1]) + enc_fp2(Q1[0]) + enc_fp2(Q1[1])
+    f = dec_fp12(run("MILLER2", [rec])[0])
+    assert O.final_exponentiation(f) == O.f12_mul(O.pairing(P0, Q0), O.pairing(P1, Q1))
