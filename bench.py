@@ -33,14 +33,13 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 from teku_amd import native  # noqa: E402
+from teku_amd.dist import all_gather_partials, shard_bounds  # noqa: E402
 
 R_ORDER = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
 DST = b"BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_POP_"
 
-# Algorithmic work per unit, in Fp-multiplication equivalents (M), counted by
-# tools/count_muls.py on the hostsim build of the same kernel code.
-# One M = 12x12 limb Montgomery product = 2*12^2 = 288 32x32->64 MACs.
-MACS_PER_M = 288
+# Algorithmic work per unit: Fp products (and their v_mad_u64_u32 count),
+# counted by tools/count_muls.py on the hostsim build of the same stage code.
 STAGES = ["pk_decompress", "set_pk", "set_sig", "set_hash", "g2_sum", "miller", "fp12_prod"]
 M_PER_UNIT = json.load(open(os.path.join(ROOT, "tools", "mul_counts.json"))) if os.path.exists(
     os.path.join(ROOT, "tools", "mul_counts.json")
@@ -100,25 +99,70 @@ class DevBatch:
         self.n = n
 
 
-def cpu_baseline_oracle(sample_sets=4):
-    """The oracle (pure-Python restatement) timed on a bounded sample."""
-    from oracle import bls12_381 as O
+# Integer-MAC roofline.  The bound is the v_mad_u64_u32 issue rate: measured
+# 47.6 lane-ops/CU/clk on MI355X (tools/microbench/fp_rates.hip,
+# profiles/r01_microbench_fp_rates.json) -> x CUs x 2.4 GHz.  Algorithmic work
+# = Fp products per unit (tools/count_muls.py on the same stage code) x 392
+# v_mad_u64_u32 per product (301 per squaring), tools/mul_counts.json.
+MAD_RATE_PER_CU_CLK = 47.6
+CLOCK_HZ = 2.4e9
+STAGE_UNITS = {"pk_decompress": "keys", "set_pk": "sets", "set_sig": "sets", "set_hash": "sets", "g2_sum": "sets", "miller": "pairs", "fp12_prod": "pairs"}
 
-    sks = [interop_sk(i) for i in range(sample_sets)]
-    msgs = [bench_message(0, j) for j in range(sample_sets)]
-    pks = [[O.sk_to_pk(s)] for s in sks]
-    sigs = [O.sign(s, m) for s, m in zip(sks, msgs)]
-    rands = [secrets.randbits(64) | 1 for _ in range(sample_sets)]
-    t0 = time.perf_counter()
-    ok = O.batch_verify(pks, msgs, sigs, rands)
-    dt = time.perf_counter() - t0
-    assert ok
+
+def roofline_entry(stage_ms, S, device):
+    props = torch.cuda.get_device_properties(device)
+    peak = MAD_RATE_PER_CU_CLK * props.multi_processor_count * CLOCK_HZ / 1e12  # T mad/s
+    mads = M_PER_UNIT.get("mads_per_unit", {})
+    per_stage = {}
+    for i, name in enumerate(STAGES):
+        if name in mads and stage_ms[i] > 0:
+            per_stage[name] = mads[name] * S / (stage_ms[i] * 1e-3) / 1e12
+    dom = max(range(len(STAGES)), key=lambda i: stage_ms[i])
+    name = STAGES[dom]
+    achieved = per_stage.get(name)
+    traffic = None
+    tpath = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(tpath):
+        traffic = json.load(open(tpath)).get("k_" + ("miller2" if name == "miller" else name), {}).get("bytes_per_launch")
     return {
-        "value": sample_sets / dt,
+        "bound": "valu-int (v_mad_u64_u32 issue)",
+        "kernel": "k_" + ("miller2" if name == "miller" else name),
+        "achieved": achieved,
+        "peak": peak,
+        "unit": "T v_mad_u64_u32/s",
+        "frac": (achieved / peak) if achieved else None,
+        "traffic": traffic,
+        "units_per_launch": S,
+        "unit_of_work": STAGE_UNITS[name],
+        "mads_per_unit": mads.get(name),
+        "fp_products_per_unit": M_PER_UNIT.get(name),
+        "kernel_ms": stage_ms[dom],
+        "stage_frac": {k: v / peak for k, v in per_stage.items()},
+    }
+
+
+def cpu_baseline_oracle(pks, msgs, sigs, sample_sets=4096, threads=16):
+    """The C oracle (oracle/c/bls_oracle.c, 'port') timed on this host over a
+    bounded sample of the same workload: the first `sample_sets` sets."""
+    from oracle import c_oracle as C
+
+    threads = max(1, min(threads, os.cpu_count() or 1))
+    n = sample_sets
+    pk = [pks[48 * j : 48 * j + 48] for j in range(n)]
+    ms = [msgs[32 * j : 32 * j + 32] for j in range(n)]
+    sg = [sigs[96 * j : 96 * j + 96] for j in range(n)]
+    rr = [secrets.randbits(64) | 1 for _ in range(n)]
+    t0 = time.perf_counter()
+    ok = C.batch_verify(pk, ms, sg, rr, threads=threads)
+    dt = time.perf_counter() - t0
+    assert ok, "C oracle rejected the valid sample"
+    return {
+        "value": n / dt,
         "unit": "sigs/s",
-        "cores": 1,
+        "cores": threads,
         "kind": "port",
-        "sample": f"oracle.bls12_381.batch_verify of {sample_sets} interop-key sets (pure Python, 1 thread); build CPU path, not blst",
+        "sample": f"oracle/c batch_verify of the first {n} sets of this workload, {threads} pthreads, {dt:.1f} s; "
+        "build's own C restatement (6x64-bit CIOS Montgomery), not blst",
     }
 
 
@@ -143,11 +187,11 @@ def main():
 
     S = args.sets_per_gpu
     t_gen = time.perf_counter()
-    pks, msgs, sigs = make_workload(L, rank * S, S)
+    lo, hi = shard_bounds(S * world, world, rank)  # weak scaling: S sets per rank
+    pks, msgs, sigs = make_workload(L, lo, hi - lo)
     batch = DevBatch(pks, msgs, sigs, S, device)
     gen_s = time.perf_counter() - t_gen
     partial = torch.empty(native.PARTIAL_BYTES, dtype=torch.uint8, device=device)
-    gathered = torch.empty(world * native.PARTIAL_BYTES, dtype=torch.uint8, device=device)
     stream = torch.cuda.current_stream(device).cuda_stream
     stage_acc = [0.0] * len(STAGES)
     ok = ctypes.c_int(0)
@@ -160,11 +204,7 @@ def main():
                 stage_acc[i] += stage[i]
         else:
             native.check(L.tbls_dev_batch_partial(local, ctypes.byref(batch.desc), stream, partial.data_ptr()), "partial")
-        if world > 1:
-            dist.all_gather_into_tensor(gathered, partial)
-            src = gathered
-        else:
-            src = partial
+        src = all_gather_partials(partial)
         if rank == 0:
             native.check(L.tbls_dev_final_verify(local, src.data_ptr(), world, stream, ctypes.byref(ok)), "final")
             if ok.value != 1:
@@ -195,35 +235,7 @@ def main():
         return
 
     stage_ms = [a / args.steps for a in stage_acc]
-    # integer-VALU roofline of the dominant kernel: k_miller (largest single
-    # kernel; it runs alone after the three concurrent per-set stages join)
-    dom = STAGES.index("miller")
-    props = torch.cuda.get_device_properties(device)
-    cus = props.multi_processor_count
-    peak_tmacs = cus * 128 * 2.4e9 / 1e12  # v_mad_u64_u32: full rate, 4 SIMD32 per CU, 2.4 GHz max clock
-    m_unit = M_PER_UNIT.get(STAGES[dom])
-    units = S + 1 if STAGES[dom] == "miller" else S
-    achieved = None
-    if m_unit:
-        achieved = m_unit * MACS_PER_M * units / (stage_ms[dom] * 1e-3) / 1e12
-    roofline = {
-        "bound": "valu-int",
-        "kernel": "k_" + STAGES[dom],
-        "achieved": achieved,
-        "peak": peak_tmacs,
-        "unit": "TMAC/s",
-        "frac": (achieved / peak_tmacs) if achieved else None,
-        "traffic": None,
-        "m_per_unit": m_unit,
-        "macs_per_m": MACS_PER_M,
-        "units_per_launch": units,
-        "kernel_ms": stage_ms[dom],
-        "stage_tmacs": {
-            STAGES[i]: (M_PER_UNIT[STAGES[i]] * MACS_PER_M * (S + 1 if STAGES[i] == "miller" else S) / (stage_ms[i] * 1e-3) / 1e12)
-            if M_PER_UNIT.get(STAGES[i]) and stage_ms[i] > 0 else None
-            for i in range(len(STAGES))
-        },
-    }
+    roofline = roofline_entry(stage_ms, S, device)
 
     # p50 latency of a 128-set batchVerify through the host C ABI (config 1 shape)
     from teku_amd import bls
@@ -240,7 +252,7 @@ def main():
         assert good
     lat = sorted(lat[3:]) if args.lat_reps > 0 else lat
 
-    cpu = None if args.no_cpu_baseline else cpu_baseline_oracle()
+    cpu = None if args.no_cpu_baseline else cpu_baseline_oracle(pks, msgs, sigs, min(4096, S))
     line = {
         "metric": "BLS sigs verified/sec (batchVerify), 1-8 GPUs; p50 latency @128-sig batch",
         "value": value,
@@ -252,7 +264,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "u32 (381-bit Montgomery Fp on 12x32-bit limbs)",
+        "dtype": "u32 (381-bit Montgomery Fp, 14x29-bit limb products)",
         "data": "synthetic: interop keys (first 65,536 reused cyclically), distinct sha256 messages, GPU-signed",
         "config": {
             "workload": "config 5 per-GPU shard: randomized batchVerify of %d single-signer sets per GPU, RCCL Fp12 partial gather, 1 final exp" % S,

@@ -1,0 +1,29 @@
+// Miller loops: two pairs per Fp12 accumulator (miller_loop2).
+#include "tb_kdecl.h"
+
+using namespace tb;
+
+// Two pairs per thread share one Fp12 accumulator (miller_loop2): thread t
+// owns pairs 2t and 2t+1 of the n set pairs.  Invalid sets (any code) and
+// skipped pairs contribute 1; the batch already fails through n_bad.
+extern "C" __global__ void __launch_bounds__(TB_BLOCK)
+    k_miller2(const g1a* __restrict__ P, const g2a* __restrict__ Q, const uint8_t* __restrict__ skip,
+              const uint8_t* __restrict__ code_a, const uint8_t* __restrict__ code_b, uint32_t n, fp12* __restrict__ f) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t i0 = 2 * t, i1 = 2 * t + 1;
+  if (i0 >= n) return;
+  const bool s0 = skip[i0] != 0 || code_a[i0] != 0 || code_b[i0] != 0;
+  const bool s1 = i1 >= n || skip[i1] != 0 || code_a[i1] != 0 || code_b[i1] != 0;
+  const uint32_t j1 = i1 < n ? i1 : i0;
+  f[t] = miller_loop2(P[i0], Q[i0], s0, P[j1], Q[j1], s1);
+}
+
+// The batch's (-g1, sum r_i sig_i) pair: one thread, launched on the signature
+// stream right after the G2 sum so it overlaps the per-set stages.
+extern "C" __global__ void __launch_bounds__(64)
+    k_miller_one(const g1a* __restrict__ P, const g2a* __restrict__ Q, const uint8_t* __restrict__ skip, uint32_t slot,
+                 fp12* __restrict__ f) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  f[0] = skip[slot] ? fp12_one() : miller_loop(P[slot], Q[slot]);
+}
+

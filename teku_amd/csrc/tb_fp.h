@@ -19,9 +19,12 @@ struct fp {
 
 #if !TB_DEVICE_PASS && defined(TB_COUNT_MULS)
 extern "C" unsigned long long tb_mul_count;  // host instrumentation (tools/count_muls.py)
+extern "C" unsigned long long tb_sqr_count;  // the squarings among them (301 vs 392 v_mad_u64_u32)
 #define TB_COUNT_MUL() (++tb_mul_count)
+#define TB_COUNT_SQR() (++tb_mul_count, ++tb_sqr_count)
 #else
 #define TB_COUNT_MUL() ((void)0)
+#define TB_COUNT_SQR() ((void)0)
 #endif
 
 // ---------------------------------------------------------------------------
@@ -146,7 +149,7 @@ TB_HD TB_INLINE fp fp_mul(fp a, fp b) {
 }
 
 TB_HD TB_INLINE fp fp_sqr(fp a) {
-  TB_COUNT_MUL();
+  TB_COUNT_SQR();
   fp r[1];
   const fp x[1] = {a};
   fp_sqr_n<1>(r, x);

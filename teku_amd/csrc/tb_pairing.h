@@ -31,7 +31,7 @@ TB_HD TB_INLINE fp2 fp2_mul_3b(const fp2& c) {
 // 2011 homogeneous formulas for the M-type twist; 3 Fp2 mul + 6 Fp2 sqr +
 // 4 Fp mul).  Line = I + (3 X^2 xP) v - (2YZ yP) v w, an Fp2 multiple of the
 // affine tangent (the factor is killed by the final exponentiation).
-TB_HD TB_NOINLINE line3 miller_dbl_step(g2p& T, const g1a& P) {
+TB_HD TB_INLINE line3 miller_dbl_step(g2p& T, const g1a& P) {
   const fp2 A = fp2_half(fp2_mul(T.x, T.y));
   const fp2 B = fp2_sqr(T.y);
   const fp2 C = fp2_sqr(T.z);
@@ -53,7 +53,7 @@ TB_HD TB_NOINLINE line3 miller_dbl_step(g2p& T, const g1a& P) {
 
 // T <- T + Q (Q affine) with the chord line at P (mixed homogeneous addition).
 // Line = (theta xQ - lambda yQ) - (theta xP) v + (lambda yP) v w.
-TB_HD TB_NOINLINE line3 miller_add_step(g2p& T, const g2a& Q, const g1a& P) {
+TB_HD TB_INLINE line3 miller_add_step(g2p& T, const g2a& Q, const g1a& P) {
   const fp2 theta = fp2_sub(T.y, fp2_mul(Q.y, T.z));
   const fp2 lambda = fp2_sub(T.x, fp2_mul(Q.x, T.z));
   const fp2 c = fp2_sqr(theta);
@@ -72,6 +72,17 @@ TB_HD TB_NOINLINE line3 miller_add_step(g2p& T, const g2a& Q, const g1a& P) {
   return l;
 }
 
+// One leaf call per Miller step and pair: T <- 2T (or T + Q) and f <- f * line.
+TB_HD TB_NOINLINE void miller_dbl_line(fp12& f, g2p& T, const g1a& P) {
+  const line3 l = miller_dbl_step(T, P);
+  f = fp12_mul_by_line(f, l.a, l.b, l.c);
+}
+
+TB_HD TB_NOINLINE void miller_add_line(fp12& f, g2p& T, const g2a& Q, const g1a& P) {
+  const line3 l = miller_add_step(T, Q, P);
+  f = fp12_mul_by_line(f, l.a, l.b, l.c);
+}
+
 // Two Miller loops sharing one accumulator:
 //   f = f_{|x|,Q0}(P0) * f_{|x|,Q1}(P1), conjugated (x < 0).
 // The per-step Fp12 squaring -- the part of a step that does not depend on
@@ -82,23 +93,11 @@ TB_HD TB_NOINLINE fp12 miller_loop2(const g1a& P0, const g2a& Q0, bool s0, const
   fp12 f = fp12_one();
   TB_NOUNROLL for (int i = 62; i >= 0; --i) {
     if (i != 62) f = fp12_sqr(f);
-    if (!s0) {
-      const line3 l = miller_dbl_step(T0, P0);
-      f = fp12_mul_by_line(f, l.a, l.b, l.c);
-    }
-    if (!s1) {
-      const line3 l = miller_dbl_step(T1, P1);
-      f = fp12_mul_by_line(f, l.a, l.b, l.c);
-    }
+    if (!s0) miller_dbl_line(f, T0, P0);
+    if (!s1) miller_dbl_line(f, T1, P1);
     if ((X_ABS >> i) & 1) {
-      if (!s0) {
-        const line3 l = miller_add_step(T0, Q0, P0);
-        f = fp12_mul_by_line(f, l.a, l.b, l.c);
-      }
-      if (!s1) {
-        const line3 l = miller_add_step(T1, Q1, P1);
-        f = fp12_mul_by_line(f, l.a, l.b, l.c);
-      }
+      if (!s0) miller_add_line(f, T0, Q0, P0);
+      if (!s1) miller_add_line(f, T1, Q1, P1);
     }
   }
   return fp12_conj(f);

@@ -7,6 +7,7 @@
 #if defined(TB_COUNT_MULS)
 extern "C" {
 unsigned long long tb_mul_count = 0;
+unsigned long long tb_sqr_count = 0;
 }
 #endif
 #include "../../teku_amd/csrc/tb_testops.h"
@@ -14,6 +15,17 @@ unsigned long long tb_mul_count = 0;
 extern "C" int tbls_hostsim_test_ops(int op, const uint8_t* in, uint8_t* out, size_t n) {
   for (size_t i = 0; i < n; i++) tb::test_op(op, in + i * TB_TEST_IN, out + i * TB_TEST_OUT);
   return 0;
+}
+
+extern "C" unsigned long long tbls_hostsim_sqr_count(int reset) {
+#if defined(TB_COUNT_MULS)
+  unsigned long long v = tb_sqr_count;
+  if (reset) tb_sqr_count = 0;
+  return v;
+#else
+  (void)reset;
+  return 0;
+#endif
 }
 
 extern "C" unsigned long long tbls_hostsim_mul_count(int reset) {

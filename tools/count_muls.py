@@ -16,6 +16,7 @@ from oracle.keys import interop_sk  # noqa: E402
 from tests.opcodec import OPS, enc_fp, enc_fp2, enc_fp12, enc_h2c, run_ops  # noqa: E402
 
 OPS.update(STAGE_PK=24, STAGE_SET_PK=25, STAGE_SET_SIG=26, STAGE_SET_HASH=27, G2_JADD=28)
+MADS_MUL, MADS_SQR = 392, 301  # v_mad_u64_u32 per 14 x 29-bit Montgomery product / squaring (tb_fp.h)
 
 
 def main():
@@ -25,6 +26,9 @@ def main():
     cnt = lib.tbls_hostsim_mul_count
     cnt.restype = ctypes.c_ulonglong
     cnt.argtypes = [ctypes.c_int]
+    sqc = lib.tbls_hostsim_sqr_count
+    sqc.restype = ctypes.c_ulonglong
+    sqc.argtypes = [ctypes.c_int]
     N = 8
     sks = [interop_sk(i) for i in range(N)]
     pks = [O.sk_to_pk(s) for s in sks]
@@ -32,27 +36,39 @@ def main():
     sigs = [O.sign(s, m) for s, m in zip(sks, msgs)]
     r = 0xF123456789ABCDEF
 
-    def per_unit(op, recs):
+    sq = {}
+
+    def per_unit(op, recs, units_per_rec=1, name=None):
         cnt(1)
+        sqc(1)
         run_ops(fn, op, recs)
-        return cnt(1) / len(recs)
+        m, s_ = cnt(1) / (len(recs) * units_per_rec), sqc(1) / (len(recs) * units_per_rec)
+        if name:
+            sq[name] = s_
+        return m
 
     res = {}
-    res["pk_decompress"] = per_unit("STAGE_PK", pks)
+    res["pk_decompress"] = per_unit("STAGE_PK", pks, name="pk_decompress")
     aff = [O.g1_decompress(p)[1] for p in pks]
-    res["set_pk"] = per_unit("STAGE_SET_PK", [enc_fp(a[0]) + enc_fp(a[1]) + r.to_bytes(8, "little") for a in aff])
-    res["set_sig"] = per_unit("STAGE_SET_SIG", [s + r.to_bytes(8, "little") for s in sigs])
-    res["set_hash"] = per_unit("STAGE_SET_HASH", [enc_h2c(m) for m in msgs])
+    res["set_pk"] = per_unit("STAGE_SET_PK", [enc_fp(a[0]) + enc_fp(a[1]) + r.to_bytes(8, "little") for a in aff], name="set_pk")
+    res["set_sig"] = per_unit("STAGE_SET_SIG", [s + r.to_bytes(8, "little") for s in sigs], name="set_sig")
+    res["set_hash"] = per_unit("STAGE_SET_HASH", [enc_h2c(m) for m in msgs], name="set_hash")
     q = [O.g2_decompress(s)[1] for s in sigs]
-    res["g2_sum"] = per_unit("G2_JADD", [enc_fp2(a[0]) + enc_fp2(a[1]) + enc_fp2(b[0]) + enc_fp2(b[1]) for a, b in zip(q, q[1:] + q[:1])])
-    res["miller"] = per_unit("MILLER", [enc_fp(a[0]) + enc_fp(a[1]) + enc_fp2(b[0]) + enc_fp2(b[1]) for a, b in zip(aff, q)])
+    res["g2_sum"] = per_unit("G2_JADD", [enc_fp2(a[0]) + enc_fp2(a[1]) + enc_fp2(b[0]) + enc_fp2(b[1]) for a, b in zip(q, q[1:] + q[:1])], name="g2_sum")
+    # k_miller2: two pairs per Fp12 accumulator -> work per pair = MILLER2 / 2
+    pair = [enc_fp(a[0]) + enc_fp(a[1]) + enc_fp2(b[0]) + enc_fp2(b[1]) for a, b in zip(aff, q)]
+    res["miller"] = per_unit("MILLER2", [pair[i] + pair[i + 1] for i in range(0, N, 2)], units_per_rec=2, name="miller")
     f = [tuple(tuple((i + j + k, 3 * i + 1) for k in range(3)) for j in range(2)) for i in range(2)]
-    res["fp12_prod"] = per_unit("FP12_MUL", [enc_fp12(f[0]) + enc_fp12(f[1])])
+    # one Fp12 product per accumulator, i.e. per two pairs
+    res["fp12_prod"] = per_unit("FP12_MUL", [enc_fp12(f[0]) + enc_fp12(f[1])], units_per_rec=2, name="fp12_prod")
     res["final_exp"] = per_unit("FINAL_EXP", [enc_fp12(f[0])])
     # per single-signer set (the unit of the headline metric), excluding the once-per-batch final exp
     res["per_set_total"] = sum(res[k] for k in ["pk_decompress", "set_pk", "set_sig", "set_hash", "g2_sum", "miller", "fp12_prod"])
+    res["sqr_per_unit"] = {k: round(v, 1) for k, v in sq.items()}
+    res["mads_per_unit"] = {k: round((res[k] - sq[k]) * MADS_MUL + sq[k] * MADS_SQR) for k in sq}
+    res["mads_per_mul"], res["mads_per_sqr"] = MADS_MUL, MADS_SQR
     out = os.path.join(ROOT, "tools", "mul_counts.json")
-    json.dump({k: round(v, 1) for k, v in res.items()}, open(out, "w"), indent=1)
+    json.dump({k: (round(v, 1) if isinstance(v, float) else v) for k, v in res.items()}, open(out, "w"), indent=1)
     print(json.dumps(res, indent=1))
 
 
