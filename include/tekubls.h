@@ -146,6 +146,10 @@ int tbls_dev_batch_partial(int device, const tbls_dev_batch* b, void* stream, vo
  * loops, Fp12 product.  Blocks until the partial is ready. */
 int tbls_dev_batch_partial_timed(int device, const tbls_dev_batch* b, void* stream, void* partial_out, float* stage_ms);
 
+/* Profiling variant: every stage runs alone on `stream` (no stage overlap),
+ * so stage_ms[7] are exclusive kernel times (the roofline's denominators). */
+int tbls_dev_batch_stage_profile(int device, const tbls_dev_batch* b, void* stream, void* partial_out, float* stage_ms);
+
 /* Multiply g partial records (device memory, contiguous) and run the final
  * exponentiation: *ok = 1 iff no invalid set and the product is 1. */
 int tbls_dev_final_verify(int device, const void* partials, uint32_t g, void* stream, int* ok);

@@ -18,12 +18,24 @@ extern "C" __global__ void __launch_bounds__(TB_BLOCK)
   f[t] = miller_loop2(P[i0], Q[i0], s0, P[j1], Q[j1], s1);
 }
 
+// One pair per thread (small batches: half the per-thread latency of the
+// two-pair accumulator when the GPU is mostly idle).
+extern "C" __global__ void __launch_bounds__(TB_BLOCK)
+    k_miller1(const g1a* __restrict__ P, const g2a* __restrict__ Q, const uint8_t* __restrict__ skip,
+              const uint8_t* __restrict__ code_a, const uint8_t* __restrict__ code_b, uint32_t n, fp12* __restrict__ f) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const bool s0 = skip[i] != 0 || code_a[i] != 0 || code_b[i] != 0;
+  f[i] = s0 ? fp12_one() : miller_loop(P[i], Q[i]);
+}
+
 // The batch's (-g1, sum r_i sig_i) pair: one thread, launched on the signature
 // stream right after the G2 sum so it overlaps the per-set stages.
 extern "C" __global__ void __launch_bounds__(64)
     k_miller_one(const g1a* __restrict__ P, const g2a* __restrict__ Q, const uint8_t* __restrict__ skip, uint32_t slot,
                  fp12* __restrict__ f) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  tb_latency_prio();
   f[0] = skip[slot] ? fp12_one() : miller_loop(P[slot], Q[slot]);
 }
 

@@ -20,6 +20,7 @@ __device__ TB_INLINE void fp12_block_reduce(fp12& v) {
 
 extern "C" __global__ void __launch_bounds__(TB_BLOCK)
     k_fp12_prod(const fp12* __restrict__ in, uint32_t n, fp12* __restrict__ part) {
+  tb_latency_prio();
   const uint32_t stride = gridDim.x * blockDim.x;
   fp12 acc = fp12_one();
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -35,6 +36,7 @@ extern "C" __global__ void __launch_bounds__(TB_BLOCK)
 extern "C" __global__ void __launch_bounds__(64) k_final_verify_wave(const fp12* __restrict__ f, const uint32_t* __restrict__ n_bad,
                                                                      int* __restrict__ result) {
   __shared__ final_exp_lds L;
+  tb_latency_prio();
   if (threadIdx.x == 0) fp12_to_coords(L.F, f[0]);
   __syncthreads();
   final_exp_wave(L);

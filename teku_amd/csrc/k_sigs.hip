@@ -34,6 +34,7 @@ __device__ TB_INLINE void g2_block_reduce(g2j& v) {
 
 extern "C" __global__ void __launch_bounds__(TB_BLOCK)
     k_g2_sum_partial(const g2j* __restrict__ in, uint32_t n, g2j* __restrict__ part) {
+  tb_latency_prio();
   const uint32_t stride = gridDim.x * blockDim.x;
   g2j acc = jac_inf<fp2>();
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) acc = jac_add(acc, in[i]);
@@ -45,6 +46,7 @@ extern "C" __global__ void __launch_bounds__(TB_BLOCK)
 extern "C" __global__ void __launch_bounds__(TB_BLOCK)
     k_g2_sum_final(const g2j* __restrict__ part, uint32_t nparts, uint32_t slot, g1a* __restrict__ P, g2a* __restrict__ Q,
                    uint8_t* __restrict__ skip) {
+  tb_latency_prio();
   g2j acc = jac_inf<fp2>();
   for (uint32_t i = threadIdx.x; i < nparts; i += blockDim.x) acc = jac_add(acc, part[i]);
   g2_block_reduce(acc);

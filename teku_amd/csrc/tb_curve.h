@@ -77,9 +77,14 @@ TB_HD TB_INLINE jac<F> jac_sel(bool c, const jac<F>& a, const jac<F>& b) {
   return {f_sel(c, a.x, b.x), f_sel(c, a.y, b.y), f_sel(c, a.z, b.z)};
 }
 
+// Point operations come in two forms: the *_i bodies are inlined into the
+// scalar-multiplication loops (so the loop keeps its point in registers and
+// makes no call per bit); jac_dbl / jac_add / jac_add_aff are leaf calls for
+// everything else (reductions, cofactor clearing, aggregation).
+
 // dbl-2009-l (a = 0); infinity (Z=0) maps to Z=0.
 template <typename F>
-TB_HD TB_NOINLINE jac<F> jac_dbl(const jac<F>& p) {
+TB_HD TB_INLINE jac<F> jac_dbl_i(const jac<F>& p) {
   F A = f_sqr(p.x);
   F B = f_sqr(p.y);
   F C = f_sqr(B);
@@ -97,7 +102,12 @@ TB_HD TB_NOINLINE jac<F> jac_dbl(const jac<F>& p) {
 // add-2007-bl with the exceptional cases (P == Q -> dbl, P == -Q -> inf,
 // either infinite) handled by a rarely-taken branch.
 template <typename F>
-TB_HD TB_NOINLINE jac<F> jac_add(const jac<F>& p, const jac<F>& q) {
+TB_HD TB_NOINLINE jac<F> jac_dbl(const jac<F>& p) {
+  return jac_dbl_i(p);
+}
+
+template <typename F>
+TB_HD TB_INLINE jac<F> jac_add_i(const jac<F>& p, const jac<F>& q) {
   F Z1Z1 = f_sqr(p.z);
   F Z2Z2 = f_sqr(q.z);
   F U1 = f_mul(p.x, Z2Z2);
@@ -125,7 +135,12 @@ TB_HD TB_NOINLINE jac<F> jac_add(const jac<F>& p, const jac<F>& q) {
 
 // madd-2007-bl: p Jacobian + q affine (q finite)
 template <typename F>
-TB_HD TB_NOINLINE jac<F> jac_add_aff(const jac<F>& p, const aff<F>& q) {
+TB_HD TB_NOINLINE jac<F> jac_add(const jac<F>& p, const jac<F>& q) {
+  return jac_add_i(p, q);
+}
+
+template <typename F>
+TB_HD TB_INLINE jac<F> jac_add_aff_i(const jac<F>& p, const aff<F>& q) {
   F Z1Z1 = f_sqr(p.z);
   F U2 = f_mul(q.x, Z1Z1);
   F S2 = f_mul(f_mul(q.y, p.z), Z1Z1);
@@ -146,6 +161,11 @@ TB_HD TB_NOINLINE jac<F> jac_add_aff(const jac<F>& p, const aff<F>& q) {
   o.y = f_sub(f_mul(r, f_sub(V, o.x)), f_dbl(f_mul(p.y, J)));
   o.z = f_sub(f_sub(f_sqr(f_add(p.z, H)), Z1Z1), HH);
   return o;
+}
+
+template <typename F>
+TB_HD TB_NOINLINE jac<F> jac_add_aff(const jac<F>& p, const aff<F>& q) {
+  return jac_add_aff_i(p, q);
 }
 
 // projective equality (either may be infinite)
@@ -177,8 +197,8 @@ TB_HD TB_NOINLINE jac<F> jac_mul_u64_aff(const aff<F>& P, uint64_t k) {
   int top = 63 - __builtin_clzll(k);
   r = jac_from_aff(P);
   TB_NOUNROLL for (int i = top - 1; i >= 0; --i) {
-    r = jac_dbl(r);
-    if ((k >> i) & 1) r = jac_add_aff(r, P);
+    r = jac_dbl_i(r);
+    if ((k >> i) & 1) r = jac_add_aff_i(r, P);
   }
   return r;
 }
@@ -191,8 +211,8 @@ TB_HD TB_NOINLINE jac<F> jac_mul_u64(const jac<F>& P, uint64_t k) {
   int top = 63 - __builtin_clzll(k);
   r = P;
   TB_NOUNROLL for (int i = top - 1; i >= 0; --i) {
-    r = jac_dbl(r);
-    if ((k >> i) & 1) r = jac_add(r, P);
+    r = jac_dbl_i(r);
+    if ((k >> i) & 1) r = jac_add_i(r, P);
   }
   return r;
 }

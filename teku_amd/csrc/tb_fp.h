@@ -451,6 +451,50 @@ TB_HD TB_NOINLINE fp fp_pow_win(const fp& a, uint32_t first, const uint16_t* sch
   }
   return r;
 }
+// Two bases, same fixed exponent, interleaved: every squaring / product step
+// is a 2-wide fp_*_n<2>, giving the multiplier two independent chains (a lone
+// exponentiation is one long dependent chain).
+TB_HD TB_NOINLINE void fp_pow_win2(fp& r0, fp& r1, const fp& a0, const fp& a1, uint32_t first, const uint16_t* sched, int nstep) {
+  fp t0[8], t1[8], sq[2], r[2];
+  t0[0] = a0;
+  t1[0] = a1;
+  {
+    const fp x[2] = {a0, a1};
+    fp_sqr_n<2>(sq, x);
+  }
+  TB_NOUNROLL for (int i = 1; i < 8; i++) {
+    const fp x[2] = {t0[i - 1], t1[i - 1]};
+    fp_mul_n<2>(r, x, sq);
+    t0[i] = r[0];
+    t1[i] = r[1];
+  }
+  r[0] = t0[first];
+  r[1] = t1[first];
+  TB_NOUNROLL for (int k = 0; k < nstep; k++) {
+    const uint32_t e = sched[k];
+    TB_NOUNROLL for (uint32_t j = 0; j < (e >> 4); j++) {
+      const fp x[2] = {r[0], r[1]};
+      fp_sqr_n<2>(r, x);
+#if !TB_DEVICE_PASS && defined(TB_COUNT_MULS)
+      tb_mul_count += 2;
+      tb_sqr_count += 2;
+#endif
+    }
+    if ((e & 15u) < 8u) {
+      const fp x[2] = {r[0], r[1]}, y[2] = {t0[e & 15u], t1[e & 15u]};
+      fp_mul_n<2>(r, x, y);
+#if !TB_DEVICE_PASS && defined(TB_COUNT_MULS)
+      tb_mul_count += 2;
+#endif
+    }
+  }
+#if !TB_DEVICE_PASS && defined(TB_COUNT_MULS)
+  tb_mul_count += 16;  // the table
+  tb_sqr_count += 2;
+#endif
+  r0 = r[0];
+  r1 = r[1];
+}
 TB_HD TB_INLINE fp fp_sqrt_cand(const fp& a) { return fp_pow_win(a, EXPW_SQRT_FIRST, EXPW_SQRT, EXPW_SQRT_N); }     // a^((p+1)/4)
 TB_HD TB_INLINE fp fp_pow_pm3d4(const fp& a) { return fp_pow_win(a, EXPW_PM3D4_FIRST, EXPW_PM3D4, EXPW_PM3D4_N); }  // a^((p-3)/4)
 

@@ -193,6 +193,68 @@ TB_HD TB_NOINLINE g2a map_to_curve_sswu(const fp2& u) {
   return {x, y};
 }
 
+// Both field elements of hash_to_field through SSWU together: one shared
+// inversion (Montgomery's trick on the two tv values) and both square-root
+// exponentiations interleaved (fp_pow_win2).  Same results as two calls of
+// map_to_curve_sswu.  (Per-input state is in named variables, not arrays,
+// so nothing is dynamically indexed.)
+struct sswu_state {
+  fp2 zu2, tvs, x1, gx1, x2, gx2, x, gx;
+  fp n1, c, delta;
+  bool exc;
+};
+
+TB_HD TB_INLINE void sswu_pre(sswu_state& st, const fp2& u) {
+  st.zu2 = fp2_mul(fp2_from_const(SSWU_Z), fp2_sqr(u));
+  const fp2 tv = fp2_add(fp2_sqr(st.zu2), st.zu2);
+  st.exc = fp2_is_zero(tv);
+  st.tvs = fp2_sel(st.exc, fp2_one(), tv);
+}
+
+TB_HD TB_INLINE void sswu_mid(sswu_state& st, const fp2& u, const fp2& tinv) {
+  const fp2 A = fp2_from_const(SSWU_A), B = fp2_from_const(SSWU_B);
+  st.x1 = fp2_mul(fp2_from_const(SSWU_MINUS_B_OVER_A), fp2_add(fp2_one(), tinv));
+  st.x1 = fp2_sel(st.exc, fp2_from_const(SSWU_B_OVER_ZA), st.x1);
+  st.gx1 = fp2_add(fp2_mul(fp2_add(fp2_sqr(st.x1), A), st.x1), B);
+  st.x2 = fp2_mul(st.zu2, st.x1);
+  st.gx2 = fp2_add(fp2_mul(fp2_add(fp2_sqr(st.x2), A), st.x2), B);
+  st.n1 = fp2_norm(st.gx1);
+  const fp nu = fp2_norm(u);
+  st.c = fp_mul(fp_mul(fp_sqr(nu), nu), fp_from_const(SQRT_MINUS_125));
+}
+
+TB_HD TB_INLINE void sswu_select(sswu_state& st, const fp& g1) {
+  const bool sq1 = fp_eq(fp_sqr(g1), st.n1);
+  const fp g2 = fp_mul(st.c, g1);  // N(gx2) = 125 N(u)^6 N(gx1)
+  st.x = fp2_sel(sq1, st.x1, st.x2);
+  st.gx = fp2_sel(sq1, st.gx1, st.gx2);
+  st.delta = fp2_sqrt_delta(st.gx, fp_sel(sq1, g1, g2));
+}
+
+TB_HD TB_INLINE g2a sswu_post(const sswu_state& st, const fp2& u, const fp& s) {
+  fp2 y;
+  fp2_sqrt_finish(y, st.gx, st.delta, s);
+  if (fp2_sgn0(u) != fp2_sgn0(y)) y = fp2_neg(y);
+  return {st.x, y};
+}
+
+TB_HD TB_NOINLINE void map_to_curve_sswu2(g2a& q0, g2a& q1, const fp2& u0, const fp2& u1) {
+  sswu_state a, b;
+  sswu_pre(a, u0);
+  sswu_pre(b, u1);
+  const fp2 inv = fp2_inv(fp2_mul(a.tvs, b.tvs));
+  sswu_mid(a, u0, fp2_mul(inv, b.tvs));
+  sswu_mid(b, u1, fp2_mul(inv, a.tvs));
+  fp g1a_, g1b_;
+  fp_pow_win2(g1a_, g1b_, a.n1, b.n1, EXPW_SQRT_FIRST, EXPW_SQRT, EXPW_SQRT_N);
+  sswu_select(a, g1a_);
+  sswu_select(b, g1b_);
+  fp sa, sb;
+  fp_pow_win2(sa, sb, a.delta, b.delta, EXPW_PM3D4_FIRST, EXPW_PM3D4, EXPW_PM3D4_N);
+  q0 = sswu_post(a, u0, sa);
+  q1 = sswu_post(b, u1, sb);
+}
+
 // Q0 + Q1 on E2' (a = A' != 0): madd with a general-a doubling for Q0 == Q1
 TB_HD TB_NOINLINE g2j e2p_add_aff_aff(const g2a& p, const g2a& q) {
   fp2 H = fp2_sub(q.x, p.x);
@@ -257,8 +319,8 @@ TB_HD TB_NOINLINE g2j iso_map_jac(const g2j& p) {
 TB_HD TB_NOINLINE g2j hash_to_g2(const xmd_ctx& c) {
   fp2 u0, u1;
   hash_to_field_fp2(u0, u1, c);
-  g2a q0 = map_to_curve_sswu(u0);
-  g2a q1 = map_to_curve_sswu(u1);
+  g2a q0, q1;
+  map_to_curve_sswu2(q0, q1, u0, u1);
   g2j q = e2p_add_aff_aff(q0, q1);
   q = iso_map_jac(q);
   return g2_clear_cofactor(q);

@@ -11,6 +11,7 @@
 //   k_set_hash        per set: H(m_i) = hash_to_G2 -> affine Q_i
 //   k_g2_sum_*        S = sum [r_i]sig_i ; pair n = (-g1, S)
 //   k_miller2         per 2 pairs: f_t = Miller(P_2t, Q_2t) Miller(P_2t+1, Q_2t+1)
+//   k_miller1         per pair (small batches)
 //   k_miller_one      the (-g1, S) pair
 //   k_fp12_prod_*     F = prod f_i  (the per-GPU partial, 576 B)
 //   k_final_verify    final_exp(F) == 1 && no invalid set
@@ -26,6 +27,11 @@ using namespace tb;
 
 #define TB_BLOCK 64
 
+// Latency-bound kernels (G2 sum, the single Miller loop, Fp12 products, the
+// final exponentiation) run underneath throughput kernels that fill every
+// SIMD; top wave priority lets their few waves win instruction arbitration.
+__device__ TB_INLINE void tb_latency_prio() { __builtin_amdgcn_s_setprio(3); }
+
 // [k]P for a 256-bit scalar (4 little-endian u64 words), MSB first
 template <typename F>
 __device__ TB_INLINE jac<F> jac_mul_u256(const jac<F>& P, const uint64_t* k) {
@@ -33,8 +39,8 @@ __device__ TB_INLINE jac<F> jac_mul_u256(const jac<F>& P, const uint64_t* k) {
   for (int w = 3; w >= 0; --w) {
     uint64_t kw = k[w];
     TB_NOUNROLL for (int b = 63; b >= 0; --b) {
-      r = jac_dbl(r);
-      if ((kw >> b) & 1) r = jac_add(r, P);
+      r = jac_dbl_i(r);
+      if ((kw >> b) & 1) r = jac_add_i(r, P);
     }
   }
   return r;
@@ -55,6 +61,7 @@ extern "C" __global__ void k_set_hash(const uint8_t* __restrict__ msgs, const ui
 extern "C" __global__ void k_hash_to_g2(const uint8_t* __restrict__ msgs, const uint32_t* __restrict__ msg_off, const uint8_t* __restrict__ dst, uint32_t dlen, uint32_t n, uint8_t* __restrict__ out);
 extern "C" __global__ void k_sign(const uint64_t* __restrict__ sks, const uint8_t* __restrict__ msgs, const uint32_t* __restrict__ msg_off, const uint8_t* __restrict__ dst, uint32_t dlen, uint32_t n, uint8_t* __restrict__ out);
 extern "C" __global__ void k_miller2(const g1a* __restrict__ P, const g2a* __restrict__ Q, const uint8_t* __restrict__ skip, const uint8_t* __restrict__ code_a, const uint8_t* __restrict__ code_b, uint32_t n, fp12* __restrict__ f);
+extern "C" __global__ void k_miller1(const g1a* __restrict__ P, const g2a* __restrict__ Q, const uint8_t* __restrict__ skip, const uint8_t* __restrict__ code_a, const uint8_t* __restrict__ code_b, uint32_t n, fp12* __restrict__ f);
 extern "C" __global__ void k_miller_one(const g1a* __restrict__ P, const g2a* __restrict__ Q, const uint8_t* __restrict__ skip, uint32_t slot, fp12* __restrict__ f);
 extern "C" __global__ void k_fp12_prod(const fp12* __restrict__ in, uint32_t n, fp12* __restrict__ part);
 extern "C" __global__ void k_final_verify_wave(const fp12* __restrict__ f, const uint32_t* __restrict__ n_bad, int* __restrict__ result);

@@ -6,6 +6,7 @@
 // AggregatingSignatureVerificationService.java:122-129).  Inputs are copied
 // into pinned staging on entry.  There is no CPU fallback.
 #include <chrono>
+#include <cstdlib>
 #include <functional>
 #include <cstring>
 #include <mutex>
@@ -74,7 +75,7 @@ struct dev_ctx {
   dbuf fin;     // final-exponentiation scratch
   dbuf dstb;    // default DST for the device-resident API
   hipStream_t aux[2] = {nullptr, nullptr};  // concurrent per-set stages
-  hipEvent_t e_fork = nullptr, e_join[2] = {nullptr, nullptr};
+  hipEvent_t e_fork = nullptr, e_join[2] = {nullptr, nullptr}, e_sig = nullptr;
   hbuf hin, hout;
 };
 
@@ -124,35 +125,55 @@ struct ws_layout {
 // hash, 4 G2 sum, 5 Miller, 6 Fp12 product.
 #define TB_NSTAGE 7
 #define TB_NSTAGE_EV (2 * TB_NSTAGE)
-// The three per-set stages are independent (keys / signatures / messages), so
-// they run concurrently on three streams forked from the caller's stream `s`
-// and joined before the Miller loops.
+// Stage order.  The chain  signatures -> G2 sum -> Miller loop of the
+// (-g1, sum r_i sig_i) pair  is latency-bound after its first kernel (one block,
+// then one thread), so:
+//  * large batches (n >= TB_SIG_FIRST_MIN) run k_set_sig alone first; the
+//    G2 sum and the single Miller loop then run on stream b underneath the
+//    hash / key stages and the set pairs' Miller loops, which fill the GPU;
+//  * small batches (GPU mostly idle) run the three per-set stages
+//    concurrently on three streams and use one pair per thread in the Miller
+//    loop (half the latency of the two-pair accumulator).
+// TBLS_SERIAL=1 (or `serial`) runs everything on the caller's stream, for
+// exclusive per-stage timings.
+#define TB_SIG_FIRST_MIN 32768u
+#define TB_MILLER1_MAX 4096u
 int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* partial_out, ws_layout& L,
-                   const uint8_t* dst, uint32_t dlen, bool keep_codes, hipEvent_t* ev = nullptr) {
+                   const uint8_t* dst, uint32_t dlen, bool keep_codes, hipEvent_t* ev = nullptr, bool serial_req = false) {
   const uint32_t n = b.n, K = b.n_keys;
   L = ws_layout(n, K);
   if (c.ws.ensure(L.total)) return TBLS_DEVICE_ERROR;
   uint8_t* w = c.ws.as<uint8_t>();
   (void)keep_codes;
-  hipStream_t sa = c.aux[0], sb = c.aux[1];
+  static const bool serial_env = getenv("TBLS_SERIAL") && getenv("TBLS_SERIAL")[0] == '1';
+  const bool serial = serial_env || serial_req;
+  const bool sig_first = !serial && n >= TB_SIG_FIRST_MIN;
+  hipStream_t sa = serial ? s : c.aux[0], sb = serial ? s : c.aux[1];
+  // the hash stage runs on the caller's stream when signatures go first
+  hipStream_t sh = sig_first ? s : sa, ss = sig_first ? s : sb;
 #define TB_EV(i, st) \
   if (ev) HIPCHK(hipEventRecord(ev[i], st))
-  HIPCHK(hipMemsetAsync(w + L.set_code, 0, n ? n : 1, s));
-  HIPCHK(hipMemsetAsync(w + L.n_bad, 0, 4, s));
-  HIPCHK(hipEventRecord(c.e_fork, s));
-  HIPCHK(hipStreamWaitEvent(sa, c.e_fork, 0));
-  HIPCHK(hipStreamWaitEvent(sb, c.e_fork, 0));
   const dim3 blk(TB_BLOCK);
   const dim3 g((n + TB_BLOCK - 1) / TB_BLOCK);
-  // stream a: hash_to_G2 per set
-  TB_EV(6, sa);
-  if (n) hipLaunchKernelGGL(k_set_hash, g, blk, 0, sa, b.msgs, b.msg_off, dst, dlen, n, (g2a*)(w + L.Q), w + L.skip);
-  TB_EV(7, sa);
-  HIPCHK(hipEventRecord(c.e_join[0], sa));
-  // stream b: signatures, then the G2 sum
-  TB_EV(4, sb);
-  if (n) hipLaunchKernelGGL(k_set_sig, g, blk, 0, sb, b.sigs, b.rand, n, (g2j*)(w + L.rsig), w + L.sig_code, (uint32_t*)(w + L.n_bad));
-  TB_EV(5, sb);
+  const bool one_pair = n <= TB_MILLER1_MAX;
+  const uint32_t nthr = one_pair ? n : (n + 1) / 2;  // Miller values f[0..nthr-1]; f[nthr] = the g1 pair
+  HIPCHK(hipMemsetAsync(w + L.set_code, 0, n ? n : 1, s));
+  HIPCHK(hipMemsetAsync(w + L.n_bad, 0, 4, s));
+  if (!sig_first) {
+    HIPCHK(hipEventRecord(c.e_fork, s));
+    HIPCHK(hipStreamWaitEvent(sa, c.e_fork, 0));
+    HIPCHK(hipStreamWaitEvent(sb, c.e_fork, 0));
+  }
+  // signatures: decompress, G2 subgroup check, [r]sig
+  TB_EV(4, ss);
+  if (n) hipLaunchKernelGGL(k_set_sig, g, blk, 0, ss, b.sigs, b.rand, n, (g2j*)(w + L.rsig), w + L.sig_code, (uint32_t*)(w + L.n_bad));
+  TB_EV(5, ss);
+  HIPCHK(hipEventRecord(c.e_sig, ss));
+  if (sig_first) {
+    HIPCHK(hipStreamWaitEvent(sa, c.e_sig, 0));
+    HIPCHK(hipStreamWaitEvent(sb, c.e_sig, 0));
+  }
+  // stream b: the G2 sum, then the Miller loop of the (-g1, S) pair
   TB_EV(8, sb);
   if (n)
     hipLaunchKernelGGL(k_g2_sum_partial, dim3(L.nb_g2), blk, 0, sb, (const g2j*)(w + L.rsig), n, (g2j*)(w + L.gpart));
@@ -161,27 +182,39 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
   hipLaunchKernelGGL(k_g2_sum_final, dim3(1), blk, 0, sb, (const g2j*)(w + L.gpart), L.nb_g2, n, (g1a*)(w + L.P), (g2a*)(w + L.Q),
                      w + L.skip);
   TB_EV(9, sb);
-  // Miller loop of the (-g1, S) pair, overlapping the per-set stages
-  const uint32_t nthr = (n + 1) / 2;
   hipLaunchKernelGGL(k_miller_one, dim3(1), dim3(64), 0, sb, (const g1a*)(w + L.P), (const g2a*)(w + L.Q), w + L.skip, n,
                      (fp12*)(w + L.f) + nthr);
   HIPCHK(hipEventRecord(c.e_join[1], sb));
-  // caller's stream: public keys
-  TB_EV(0, s);
-  if (K) hipLaunchKernelGGL(k_pk_decompress, dim3((K + TB_BLOCK - 1) / TB_BLOCK), blk, 0, s, b.pks, K, (g1a*)(w + L.pk_aff), w + L.pk_code);
-  TB_EV(1, s);
-  TB_EV(2, s);
+  // hash_to_G2 per set
+  TB_EV(6, sh);
+  if (n) hipLaunchKernelGGL(k_set_hash, g, blk, 0, sh, b.msgs, b.msg_off, dst, dlen, n, (g2a*)(w + L.Q), w + L.skip);
+  TB_EV(7, sh);
+  // public keys (stream a when signatures go first, else the caller's stream)
+  hipStream_t sk = sig_first ? sa : s;
+  TB_EV(0, sk);
+  if (K) hipLaunchKernelGGL(k_pk_decompress, dim3((K + TB_BLOCK - 1) / TB_BLOCK), blk, 0, sk, b.pks, K, (g1a*)(w + L.pk_aff), w + L.pk_code);
+  TB_EV(1, sk);
+  TB_EV(2, sk);
   if (n)
-    hipLaunchKernelGGL(k_set_pk, g, blk, 0, s, b.pk_off, (const g1a*)(w + L.pk_aff), w + L.pk_code, b.rand, n, (g1a*)(w + L.P),
+    hipLaunchKernelGGL(k_set_pk, g, blk, 0, sk, b.pk_off, (const g1a*)(w + L.pk_aff), w + L.pk_code, b.rand, n, (g1a*)(w + L.P),
                        w + L.set_code, (uint32_t*)(w + L.n_bad));
-  TB_EV(3, s);
+  TB_EV(3, sk);
+  HIPCHK(hipEventRecord(c.e_join[0], sig_first ? sa : sh));
   HIPCHK(hipStreamWaitEvent(s, c.e_join[0], 0));
-  HIPCHK(hipStreamWaitEvent(s, c.e_join[1], 0));
+  if (!sig_first) HIPCHK(hipStreamWaitEvent(s, c.e_sig, 0));
+  // Miller loops of the set pairs (invalid sets contribute 1)
   TB_EV(10, s);
-  if (nthr)
-    hipLaunchKernelGGL(k_miller2, dim3((nthr + TB_BLOCK - 1) / TB_BLOCK), blk, 0, s, (const g1a*)(w + L.P), (const g2a*)(w + L.Q),
-                       w + L.skip, w + L.set_code, w + L.sig_code, n, (fp12*)(w + L.f));
+  if (nthr) {
+    const dim3 gm((nthr + TB_BLOCK - 1) / TB_BLOCK);
+    if (one_pair)
+      hipLaunchKernelGGL(k_miller1, gm, blk, 0, s, (const g1a*)(w + L.P), (const g2a*)(w + L.Q), w + L.skip, w + L.set_code,
+                         w + L.sig_code, n, (fp12*)(w + L.f));
+    else
+      hipLaunchKernelGGL(k_miller2, gm, blk, 0, s, (const g1a*)(w + L.P), (const g2a*)(w + L.Q), w + L.skip, w + L.set_code,
+                         w + L.sig_code, n, (fp12*)(w + L.f));
+  }
   TB_EV(11, s);
+  HIPCHK(hipStreamWaitEvent(s, c.e_join[1], 0));
   TB_EV(12, s);
   hipLaunchKernelGGL(k_fp12_prod, dim3(L.nb_f), blk, 0, s, (const fp12*)(w + L.f), nthr + 1, (fp12*)(w + L.fpart));
   hipLaunchKernelGGL(k_fp12_prod, dim3(1), blk, 0, s, (const fp12*)(w + L.fpart), L.nb_f, (fp12*)partial_out);
@@ -429,7 +462,8 @@ extern "C" int tbls_init(int n_devices, uint32_t flags) {
         hipStreamCreateWithFlags(&c->aux[1], hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&c->e_fork, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->e_join[0], hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->e_join[1], hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&c->e_join[1], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->e_sig, hipEventDisableTiming) != hipSuccess) {
       delete c;
       break;
     }
@@ -453,6 +487,7 @@ extern "C" void tbls_shutdown(void) {
     for (int i = 0; i < 2; i++)
       if (c->aux[i]) (void)hipStreamDestroy(c->aux[i]);
     if (c->e_fork) (void)hipEventDestroy(c->e_fork);
+    if (c->e_sig) (void)hipEventDestroy(c->e_sig);
     for (int i = 0; i < 2; i++)
       if (c->e_join[i]) (void)hipEventDestroy(c->e_join[i]);
     delete c;
@@ -711,7 +746,7 @@ extern "C" int tbls_dev_batch_partial(int device, const tbls_dev_batch* b, void*
   return launch_partial(*c, *b, s, partial_out, L, c->dstb.as<uint8_t>(), 43, false);
 }
 
-extern "C" int tbls_dev_batch_partial_timed(int device, const tbls_dev_batch* b, void* stream, void* partial_out, float* stage_ms) {
+static int partial_timed(int device, const tbls_dev_batch* b, void* stream, void* partial_out, float* stage_ms, bool serial) {
   if (ensure_init()) return TBLS_DEVICE_ERROR;
   dev_ctx* c = ctx_for(device);
   if (!c) return TBLS_DEVICE_ERROR;
@@ -725,7 +760,7 @@ extern "C" int tbls_dev_batch_partial_timed(int device, const tbls_dev_batch* b,
   hipEvent_t ev[TB_NSTAGE_EV];
   for (int i = 0; i < TB_NSTAGE_EV; i++) HIPCHK(hipEventCreate(&ev[i]));
   ws_layout L(0, 0);
-  int rc = launch_partial(*c, *b, s, partial_out, L, c->dstb.as<uint8_t>(), 43, false, ev);
+  int rc = launch_partial(*c, *b, s, partial_out, L, c->dstb.as<uint8_t>(), 43, false, ev, serial);
   if (!rc) {
     HIPCHK(hipEventSynchronize(ev[TB_NSTAGE_EV - 1]));
     static const int order[TB_NSTAGE] = {0, 1, 2, 3, 4, 5, 6};  // pk, set_pk, set_sig, set_hash, g2_sum, miller, prod
@@ -738,6 +773,14 @@ extern "C" int tbls_dev_batch_partial_timed(int device, const tbls_dev_batch* b,
   }
   for (int i = 0; i < TB_NSTAGE_EV; i++) (void)hipEventDestroy(ev[i]);
   return rc;
+}
+
+extern "C" int tbls_dev_batch_partial_timed(int device, const tbls_dev_batch* b, void* stream, void* partial_out, float* stage_ms) {
+  return partial_timed(device, b, stream, partial_out, stage_ms, false);
+}
+
+extern "C" int tbls_dev_batch_stage_profile(int device, const tbls_dev_batch* b, void* stream, void* partial_out, float* stage_ms) {
+  return partial_timed(device, b, stream, partial_out, stage_ms, true);
 }
 
 // batched helpers for building synthetic workloads on the device

@@ -92,10 +92,13 @@ TB_HD TB_INLINE bool fp2_sign_zcash(const fp2& a) {
 //   chi = -1:  x = (-a1 s/2) + (s*delta) u
 // Returns false if a is not a square.  `norm_gamma` (optional) lets a caller
 // reuse sqrt(N(a)) (SSWU computes it to decide squareness).
-TB_HD TB_NOINLINE bool fp2_sqrt_with_gamma(fp2& out, const fp2& a, const fp& gamma) {
-  fp delta = fp_half(fp_add(a.c0, gamma));
-  delta = fp_sel(fp_is_zero(delta), fp_half(fp_sub(a.c0, gamma)), delta);
-  fp s = fp_pow_pm3d4(delta);
+TB_HD TB_INLINE fp fp2_sqrt_delta(const fp2& a, const fp& gamma) {
+  const fp delta = fp_half(fp_add(a.c0, gamma));
+  return fp_sel(fp_is_zero(delta), fp_half(fp_sub(a.c0, gamma)), delta);
+}
+
+// given s = delta^((p-3)/4)
+TB_HD TB_INLINE bool fp2_sqrt_finish(fp2& out, const fp2& a, const fp& delta, const fp& s) {
   fp sd = fp_mul(s, delta);
   fp chi = fp_mul(s, sd);
   fp hs = fp_half(fp_mul(a.c1, s));
@@ -105,6 +108,11 @@ TB_HD TB_NOINLINE bool fp2_sqrt_with_gamma(fp2& out, const fp2& a, const fp& gam
   x.c1 = fp_sel(pos, hs, sd);
   out = x;
   return fp2_eq(fp2_sqr(x), a);
+}
+
+TB_HD TB_NOINLINE bool fp2_sqrt_with_gamma(fp2& out, const fp2& a, const fp& gamma) {
+  const fp delta = fp2_sqrt_delta(a, gamma);
+  return fp2_sqrt_finish(out, a, delta, fp_pow_pm3d4(delta));
 }
 
 TB_HD TB_INLINE fp fp2_norm(const fp2& a) { return fp_add(fp_sqr(a.c0), fp_sqr(a.c1)); }

@@ -121,6 +121,10 @@ _SIGS = {
         ctypes.c_int,
         [ctypes.c_int, ctypes.POINTER(TblsDevBatch), ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_float)],
     ),
+    "tbls_dev_batch_stage_profile": (
+        ctypes.c_int,
+        [ctypes.c_int, ctypes.POINTER(TblsDevBatch), ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_float)],
+    ),
     "tbls_sk_to_pk_many": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p]),
     "tbls_sign_many": (
         ctypes.c_int,
