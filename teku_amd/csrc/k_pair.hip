@@ -6,39 +6,54 @@ using namespace tb;
 // ---------------------------------------------------------------------------
 // Miller loops and the Fp12 product
 // ---------------------------------------------------------------------------
-__device__ TB_INLINE void fp12_block_reduce(fp12& v) {
-  __shared__ fp12 sh[TB_BLOCK];
-  const int t = threadIdx.x;
-  sh[t] = v;
+// Wave-parallel chunked product: workgroup g (64 lanes) multiplies
+// in[g*chunk .. min(n, (g+1)*chunk)) with w_mul (54 Fp products per Fp12
+// multiply spread over the lanes, so the serial chain is ~1 Fp product per
+// element instead of 54) and writes out[g].  Levels of this kernel reduce the
+// Miller values to the per-GPU partial.
+__device__ TB_INLINE void w_load(fp* dst, const fp12* src) {
+  const int l = threadIdx.x;
+  if (l < 12) dst[l] = reinterpret_cast<const fp*>(src)[l];
   __syncthreads();
-  for (int s = TB_BLOCK / 2; s > 0; s >>= 1) {
-    if (t < s) sh[t] = fp12_mul(sh[t], sh[t + s]);
-    __syncthreads();
-  }
-  v = sh[0];
 }
 
-extern "C" __global__ void __launch_bounds__(TB_BLOCK)
-    k_fp12_prod(const fp12* __restrict__ in, uint32_t n, fp12* __restrict__ part) {
+__device__ TB_INLINE void w_store(fp12* dst, const fp* src) {
+  const int l = threadIdx.x;
+  if (l < 12) reinterpret_cast<fp*>(dst)[l] = src[l];
+}
+
+struct prod_lds {
+  fp A[12], X[12];
+  wave12_scratch s;
+};
+
+extern "C" __global__ void __launch_bounds__(64)
+    k_fp12_prod_wave(const fp12* __restrict__ in, uint32_t n, uint32_t chunk, fp12* __restrict__ out) {
+  __shared__ prod_lds L;
   tb_latency_prio();
-  const uint32_t stride = gridDim.x * blockDim.x;
-  fp12 acc = fp12_one();
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) {
-    acc = in[i];
-    for (i += stride; i < n; i += stride) acc = fp12_mul(acc, in[i]);
+  const uint32_t b = blockIdx.x * chunk;
+  uint32_t e = b + chunk;
+  if (e > n) e = n;
+  if (b >= e) return;
+  w_load(L.A, in + b);
+  for (uint32_t i = b + 1; i < e; i++) {
+    w_load(L.X, in + i);
+    w_mul(L.A, L.A, L.X, L.s);
   }
-  fp12_block_reduce(acc);
-  if (threadIdx.x == 0) part[blockIdx.x] = acc;
+  w_store(out + blockIdx.x, L.A);
 }
 
-// result[0] = 1 iff no set is invalid and final_exp(prod f) == 1 (one 64-lane wave)
-extern "C" __global__ void __launch_bounds__(64) k_final_verify_wave(const fp12* __restrict__ f, const uint32_t* __restrict__ n_bad,
-                                                                     int* __restrict__ result) {
+// result[0] = 1 iff no set is invalid and final_exp(prod_{i<g} f_i) == 1
+// (one 64-lane wave; g = number of per-GPU partials)
+extern "C" __global__ void __launch_bounds__(64) k_final_verify_wave(const fp12* __restrict__ f, uint32_t g,
+                                                                     const uint32_t* __restrict__ n_bad, int* __restrict__ result) {
   __shared__ final_exp_lds L;
   tb_latency_prio();
-  if (threadIdx.x == 0) fp12_to_coords(L.F, f[0]);
-  __syncthreads();
+  w_load(L.F, f);
+  for (uint32_t i = 1; i < g; i++) {
+    w_load(L.X, f + i);
+    w_mul(L.F, L.F, L.X, L.s);
+  }
   final_exp_wave(L);
   if (threadIdx.x == 0) result[0] = (n_bad[0] == 0 && fp12_is_one(fp12_from_coords(L.F))) ? 1 : 0;
 }

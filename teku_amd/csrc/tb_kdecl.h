@@ -13,7 +13,7 @@
 //   k_miller2         per 2 pairs: f_t = Miller(P_2t, Q_2t) Miller(P_2t+1, Q_2t+1)
 //   k_miller1         per pair (small batches)
 //   k_miller_one      the (-g1, S) pair
-//   k_fp12_prod_*     F = prod f_i  (the per-GPU partial, 576 B)
+//   k_fp12_prod_wave  F = prod f_i  (chunked wave-parallel levels; the per-GPU partial, 576 B)
 //   k_final_verify    final_exp(F) == 1 && no invalid set
 //
 // Every thread's work is independent; reductions are two-level (block tree
@@ -63,8 +63,8 @@ extern "C" __global__ void k_sign(const uint64_t* __restrict__ sks, const uint8_
 extern "C" __global__ void k_miller2(const g1a* __restrict__ P, const g2a* __restrict__ Q, const uint8_t* __restrict__ skip, const uint8_t* __restrict__ code_a, const uint8_t* __restrict__ code_b, uint32_t n, fp12* __restrict__ f);
 extern "C" __global__ void k_miller1(const g1a* __restrict__ P, const g2a* __restrict__ Q, const uint8_t* __restrict__ skip, const uint8_t* __restrict__ code_a, const uint8_t* __restrict__ code_b, uint32_t n, fp12* __restrict__ f);
 extern "C" __global__ void k_miller_one(const g1a* __restrict__ P, const g2a* __restrict__ Q, const uint8_t* __restrict__ skip, uint32_t slot, fp12* __restrict__ f);
-extern "C" __global__ void k_fp12_prod(const fp12* __restrict__ in, uint32_t n, fp12* __restrict__ part);
-extern "C" __global__ void k_final_verify_wave(const fp12* __restrict__ f, const uint32_t* __restrict__ n_bad, int* __restrict__ result);
+extern "C" __global__ void k_fp12_prod_wave(const fp12* __restrict__ in, uint32_t n, uint32_t chunk, fp12* __restrict__ out);
+extern "C" __global__ void k_final_verify_wave(const fp12* __restrict__ f, uint32_t g, const uint32_t* __restrict__ n_bad, int* __restrict__ result);
 extern "C" __global__ void k_final_verify(const fp12* __restrict__ f, const uint32_t* __restrict__ n_bad, int* __restrict__ result);
 extern "C" __global__ void k_test_ops(int op, const uint8_t* in, uint8_t* out, uint32_t n);
 extern "C" __global__ void k_test_final_exp_wave(const uint8_t* in, uint8_t* out);

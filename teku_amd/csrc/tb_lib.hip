@@ -88,6 +88,8 @@ size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
 // --------------------------------------------------------------------------
 // workspace layout for one device pipeline over n sets / K keys
 // --------------------------------------------------------------------------
+// Fp12 product levels: each wave multiplies TB_PROD_CHUNK values (k_fp12_prod_wave)
+#define TB_PROD_CHUNK 16u
 struct ws_layout {
   size_t pk_aff, pk_code, P, Q, skip, set_code, sig_code, rsig, f, gpart, fpart, fpart2, n_bad, result, total;
   uint32_t nb_g2, nb_f;
@@ -96,8 +98,7 @@ struct ws_layout {
     nb_g2 = (n + TB_BLOCK - 1) / TB_BLOCK;
     if (nb_g2 > 256) nb_g2 = 256;
     if (nb_g2 == 0) nb_g2 = 1;
-    nb_f = (np + TB_BLOCK - 1) / TB_BLOCK;
-    if (nb_f > 256) nb_f = 256;
+    nb_f = (np + TB_PROD_CHUNK - 1) / TB_PROD_CHUNK;  // first product level
     size_t o = 0;
     pk_aff = o;   o = align_up(o + (size_t)K * sizeof(g1a));
     pk_code = o;  o = align_up(o + K);
@@ -110,7 +111,7 @@ struct ws_layout {
     f = o;        o = align_up(o + (size_t)np * sizeof(fp12));
     gpart = o;    o = align_up(o + (size_t)nb_g2 * sizeof(g2j));
     fpart = o;    o = align_up(o + (size_t)nb_f * sizeof(fp12));
-    fpart2 = o;   o = align_up(o + sizeof(fp12));
+    fpart2 = o;   o = align_up(o + (size_t)((nb_f + TB_PROD_CHUNK - 1) / TB_PROD_CHUNK) * sizeof(fp12));
     n_bad = o;    o = align_up(o + 4);
     result = o;   o = align_up(o + 4);
     total = o;
@@ -216,8 +217,21 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
   TB_EV(11, s);
   HIPCHK(hipStreamWaitEvent(s, c.e_join[1], 0));
   TB_EV(12, s);
-  hipLaunchKernelGGL(k_fp12_prod, dim3(L.nb_f), blk, 0, s, (const fp12*)(w + L.f), nthr + 1, (fp12*)(w + L.fpart));
-  hipLaunchKernelGGL(k_fp12_prod, dim3(1), blk, 0, s, (const fp12*)(w + L.fpart), L.nb_f, (fp12*)partial_out);
+  {
+    // levels of chunked wave products: f -> fpart -> fpart2 -> fpart ... -> partial_out
+    const fp12* src = (const fp12*)(w + L.f);
+    uint32_t cnt = nthr + 1;
+    int lvl = 0;
+    for (;;) {
+      const uint32_t nout = (cnt + TB_PROD_CHUNK - 1) / TB_PROD_CHUNK;
+      fp12* dstp = nout == 1 ? (fp12*)partial_out : (fp12*)(w + ((lvl & 1) ? L.fpart2 : L.fpart));
+      hipLaunchKernelGGL(k_fp12_prod_wave, dim3(nout), dim3(64), 0, s, src, cnt, TB_PROD_CHUNK, dstp);
+      if (nout == 1) break;
+      src = dstp;
+      cnt = nout;
+      lvl++;
+    }
+  }
   TB_EV(13, s);
   HIPCHK(hipMemcpyAsync((uint8_t*)partial_out + sizeof(fp12), w + L.n_bad, 4, hipMemcpyDeviceToDevice, s));
   HIPCHK(hipGetLastError());
@@ -244,8 +258,8 @@ int launch_final(dev_ctx& c, const void* recs, uint32_t g, hipStream_t s, int* r
   uint32_t* nbad = (uint32_t*)(w + align_up((size_t)g * sizeof(fp12)) + align_up(sizeof(fp12)));
   int* res = (int*)(nbad + 1);
   hipLaunchKernelGGL(k_gather_partials, dim3(1), dim3(64), 0, s, (const uint8_t*)recs, g, f, nbad);
-  hipLaunchKernelGGL(k_fp12_prod, dim3(1), dim3(TB_BLOCK), 0, s, (const fp12*)f, g, prod);
-  hipLaunchKernelGGL(k_final_verify_wave, dim3(1), dim3(64), 0, s, (const fp12*)prod, (const uint32_t*)nbad, res);
+  (void)prod;
+  hipLaunchKernelGGL(k_final_verify_wave, dim3(1), dim3(64), 0, s, (const fp12*)f, g, (const uint32_t*)nbad, res);
   HIPCHK(hipGetLastError());
   if (c.hout.ensure(16)) return TBLS_DEVICE_ERROR;
   HIPCHK(hipMemcpyAsync(c.hout.p, res, 4, hipMemcpyDeviceToHost, s));
