@@ -79,6 +79,18 @@ __device__ TB_INLINE void w_cyc_sqr(fp* dst, const fp* x, wave12_scratch& s) {
                          W12C_LIN_ENT);
 }
 
+// general Fp12 squaring (tb_tower.h fp12_sqr: 36 products)
+__device__ TB_INLINE void w_sqr(fp* dst, const fp* x, wave12_scratch& s) {
+  w_bilinear<W12S_NPROD>(dst, x, x, s, W12S_A_OFF, W12S_A_ENT, W12S_B_OFF, W12S_B_ENT, W12S_POST_OFF, W12S_POST_ENT, W12S_LIN_OFF,
+                         W12S_LIN_ENT);
+}
+
+// x * line, line dense in coordinates 0,1 (A), 2,3 (B), 8,9 (C), zero elsewhere (39 products)
+__device__ TB_INLINE void w_mul_line(fp* dst, const fp* x, const fp* ln, wave12_scratch& s) {
+  w_bilinear<W12L_NPROD>(dst, x, ln, s, W12L_A_OFF, W12L_A_ENT, W12L_B_OFF, W12L_B_ENT, W12L_POST_OFF, W12L_POST_ENT, W12L_LIN_OFF,
+                         W12L_LIN_ENT);
+}
+
 __device__ TB_INLINE void w_copy(fp* dst, const fp* x) {
   const int l = threadIdx.x;
   fp v;
@@ -191,6 +203,111 @@ __device__ TB_INLINE void final_exp_wave(final_exp_lds& L) {
   w_cyc_sqr(L.X, L.T, L.s);
   w_mul(L.X, L.X, L.T, L.s);  // t^3
   w_mul(L.F, L.C, L.X, L.s);
+}
+
+// ---------------------------------------------------------------------------
+// Wave-parallel Miller loop: one pair per 64-lane workgroup, for batches too
+// small to fill the GPU with one pair per thread (the p50@128 latency path)
+// and for the batch's (-g1, sum r_i sig_i) pair.  Same algorithm and formulas
+// as tb_pairing.h miller_loop (homogeneous projective doubling / mixed
+// addition, lines at coordinates 0, 1, 4 of the Fp12 Fp2 slots):
+//   f^2            36 Fp products on 36 lanes (w_sqr)
+//   T <- 2T, line  two levels of Fp2 products on 5 / 6 lanes (w_dbl_step)
+//   f * line       39 Fp products on 39 lanes (w_mul_line)
+// so a step's serial chain is ~4 Fp-product latencies instead of ~90.
+// The 5 addition steps run on lane 0.
+// ---------------------------------------------------------------------------
+struct miller_lds {
+  fp F[12];   // accumulator
+  fp LN[12];  // line, dense coordinates (zeros outside 0,1,2,3,8,9)
+  fp2 T[3];   // X, Y, Z
+  fp2 PR[6];  // per-lane Fp2 products of the doubling step
+  wave12_scratch s;
+};
+
+__device__ TB_INLINE void w_store_line(miller_lds& L, const line3& l) {
+  L.LN[0] = l.a.c0;
+  L.LN[1] = l.a.c1;
+  L.LN[2] = l.b.c0;
+  L.LN[3] = l.b.c1;
+  L.LN[8] = l.c.c0;
+  L.LN[9] = l.c.c1;
+}
+
+// T <- 2T and the tangent line at P into L.LN (tb_pairing.h miller_dbl_step)
+__device__ TB_INLINE void w_dbl_step(miller_lds& L, const g1a& P) {
+  const int l = threadIdx.x;
+  const fp2 X = L.T[0], Y = L.T[1], Z = L.T[2];
+  __syncthreads();
+  // level 1: X Y, Y^2, Z^2, (Y + Z)^2, X^2
+  if (l < 5) {
+    const fp2 a = fp2_sel(l == 0 || l == 4, X, fp2_sel(l == 1, Y, fp2_sel(l == 2, Z, fp2_add(Y, Z))));
+    const fp2 b = fp2_sel(l == 0, Y, a);
+    L.PR[l] = fp2_mul(a, b);
+  }
+  __syncthreads();
+  const fp2 B = L.PR[1], C = L.PR[2];
+  const fp2 A = fp2_half(L.PR[0]);
+  const fp2 E = fp2_mul_3b(C);
+  const fp2 F = fp2_add(fp2_dbl(E), E);
+  const fp2 G = fp2_half(fp2_add(B, F));
+  const fp2 H = fp2_sub(L.PR[3], fp2_add(B, C));
+  const fp2 J3 = fp2_add(fp2_dbl(L.PR[4]), L.PR[4]);
+  __syncthreads();
+  // level 2: A (B - F) -> X', B H -> Z', G^2, E^2, 3J xP, H yP
+  if (l < 6) {
+    const fp2 px = {P.x, fp_zero()}, py = {P.y, fp_zero()};
+    const fp2 a = fp2_sel(l == 0, A, fp2_sel(l == 1, B, fp2_sel(l == 2, G, fp2_sel(l == 3, E, fp2_sel(l == 4, J3, H)))));
+    const fp2 b =
+        fp2_sel(l == 0, fp2_sub(B, F), fp2_sel(l == 1, H, fp2_sel(l == 2, G, fp2_sel(l == 3, E, fp2_sel(l == 4, px, py)))));
+    L.PR[l] = fp2_mul(a, b);
+  }
+  __syncthreads();
+  if (l == 0) {
+    const fp2 ee = L.PR[3];
+    L.T[0] = L.PR[0];
+    L.T[1] = fp2_sub(L.PR[2], fp2_add(fp2_dbl(ee), ee));
+    L.T[2] = L.PR[1];
+    line3 ln;
+    ln.a = fp2_sub(E, B);
+    ln.b = L.PR[4];
+    ln.c = fp2_neg(L.PR[5]);
+    w_store_line(L, ln);
+  }
+  __syncthreads();
+}
+
+// f_{|x|,Q}(P), conjugated, into L.F (whole workgroup of 64 lanes)
+__device__ TB_INLINE void miller_loop_wave(miller_lds& L, const g1a& P, const g2a& Q) {
+  const int l = threadIdx.x;
+  if (l < 12) {
+    L.F[l] = l == 0 ? fp_one() : fp_zero();
+    L.LN[l] = fp_zero();
+  }
+  if (l == 0) {
+    L.T[0] = Q.x;
+    L.T[1] = Q.y;
+    L.T[2] = fp2_one();
+  }
+  __syncthreads();
+  for (int i = 62; i >= 0; --i) {
+    if (i != 62) w_sqr(L.F, L.F, L.s);
+    w_dbl_step(L, P);
+    w_mul_line(L.F, L.F, L.LN, L.s);
+    if ((X_ABS >> i) & 1) {
+      if (l == 0) {
+        g2p T = {L.T[0], L.T[1], L.T[2]};
+        const line3 ln = miller_add_step(T, Q, P);
+        L.T[0] = T.x;
+        L.T[1] = T.y;
+        L.T[2] = T.z;
+        w_store_line(L, ln);
+      }
+      __syncthreads();
+      w_mul_line(L.F, L.F, L.LN, L.s);
+    }
+  }
+  w_conj(L.F, L.F);
 }
 
 }  // namespace tb

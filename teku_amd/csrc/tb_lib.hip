@@ -139,6 +139,12 @@ struct ws_layout {
 // exclusive per-stage timings.
 #define TB_SIG_FIRST_MIN 32768u
 #define TB_MILLER1_MAX 4096u
+// up to this many sets, one pair per 64-lane workgroup (k_miller_wave);
+// TBLS_MILLER_WAVE_MAX overrides (tuning)
+static uint32_t miller_wave_max() {
+  static const uint32_t v = getenv("TBLS_MILLER_WAVE_MAX") ? (uint32_t)atoi(getenv("TBLS_MILLER_WAVE_MAX")) : 1024u;
+  return v;
+}
 int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* partial_out, ws_layout& L,
                    const uint8_t* dst, uint32_t dlen, bool keep_codes, hipEvent_t* ev = nullptr, bool serial_req = false) {
   const uint32_t n = b.n, K = b.n_keys;
@@ -183,7 +189,7 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
   hipLaunchKernelGGL(k_g2_sum_final, dim3(1), blk, 0, sb, (const g2j*)(w + L.gpart), L.nb_g2, n, (g1a*)(w + L.P), (g2a*)(w + L.Q),
                      w + L.skip);
   TB_EV(9, sb);
-  hipLaunchKernelGGL(k_miller_one, dim3(1), dim3(64), 0, sb, (const g1a*)(w + L.P), (const g2a*)(w + L.Q), w + L.skip, n,
+  hipLaunchKernelGGL(k_miller_one_wave, dim3(1), dim3(64), 0, sb, (const g1a*)(w + L.P), (const g2a*)(w + L.Q), w + L.skip, n,
                      (fp12*)(w + L.f) + nthr);
   HIPCHK(hipEventRecord(c.e_join[1], sb));
   // hash_to_G2 per set
@@ -207,7 +213,10 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
   TB_EV(10, s);
   if (nthr) {
     const dim3 gm((nthr + TB_BLOCK - 1) / TB_BLOCK);
-    if (one_pair)
+    if (n <= miller_wave_max())
+      hipLaunchKernelGGL(k_miller_wave, dim3(n), dim3(64), 0, s, (const g1a*)(w + L.P), (const g2a*)(w + L.Q), w + L.skip,
+                         w + L.set_code, w + L.sig_code, n, (fp12*)(w + L.f));
+    else if (one_pair)
       hipLaunchKernelGGL(k_miller1, gm, blk, 0, s, (const g1a*)(w + L.P), (const g2a*)(w + L.Q), w + L.skip, w + L.set_code,
                          w + L.sig_code, n, (fp12*)(w + L.f));
     else

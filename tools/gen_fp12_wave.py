@@ -44,6 +44,8 @@ class Ctx:
         self.prods = []  # (A lin over x, B lin over y)
 
     def mul(self, a, b):
+        if not a.d or not b.d:  # a structurally zero operand (sparse line): no product
+            return Lin()
         self.prods.append((a, b))
         return Lin({("p", len(self.prods) - 1): 1})
 
@@ -139,6 +141,23 @@ def cycsqr(C, f):  # tb_tower.h fp12_cyc_sqr
     return ((z0, z4, z3), (z2, z1, z5))
 
 
+def f12sqr(C, a):  # tb_tower.h fp12_sqr
+    ab = f6mul(C, a[0], a[1])
+    t = f6mul(C, f6add(a[0], a[1]), f6add(a[0], f6mulv(a[1])))
+    c0 = f6sub(f6sub(t, ab), f6mulv(ab))
+    c1 = f6add(ab, ab)
+    return (c0, c1)
+
+
+LINE_COORDS = (0, 1, 2, 3, 8, 9)  # line = (A + B v) + (C v) w: Fp2 slots c0.c0, c0.c1, c1.c1
+
+
+def sym12_line(prefix):
+    v = [Lin({(prefix, k): 1}) if k in LINE_COORDS else Lin() for k in range(12)]
+    f2 = [(v[2 * i], v[2 * i + 1]) for i in range(6)]
+    return ((f2[0], f2[1], f2[2]), (f2[3], f2[4], f2[5]))
+
+
 def sym12(prefix):
     v = [Lin({(prefix, k): 1}) for k in range(12)]
     f2 = [(v[2 * i], v[2 * i + 1]) for i in range(6)]
@@ -158,6 +177,12 @@ def tables(kind):
     if kind == "mul":
         res = f12mul(C, sym12("x"), sym12("y"))
         ys = "y"
+    elif kind == "line":
+        res = f12mul(C, sym12("x"), sym12_line("y"))
+        ys = "y"
+    elif kind == "sqr":
+        res = f12sqr(C, sym12("x"))
+        ys = "x"
     else:
         res = cycsqr(C, sym12("x"))
         ys = "x"
@@ -184,8 +209,13 @@ def check(kind, A, B, POST, LIN):
             x = flat_vals(t)
             y = x
             exp = flat_vals(O.f12_mul(t, t))
+        elif kind == "sqr":
+            y = x
+            exp = flat_vals(O.f12_mul(unflat(x), unflat(x)))
         else:
             y = [rng.randrange(P) for _ in range(12)]
+            if kind == "line":
+                y = [v if k in LINE_COORDS else 0 for k, v in enumerate(y)]
             exp = flat_vals(O.f12_mul(unflat(x), unflat(y)))
         prods = [sum(a * xv for a, xv in zip(Aj, x)) * sum(b * yv for b, yv in zip(Bj, y)) % P for Aj, Bj in zip(A, B)]
         got = [(sum(c * pv for c, pv in zip(Pi, prods)) + sum(c * xv for c, xv in zip(Li, x))) % P for Pi, Li in zip(POST, LIN)]
@@ -220,7 +250,7 @@ def emit_rows(name, rows):
 
 def main():
     out = ["// GENERATED by tools/gen_fp12_wave.py -- do not edit.", "#pragma once", "#include <stdint.h>", "namespace tb {"]
-    for kind, pre in (("mul", "W12M"), ("cyc", "W12C")):
+    for kind, pre in (("mul", "W12M"), ("cyc", "W12C"), ("sqr", "W12S"), ("line", "W12L")):
         A, B, POST, LIN = tables(kind)
         check(kind, A, B, POST, LIN)
         out.append("// %s: %d products" % (kind, len(A)))
