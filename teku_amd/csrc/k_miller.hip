@@ -56,6 +56,7 @@ extern "C" __global__ void __launch_bounds__(64)
     if (threadIdx.x < 12) out[threadIdx.x] = threadIdx.x == 0 ? fp_one() : fp_zero();
     return;
   }
+  w12_tabs_load(L.s);
   miller_loop_wave(L, P[i], Q[i]);
   if (threadIdx.x < 12) out[threadIdx.x] = L.F[threadIdx.x];
 }
@@ -72,6 +73,7 @@ extern "C" __global__ void __launch_bounds__(64)
     if (threadIdx.x < 12) out[threadIdx.x] = threadIdx.x == 0 ? fp_one() : fp_zero();
     return;
   }
+  w12_tabs_load(L.s);
   miller_loop_wave(L, P[slot], Q[slot]);
   if (threadIdx.x < 12) out[threadIdx.x] = L.F[threadIdx.x];
 }

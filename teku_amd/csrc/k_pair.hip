@@ -35,6 +35,7 @@ extern "C" __global__ void __launch_bounds__(64)
   uint32_t e = b + chunk;
   if (e > n) e = n;
   if (b >= e) return;
+  w12_tabs_load(L.s);
   w_load(L.A, in + b);
   for (uint32_t i = b + 1; i < e; i++) {
     w_load(L.X, in + i);
@@ -49,6 +50,7 @@ extern "C" __global__ void __launch_bounds__(64) k_final_verify_wave(const fp12*
                                                                      const uint32_t* __restrict__ n_bad, int* __restrict__ result) {
   __shared__ final_exp_lds L;
   tb_latency_prio();
+  w12_tabs_load(L.s);
   w_load(L.F, f);
   for (uint32_t i = 1; i < g; i++) {
     w_load(L.X, f + i);

@@ -14,81 +14,87 @@
 
 namespace tb {
 
-// LDS scratch for the wave ops
+// LDS scratch for the wave ops: product / partial-sum exchange and the
+// coefficient tables (staged from W12_ALL once per kernel by w12_tabs_load, so
+// the lane-varying table reads are LDS reads, not global loads).
+#define W12_QP 5  // lanes per output coordinate in the post-combination
 struct wave12_scratch {
   fp prod[64];
-  fp part[48];
+  fp part[12 * W12_QP];
+  uint16_t tab[W12_ALL_N];
 };
 
+__device__ TB_INLINE void w12_tabs_load(wave12_scratch& s) {
+  for (int i = threadIdx.x; i < W12_ALL_N; i += blockDim.x) s.tab[i] = W12_ALL[i];
+  __syncthreads();
+}
+
+// sum_{t in [b, e)} +-src[idx_t]; entries (idx << 1) | negative; at most
+// MAXLEN terms (unrolled and predicated so the LDS reads issue early)
+template <int MAXLEN>
 __device__ TB_INLINE fp w_sparse_sum(const fp* src, const uint16_t* ent, int b, int e) {
   fp acc = fp_zero();
-  for (int t = b; t < e; t++) {
-    const uint32_t x = ent[t];
-    const int idx = (int)(x >> 4);
-    int c = (int)(x & 15u);
-    if (c >= 8) c -= 16;
-    fp v = src[idx];
-    if (c < 0) {
-      c = -c;
-      v = fp_neg(v);
+  TB_UNROLL for (int t = 0; t < MAXLEN; t++) {
+    if (b + t < e) {
+      const uint32_t x = ent[b + t];
+      const fp v = src[x >> 1];
+      fp nv;
+      uint32_t br = 0;
+      TB_UNROLL for (int i = 0; i < 12; i++) nv.l[i] = subc32(P2_MOD[i], v.l[i], br, &br);  // 2p - v in (0, 2p]
+      acc = fp_add(acc, fp_sel((x & 1u) != 0, nv, v));
     }
-    for (int k = 0; k < c; k++) acc = fp_add(acc, v);
   }
   return acc;
 }
 
-// generic bilinear op: dst = POST(prod(A x, B y)) + LIN x
-template <int NPROD>
-__device__ TB_INLINE void w_bilinear(fp* dst, const fp* x, const fp* y, wave12_scratch& s, const uint16_t* aoff,
-                                     const uint16_t* aent, const uint16_t* boff, const uint16_t* bent, const uint16_t* poff,
-                                     const uint16_t* pent, const uint16_t* loff, const uint16_t* lent) {
+// generic bilinear op: dst = POST(prod(A x, B y)) + LIN x, tables at offsets
+// in s.tab (tb_fp12_wave_tables.h)
+template <int NPROD, int AOFF, int AENT, int AMAX, int BOFF, int BENT, int BMAX, int POFF, int PENT, int PMAX, int LOFF,
+          int LENT, int LMAX>
+__device__ TB_INLINE void w_bilinear(fp* dst, const fp* x, const fp* y, wave12_scratch& s) {
   const int l = threadIdx.x;
+  const uint16_t* T = s.tab;
   if (l < NPROD) {
-    fp a = w_sparse_sum(x, aent, aoff[l], aoff[l + 1]);
-    fp b = w_sparse_sum(y, bent, boff[l], boff[l + 1]);
+    const fp a = w_sparse_sum<AMAX>(x, T + AENT, T[AOFF + l], T[AOFF + l + 1]);
+    const fp b = w_sparse_sum<BMAX>(y, T + BENT, T[BOFF + l], T[BOFF + l + 1]);
     s.prod[l] = fp_mul(a, b);
   }
   __syncthreads();
-  if (l < 48) {
-    const int i = l >> 2, q = l & 3;
-    const int b0 = poff[i], e0 = poff[i + 1];
-    const int chunk = (e0 - b0 + 3) >> 2;
+  if (l < 12 * W12_QP) {
+    const int i = l / W12_QP, q = l - i * W12_QP;
+    const int b0 = T[POFF + i], e0 = T[POFF + i + 1];
+    const int chunk = (e0 - b0 + W12_QP - 1) / W12_QP;
     int lo = b0 + q * chunk, hi = lo + chunk;
     if (hi > e0) hi = e0;
     if (lo > e0) lo = e0;
-    s.part[l] = w_sparse_sum(s.prod, pent, lo, hi);
+    s.part[l] = w_sparse_sum<(PMAX + W12_QP - 1) / W12_QP>(s.prod, T + PENT, lo, hi);
   }
   __syncthreads();
   fp r;
   if (l < 12) {
-    r = fp_add(fp_add(s.part[4 * l], s.part[4 * l + 1]), fp_add(s.part[4 * l + 2], s.part[4 * l + 3]));
-    r = fp_add(r, w_sparse_sum(x, lent, loff[l], loff[l + 1]));
+    r = s.part[W12_QP * l];
+    TB_UNROLL for (int q = 1; q < W12_QP; q++) r = fp_add(r, s.part[W12_QP * l + q]);
+    if (LMAX > 0) r = fp_add(r, w_sparse_sum<LMAX>(x, T + LENT, T[LOFF + l], T[LOFF + l + 1]));
   }
   __syncthreads();
   if (l < 12) dst[l] = r;
   __syncthreads();
 }
 
-__device__ TB_INLINE void w_mul(fp* dst, const fp* x, const fp* y, wave12_scratch& s) {
-  w_bilinear<W12M_NPROD>(dst, x, y, s, W12M_A_OFF, W12M_A_ENT, W12M_B_OFF, W12M_B_ENT, W12M_POST_OFF, W12M_POST_ENT, W12M_LIN_OFF,
-                         W12M_LIN_ENT);
-}
+#define W12_TABS(P)                                                                                                 \
+  P##_NPROD, P##_A_OFF, P##_A_ENT, P##_A_MAXLEN, P##_B_OFF, P##_B_ENT, P##_B_MAXLEN, P##_POST_OFF, P##_POST_ENT, \
+      P##_POST_MAXLEN, P##_LIN_OFF, P##_LIN_ENT, P##_LIN_MAXLEN
 
-__device__ TB_INLINE void w_cyc_sqr(fp* dst, const fp* x, wave12_scratch& s) {
-  w_bilinear<W12C_NPROD>(dst, x, x, s, W12C_A_OFF, W12C_A_ENT, W12C_B_OFF, W12C_B_ENT, W12C_POST_OFF, W12C_POST_ENT, W12C_LIN_OFF,
-                         W12C_LIN_ENT);
-}
+__device__ TB_INLINE void w_mul(fp* dst, const fp* x, const fp* y, wave12_scratch& s) { w_bilinear<W12_TABS(W12M)>(dst, x, y, s); }
+
+__device__ TB_INLINE void w_cyc_sqr(fp* dst, const fp* x, wave12_scratch& s) { w_bilinear<W12_TABS(W12C)>(dst, x, x, s); }
 
 // general Fp12 squaring (tb_tower.h fp12_sqr: 36 products)
-__device__ TB_INLINE void w_sqr(fp* dst, const fp* x, wave12_scratch& s) {
-  w_bilinear<W12S_NPROD>(dst, x, x, s, W12S_A_OFF, W12S_A_ENT, W12S_B_OFF, W12S_B_ENT, W12S_POST_OFF, W12S_POST_ENT, W12S_LIN_OFF,
-                         W12S_LIN_ENT);
-}
+__device__ TB_INLINE void w_sqr(fp* dst, const fp* x, wave12_scratch& s) { w_bilinear<W12_TABS(W12S)>(dst, x, x, s); }
 
 // x * line, line dense in coordinates 0,1 (A), 2,3 (B), 8,9 (C), zero elsewhere (39 products)
 __device__ TB_INLINE void w_mul_line(fp* dst, const fp* x, const fp* ln, wave12_scratch& s) {
-  w_bilinear<W12L_NPROD>(dst, x, ln, s, W12L_A_OFF, W12L_A_ENT, W12L_B_OFF, W12L_B_ENT, W12L_POST_OFF, W12L_POST_ENT, W12L_LIN_OFF,
-                         W12L_LIN_ENT);
+  w_bilinear<W12_TABS(W12L)>(dst, x, ln, s);
 }
 
 __device__ TB_INLINE void w_copy(fp* dst, const fp* x) {

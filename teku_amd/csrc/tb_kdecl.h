@@ -70,3 +70,4 @@ extern "C" __global__ void k_final_verify_wave(const fp12* __restrict__ f, uint3
 extern "C" __global__ void k_final_verify(const fp12* __restrict__ f, const uint32_t* __restrict__ n_bad, int* __restrict__ result);
 extern "C" __global__ void k_test_ops(int op, const uint8_t* in, uint8_t* out, uint32_t n);
 extern "C" __global__ void k_test_final_exp_wave(const uint8_t* in, uint8_t* out);
+extern "C" __global__ void k_test_miller_wave(const uint8_t* in, uint8_t* out);

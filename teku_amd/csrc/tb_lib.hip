@@ -860,6 +860,10 @@ extern "C" int tbls_test_ops(int op, const uint8_t* in, uint8_t* out, size_t n) 
       hipLaunchKernelGGL(k_test_final_exp_wave, dim3(n), dim3(64), 0, c.stream, c.in.as<uint8_t>(), c.ws.as<uint8_t>());
       return fetch(c, out, c.ws.p, n * TB_TEST_OUT);
     }
+    if (op == 31) {  // TOP_MILLER_WAVE: one 64-lane block per record
+      hipLaunchKernelGGL(k_test_miller_wave, dim3(n), dim3(64), 0, c.stream, c.in.as<uint8_t>(), c.ws.as<uint8_t>());
+      return fetch(c, out, c.ws.p, n * TB_TEST_OUT);
+    }
     hipLaunchKernelGGL(k_test_ops, dim3((n + TB_BLOCK - 1) / TB_BLOCK), dim3(TB_BLOCK), 0, c.stream, op, c.in.as<uint8_t>(), c.ws.as<uint8_t>(),
                        (uint32_t)n);
     return fetch(c, out, c.ws.p, n * TB_TEST_OUT);

@@ -134,3 +134,16 @@ def test_miller2_shared_accumulator(run):
     rec = enc_fp(P0[0]) + enc_fp(P0[1]) + enc_fp2(Q0[0]) + enc_fp2(Q0[1]) + enc_fp(P1[0]) + enc_fp(P1[1]) + enc_fp2(Q1[0]) + enc_fp2(Q1[1])
     f = dec_fp12(run("MILLER2", [rec])[0])
     assert O.final_exponentiation(f) == O.f12_mul(O.pairing(P0, Q0), O.pairing(P1, Q1))
+
+
+def test_miller_wave_matches_single_lane(run):
+    """k_miller_wave's loop (tb_fp12_wave.h miller_loop_wave: lane-parallel
+    f^2, doubling step and line products) == the one-thread miller_loop, as
+    field elements, and pairs to e(P, Q) after the final exponentiation."""
+    P1 = O.jac_to_affine(O.FP, O.jac_mul(O.FP, O.jac_from_affine(O.FP, O.G1_GEN), 12345))
+    pairs = [(O.G1_GEN, O.G2_GEN), (P1, O.hash_to_g2(b"wave miller")), (O.G1_GEN, O.hash_to_g2(b"x" * 32))]
+    recs = [enc_fp(P[0]) + enc_fp(P[1]) + enc_fp2(Q[0]) + enc_fp2(Q[1]) for P, Q in pairs]
+    single = [dec_fp12(x) for x in run("MILLER", recs)]
+    wave = [dec_fp12(x) for x in run("MILLER_WAVE", recs)]
+    assert wave == single
+    assert O.final_exponentiation(wave[1]) == O.pairing(*pairs[1])

@@ -234,36 +234,42 @@ def unflat(x):
     return ((tuple(x[0:2]), tuple(x[2:4]), tuple(x[4:6])), (tuple(x[6:8]), tuple(x[8:10]), tuple(x[10:12])))
 
 
-def emit_rows(name, rows):
-    """Sparse rows: entries (index << 4) | (coeff & 15), coeff in [-8, 7]; offsets table."""
+def rows_entries(rows):
+    """Sparse rows with every coefficient expanded to |c| entries of +-1:
+    entry = (index << 1) | negative; returns (offsets, entries)."""
     offs, ents = [0], []
     for r in rows:
         for k, c in enumerate(r):
-            if c:
-                assert -8 <= c <= 7, (name, c)
-                ents.append((k << 4) | (c & 15))
+            for _ in range(abs(c)):
+                ents.append((k << 1) | (1 if c < 0 else 0))
         offs.append(len(ents))
-    s = "TB_CONST uint16_t %s_OFF[%d] = {%s};\n" % (name, len(offs), ", ".join(map(str, offs)))
-    s += "TB_CONST uint16_t %s_ENT[%d] = {%s};\n" % (name, max(1, len(ents)), ", ".join(map(str, ents or [0])))
-    return s, max(offs[i + 1] - offs[i] for i in range(len(rows)))
+    return offs, ents
 
 
 def main():
     out = ["// GENERATED by tools/gen_fp12_wave.py -- do not edit.", "#pragma once", "#include <stdint.h>", "namespace tb {"]
+    allv = []
     for kind, pre in (("mul", "W12M"), ("cyc", "W12C"), ("sqr", "W12S"), ("line", "W12L")):
         A, B, POST, LIN = tables(kind)
         check(kind, A, B, POST, LIN)
         out.append("// %s: %d products" % (kind, len(A)))
         out.append("#define %s_NPROD %d" % (pre, len(A)))
         for nm, rows in (("A", A), ("B", B), ("POST", POST), ("LIN", LIN)):
-            s, mx = emit_rows(pre + "_" + nm, rows)
-            out.append(s.rstrip())
-            out.append("#define %s_%s_MAXLEN %d" % (pre, nm, mx))
+            offs, ents = rows_entries(rows)
+            out.append("#define %s_%s_OFF %d" % (pre, nm, len(allv)))
+            allv += offs
+            out.append("#define %s_%s_ENT %d" % (pre, nm, len(allv)))
+            allv += ents or [0]
+            out.append("#define %s_%s_MAXLEN %d" % (pre, nm, max(offs[i + 1] - offs[i] for i in range(len(rows)))))
         print(kind, "products", len(A), "max |coeff| post", max(abs(c) for r in POST for c in r))
+    assert max(allv) < 65536
+    out.append("// all tables, concatenated; staged into LDS (wave12_scratch.tab) by w12_tabs_load")
+    out.append("#define W12_ALL_N %d" % len(allv))
+    out.append("TB_CONST uint16_t W12_ALL[%d] = {%s};" % (len(allv), ", ".join(map(str, allv))))
     out.append("}  // namespace tb")
     path = os.path.join(ROOT, "teku_amd", "csrc", "tb_fp12_wave_tables.h")
     open(path, "w").write("\n".join(out) + "\n")
-    print("wrote", path)
+    print("wrote", path, "entries", len(allv))
 
 
 if __name__ == "__main__":
