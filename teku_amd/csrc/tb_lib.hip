@@ -90,10 +90,19 @@ size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
 // --------------------------------------------------------------------------
 // Fp12 product levels: each wave multiplies TB_PROD_CHUNK values (k_fp12_prod_wave)
 #define TB_PROD_CHUNK 16u
+// From this many sets on, S = sum r_i sig_i is a bucket MSM (k_msm_*, k_sigs.hip)
+// instead of one [r_i] sig_i per set plus a tree sum.
+#define TB_MSM_MIN 32768u
+#define TB_MSM_BUCKETS 2048u   // 8 windows x 256 digits
+#define TB_MSM_PARTS 32768u    // buckets x 16 chunks
+#define TB_MSM_WSEGS 512u      // 8 windows x 64 digit segments
 struct ws_layout {
-  size_t pk_aff, pk_code, P, Q, skip, set_code, sig_code, rsig, f, gpart, fpart, fpart2, n_bad, result, total;
+  size_t pk_aff, pk_code, P, Q, skip, set_code, sig_code, rsig, f, gpart, fpart, fpart2, n_bad, result;
+  size_t sig_aff, sig_use, msm_cnt, msm_off, msm_cur, msm_idx, msm_part, msm_bucket, msm_wseg, msm_wsum, total;
   uint32_t nb_g2, nb_f;
+  bool msm;
   ws_layout(uint32_t n, uint32_t K) {
+    msm = n >= TB_MSM_MIN;
     const uint32_t np = n + 1;
     nb_g2 = (n + TB_BLOCK - 1) / TB_BLOCK;
     if (nb_g2 > 256) nb_g2 = 256;
@@ -107,7 +116,18 @@ struct ws_layout {
     skip = o;     o = align_up(o + np);
     set_code = o; o = align_up(o + n);
     sig_code = o; o = align_up(o + n);
-    rsig = o;     o = align_up(o + (size_t)n * sizeof(g2j));
+    rsig = o;     o = align_up(o + (msm ? 0 : (size_t)n * sizeof(g2j)));
+    const size_t nm = msm ? n : 0;
+    sig_aff = o;  o = align_up(o + nm * sizeof(g2a));
+    sig_use = o;  o = align_up(o + nm);
+    msm_cnt = o;  o = align_up(o + (msm ? TB_MSM_BUCKETS * 4 : 0));
+    msm_off = o;  o = align_up(o + (msm ? (TB_MSM_BUCKETS + 1) * 4 : 0));
+    msm_cur = o;  o = align_up(o + (msm ? TB_MSM_BUCKETS * 4 : 0));
+    msm_idx = o;  o = align_up(o + nm * 8 * 4);
+    msm_part = o; o = align_up(o + (msm ? (size_t)TB_MSM_PARTS * sizeof(g2j) : 0));
+    msm_bucket = o; o = align_up(o + (msm ? (size_t)TB_MSM_BUCKETS * sizeof(g2j) : 0));
+    msm_wseg = o; o = align_up(o + (msm ? TB_MSM_WSEGS * sizeof(g2j) : 0));
+    msm_wsum = o; o = align_up(o + (msm ? 8 * sizeof(g2j) : 0));
     f = o;        o = align_up(o + (size_t)np * sizeof(fp12));
     gpart = o;    o = align_up(o + (size_t)nb_g2 * sizeof(g2j));
     fpart = o;    o = align_up(o + (size_t)nb_f * sizeof(fp12));
@@ -137,7 +157,7 @@ struct ws_layout {
 //    loop (half the latency of the two-pair accumulator).
 // TBLS_SERIAL=1 (or `serial`) runs everything on the caller's stream, for
 // exclusive per-stage timings.
-#define TB_SIG_FIRST_MIN 32768u
+#define TB_SIG_FIRST_MIN TB_MSM_MIN
 #define TB_MILLER1_MAX 4096u
 // up to this many sets, one pair per 64-lane workgroup (k_miller_wave);
 // TBLS_MILLER_WAVE_MAX overrides (tuning)
@@ -171,9 +191,13 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
     HIPCHK(hipStreamWaitEvent(sa, c.e_fork, 0));
     HIPCHK(hipStreamWaitEvent(sb, c.e_fork, 0));
   }
-  // signatures: decompress, G2 subgroup check, [r]sig
+  // signatures: decompress, G2 subgroup check (+ [r]sig per set without the MSM)
   TB_EV(4, ss);
-  if (n) hipLaunchKernelGGL(k_set_sig, g, blk, 0, ss, b.sigs, b.rand, n, (g2j*)(w + L.rsig), w + L.sig_code, (uint32_t*)(w + L.n_bad));
+  if (L.msm)
+    hipLaunchKernelGGL(k_sig_check, g, blk, 0, ss, b.sigs, n, (g2a*)(w + L.sig_aff), w + L.sig_use, w + L.sig_code,
+                       (uint32_t*)(w + L.n_bad));
+  else if (n)
+    hipLaunchKernelGGL(k_set_sig, g, blk, 0, ss, b.sigs, b.rand, n, (g2j*)(w + L.rsig), w + L.sig_code, (uint32_t*)(w + L.n_bad));
   TB_EV(5, ss);
   HIPCHK(hipEventRecord(c.e_sig, ss));
   if (sig_first) {
@@ -182,12 +206,29 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
   }
   // stream b: the G2 sum, then the Miller loop of the (-g1, S) pair
   TB_EV(8, sb);
+  if (L.msm) {
+    uint32_t* cnt = (uint32_t*)(w + L.msm_cnt);
+    uint32_t* off = (uint32_t*)(w + L.msm_off);
+    uint32_t* cur = (uint32_t*)(w + L.msm_cur);
+    uint32_t* idx = (uint32_t*)(w + L.msm_idx);
+    HIPCHK(hipMemsetAsync(cnt, 0, TB_MSM_BUCKETS * 4, sb));
+    hipLaunchKernelGGL(k_msm_hist, g, blk, 0, sb, b.rand, w + L.sig_use, n, cnt);
+    hipLaunchKernelGGL(k_msm_scan, dim3(1), dim3(256), 0, sb, (const uint32_t*)cnt, off, cur);
+    hipLaunchKernelGGL(k_msm_scatter, g, blk, 0, sb, b.rand, w + L.sig_use, n, cur, idx);
+    hipLaunchKernelGGL(k_msm_bucket, dim3(TB_MSM_PARTS / TB_BLOCK), blk, 0, sb, (const g2a*)(w + L.sig_aff), (const uint32_t*)off,
+                       (const uint32_t*)idx, (g2j*)(w + L.msm_part));
+    hipLaunchKernelGGL(k_msm_bsum, dim3(TB_MSM_BUCKETS / TB_BLOCK), blk, 0, sb, (const g2j*)(w + L.msm_part), (g2j*)(w + L.msm_bucket));
+    hipLaunchKernelGGL(k_msm_window, dim3(TB_MSM_WSEGS / TB_BLOCK), blk, 0, sb, (const g2j*)(w + L.msm_bucket), (g2j*)(w + L.msm_wseg));
+    hipLaunchKernelGGL(k_msm_final, dim3(1), dim3(64), 0, sb, (const g2j*)(w + L.msm_wseg), (g2j*)(w + L.msm_wsum), n, (g1a*)(w + L.P),
+                       (g2a*)(w + L.Q), w + L.skip);
+  } else {
   if (n)
     hipLaunchKernelGGL(k_g2_sum_partial, dim3(L.nb_g2), blk, 0, sb, (const g2j*)(w + L.rsig), n, (g2j*)(w + L.gpart));
   else
     HIPCHK(hipMemsetAsync(w + L.gpart, 0, sizeof(g2j), sb));  // z = 0 -> infinity
   hipLaunchKernelGGL(k_g2_sum_final, dim3(1), blk, 0, sb, (const g2j*)(w + L.gpart), L.nb_g2, n, (g1a*)(w + L.P), (g2a*)(w + L.Q),
                      w + L.skip);
+  }
   TB_EV(9, sb);
   hipLaunchKernelGGL(k_miller_one_wave, dim3(1), dim3(64), 0, sb, (const g1a*)(w + L.P), (const g2a*)(w + L.Q), w + L.skip, n,
                      (fp12*)(w + L.f) + nthr);

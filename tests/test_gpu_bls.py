@@ -305,3 +305,41 @@ def test_spi_prepare_complete_combinatorics(hip):
     eager = bls.HipBLS12381(eager=True)
     with pytest.raises(ValueError):  # BlstTest.succeedsWhenPrepareBatchVerifyNotInG2ThrowsException
         eager.prepare_batch_verify(0, [pks[0]], msgs[0], bls.HipSignature(NOT_IN_G2))
+
+
+def test_large_batch_msm_path(hip):
+    """Batches of >= 32768 sets take the bucket-MSM path for sum r_i sig_i
+    (k_sig_check + k_msm_*) instead of per-set [r_i] sig_i: valid -> True;
+    a signature on the wrong message, an infinity signature, a duplicated
+    signature pair (bucket doubling case) and a non-G2 point -> False.
+    Keys / signatures come from the GPU generators (interop keys), which
+    test_hash_sign_keys_bit_exact pins to the oracle."""
+    bls, native, L, impl = hip
+    n = 32768
+    nk = 512
+    sks = b"".join(interop_sk(i % nk).to_bytes(32, "big") for i in range(n))
+    pk_out = ctypes.create_string_buffer(48 * nk)
+    native.check(L.tbls_sk_to_pk_many(sks[: 32 * nk], nk, pk_out), "sk_to_pk_many")
+    msgs = [i.to_bytes(4, "little") * 8 for i in range(n)]
+    off = (ctypes.c_uint32 * (n + 1))(*[32 * j for j in range(n + 1)])
+    sig_out = ctypes.create_string_buffer(96 * n)
+    dst = b"BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_POP_"
+    native.check(L.tbls_sign_many(sks, b"".join(msgs), off, n, dst, len(dst), sig_out), "sign_many")
+    pks = [pk_out.raw[48 * (i % nk) : 48 * (i % nk) + 48] for i in range(n)]
+    sigs = [sig_out.raw[96 * i : 96 * i + 96] for i in range(n)]
+    rng = random.Random(7)
+    rands = [rng.getrandbits(64) | 1 for _ in range(n)]
+    assert _raw(bls, pks, msgs, sigs, rands)
+    bad = list(sigs)
+    bad[12345] = sigs[12346]
+    assert not _raw(bls, pks, msgs, bad, rands)
+    bad = list(sigs)
+    bad[777] = bytes([0xC0]) + bytes(95)
+    assert not _raw(bls, pks, msgs, bad, rands)
+    bad = list(sigs)
+    bad[5] = NOT_IN_G2
+    assert not _raw(bls, pks, msgs, bad, rands)
+    # the same (pk, msg, sig) twice with the same randomizer: equal points in one bucket
+    dup_p, dup_m, dup_s, dup_r = list(pks), list(msgs), list(sigs), list(rands)
+    dup_p[1], dup_m[1], dup_s[1], dup_r[1] = pks[0], msgs[0], sigs[0], rands[0]
+    assert _raw(bls, dup_p, dup_m, dup_s, dup_r)
