@@ -229,6 +229,38 @@ def main():
 
     total_sets = S * world * args.steps
     value = total_sets / dt
+
+    # Same steps with the keys in the device-resident validator table
+    # (tbls_pk_table_load / tbls_dev_batch_partial_idx):
+    # keys decompressed and validated once, as Teku memoizes them per
+    # BLSPublicKey.  Reported beside `value`, which decodes every key per step.
+    T = min(S, 65536)
+    native.check(L.tbls_pk_table_load(pks[: 48 * T], T, None), "pk_table_load")
+    key_idx = torch.arange(0, S, dtype=torch.int32, device=device) % T
+
+    def step_tab():
+        native.check(L.tbls_dev_batch_partial_idx(local, ctypes.byref(batch.desc), key_idx.data_ptr(), stream, partial.data_ptr()), "partial_idx")
+        src = all_gather_partials(partial)
+        if rank == 0:
+            native.check(L.tbls_dev_final_verify(local, src.data_ptr(), world, stream, ctypes.byref(ok)), "final")
+            if ok.value != 1:
+                raise RuntimeError("valid synthetic batch rejected (key table)")
+
+    step_tab()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step_tab()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt_tab = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt_tab], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt_tab = float(t.item())
     if rank != 0:
         dist.barrier()
         dist.destroy_process_group()
@@ -279,6 +311,10 @@ def main():
             "sets_per_gpu": S,
             "parallelism": "data-parallel shards, dp%d" % world,
         },
+        "value_key_table": total_sets / dt_tab,
+        "ms_per_step_key_table": dt_tab / args.steps * 1e3,
+        "key_table": "value_key_table: same steps with keys from the device-resident validator table (%d keys decompressed "
+        "and validated once, as Teku memoizes BLSPublicKey); value decodes and group-checks every key per step" % T,
         "p50_latency_ms_128": statistics.median(lat),
         "p99_latency_ms_128": lat[min(len(lat) - 1, int(0.99 * len(lat)))],
         "stage_ms_overlapped": dict(zip(STAGES, stage_ms)),

@@ -111,6 +111,35 @@ typedef struct {
  * TBLS_BAD_ARGUMENT (BlstPublicKey.aggregate checkArgument, l.56). */
 int tbls_batch_verify(const tbls_set* sets, size_t n, const uint64_t* rand, int n_gpus, int* ok, tbls_timing* t);
 
+/* ---- device-resident validator public-key table ----
+ * Teku memoizes each key's decompression and validity per BLSPublicKey object
+ * (BlstPublicKey.fromBytes / isInfinity / isInGroup, BlstPublicKey.java:38-45,
+ * 74-75, 93-104) and looks keys up by validator index
+ * (BeaconStateAccessors.getValidatorPubKey, spec/.../helpers/
+ * BeaconStateAccessors.java:78-97).  tbls_pk_table_load makes that memo
+ * device-resident: the K keys are decompressed and validated once on every
+ * device (96-byte affine + status per key in HBM) and batches name keys by
+ * index, so no key bytes travel and no key is decompressed per call.
+ * Replaces any previous table.  codes (nullable, K bytes): per-key status as
+ * tbls_pk_validate (TBLS_SUCCESS, TBLS_PK_IS_INFINITY, ...). */
+int tbls_pk_table_load(const uint8_t* pks, size_t K, uint8_t* codes);
+size_t tbls_pk_table_size(void);
+
+/* A signature set whose keys are table indices (the unit of
+ * BLS.prepareBatchVerify, BLS.java:353-368, with keys by validator index). */
+typedef struct {
+  const uint32_t* key_idx;
+  uint32_t n_pks;
+  const uint8_t* msg;
+  uint32_t msg_len;
+  const uint8_t* sig;
+} tbls_set_idx;
+
+/* tbls_batch_verify with keys from the table; same semantics (an invalid
+ * table key makes its set invalid, BlstPublicKey.aggregate l.58-65).  An
+ * index >= tbls_pk_table_size() -> TBLS_BAD_ARGUMENT. */
+int tbls_batch_verify_idx(const tbls_set_idx* sets, size_t n, const uint64_t* rand, int n_gpus, int* ok, tbls_timing* t);
+
 /* fastAggregateVerify per set (BLS.java:185-207, BlstSignature.java:125-129):
  * ok_per_set[i] in {0,1}; an empty key list gives 0. */
 int tbls_fast_aggregate_verify_many(const tbls_set* sets, size_t n, int* ok_per_set);
@@ -139,6 +168,11 @@ typedef struct {
 #define TBLS_PARTIAL_BYTES 580
 
 int tbls_dev_batch_partial(int device, const tbls_dev_batch* b, void* stream, void* partial_out);
+
+/* tbls_dev_batch_partial with keys from `device`'s resident table: b->pks is
+ * ignored and key_idx (device memory, b->n_keys entries, addressed through
+ * b->pk_off) indexes the table.  No table -> TBLS_BAD_ARGUMENT. */
+int tbls_dev_batch_partial_idx(int device, const tbls_dev_batch* b, const uint32_t* key_idx, void* stream, void* partial_out);
 
 /* Same as tbls_dev_batch_partial, also returning the per-stage device time
  * (HIP events on `stream`) in stage_ms[7]: pk decompress, set pk

@@ -379,6 +379,50 @@ def batch_verify_raw(sets, rands, n_gpus=0, timing=None) -> bool:
     return ok.value == 1
 
 
+class ValidatorKeyTable:
+    """Device-resident validator public-key table (SURVEY.md 8(f) rank 1;
+    C ABI tbls_pk_table_load / tbls_batch_verify_idx).
+
+    Teku memoizes each key's decompression and validity per BLSPublicKey
+    (BlstPublicKey.java:38-45, 74-75, 93-104) and fetches keys by validator
+    index (BeaconStateAccessors.getValidatorPubKey, BeaconStateAccessors.java:
+    78-97); this keeps that memo in HBM on every device, so batches name keys
+    by index.  `codes[i]` is key i's status (0 = valid, as tbls_pk_validate)."""
+
+    def __init__(self, pks):
+        blob = b"".join(bytes(p) for p in pks)
+        self.size = len(pks)
+        codes = ctypes.create_string_buffer(max(1, self.size))
+        rc = native.lib().tbls_pk_table_load(blob, self.size, codes)
+        if rc == native.BAD_ARGUMENT:
+            raise ValueError("empty key table")
+        native.check(rc, "tbls_pk_table_load")
+        self.codes = list(codes.raw[: self.size])
+
+    def batch_verify(self, sets, rands, n_gpus=0) -> bool:
+        """BLS.batchVerify over [(key_indices, msg, sig96)] (same semantics as
+        batch_verify_raw with the keys' bytes)."""
+        n = len(sets)
+        arr = (native.TblsSetIdx * max(1, n))()
+        keep = []
+        for i, (idx, msg, sig) in enumerate(sets):
+            ib = (ctypes.c_uint32 * max(1, len(idx)))(*idx)
+            mb, sb = _buf(msg), _buf(sig)
+            keep += [ib, mb, sb]
+            arr[i].key_idx = ctypes.cast(ib, ctypes.c_void_p)
+            arr[i].n_pks = len(idx)
+            arr[i].msg = ctypes.cast(mb, ctypes.c_void_p)
+            arr[i].msg_len = len(msg)
+            arr[i].sig = ctypes.cast(sb, ctypes.c_void_p)
+        rr = (ctypes.c_uint64 * max(1, n))(*rands)
+        ok = ctypes.c_int(0)
+        rc = native.lib().tbls_batch_verify_idx(arr, n, rr, n_gpus, ctypes.byref(ok), None)
+        if rc == native.BAD_ARGUMENT:
+            raise ValueError("key index out of range / empty key list")
+        native.check(rc, "tbls_batch_verify_idx")
+        return ok.value == 1
+
+
 def _as_pk(pk) -> HipPublicKey:
     if isinstance(pk, HipPublicKey):
         return pk

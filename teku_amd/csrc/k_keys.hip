@@ -17,15 +17,16 @@ extern "C" __global__ void __launch_bounds__(TB_BLOCK)
   pk_code[i] = (uint8_t)code;
 }
 
-// per set: aggregate keys (BlstPublicKey.aggregate semantics), P = [r] apk (affine)
+// per set: aggregate keys (BlstPublicKey.aggregate semantics), P = [r] apk (affine);
+// key_idx (nullable): keys come from the device-resident table (pk_aff/pk_code = the table)
 extern "C" __global__ void __launch_bounds__(TB_BLOCK)
     k_set_pk(const uint32_t* __restrict__ pk_off, const g1a* __restrict__ pk_aff, const uint8_t* __restrict__ pk_code,
              const uint64_t* __restrict__ rand, uint32_t n, g1a* __restrict__ P, uint8_t* __restrict__ set_code,
-             uint32_t* __restrict__ n_bad) {
+             uint32_t* __restrict__ n_bad, const uint32_t* __restrict__ key_idx) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   g1a out;
-  int code = stage_set_pk(pk_aff, pk_code, pk_off[i], pk_off[i + 1], rand[i], out);
+  int code = stage_set_pk(pk_aff, pk_code, pk_off[i], pk_off[i + 1], rand[i], out, key_idx);
   P[i] = out;
   if (code != TB_SUCCESS) {
     set_code[i] = (uint8_t)code;

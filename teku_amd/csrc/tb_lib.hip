@@ -11,6 +11,7 @@
 #include <cstring>
 #include <mutex>
 #include <thread>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/tekubls.h"
@@ -75,6 +76,8 @@ struct dev_ctx {
   dbuf fin;     // final-exponentiation scratch
   dbuf dstb;    // default DST for the device-resident API
   hipStream_t aux[2] = {nullptr, nullptr};  // concurrent per-set stages
+  dbuf tab_aff, tab_code;                    // device-resident public-key table (tbls_pk_table_load)
+  uint32_t tab_n = 0;
   hipEvent_t e_fork = nullptr, e_join[2] = {nullptr, nullptr}, e_sig = nullptr;
   hbuf hin, hout;
 };
@@ -166,8 +169,11 @@ static uint32_t miller_wave_max() {
   return v;
 }
 int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* partial_out, ws_layout& L,
-                   const uint8_t* dst, uint32_t dlen, bool keep_codes, hipEvent_t* ev = nullptr, bool serial_req = false) {
-  const uint32_t n = b.n, K = b.n_keys;
+                   const uint8_t* dst, uint32_t dlen, bool keep_codes, hipEvent_t* ev = nullptr, bool serial_req = false,
+                   const uint32_t* key_idx = nullptr) {
+  const uint32_t n = b.n;
+  const bool use_tab = key_idx != nullptr;  // keys = indices into the resident table: no decompression
+  const uint32_t K = use_tab ? 0 : b.n_keys;
   L = ws_layout(n, K);
   if (c.ws.ensure(L.total)) return TBLS_DEVICE_ERROR;
   uint8_t* w = c.ws.as<uint8_t>();
@@ -244,8 +250,9 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
   TB_EV(1, sk);
   TB_EV(2, sk);
   if (n)
-    hipLaunchKernelGGL(k_set_pk, g, blk, 0, sk, b.pk_off, (const g1a*)(w + L.pk_aff), w + L.pk_code, b.rand, n, (g1a*)(w + L.P),
-                       w + L.set_code, (uint32_t*)(w + L.n_bad));
+    hipLaunchKernelGGL(k_set_pk, g, blk, 0, sk, b.pk_off, use_tab ? c.tab_aff.as<const g1a>() : (const g1a*)(w + L.pk_aff),
+                       use_tab ? c.tab_code.as<const uint8_t>() : (const uint8_t*)(w + L.pk_code), b.rand, n, (g1a*)(w + L.P),
+                       w + L.set_code, (uint32_t*)(w + L.n_bad), key_idx);
   TB_EV(3, sk);
   HIPCHK(hipEventRecord(c.e_join[0], sig_first ? sa : sh));
   HIPCHK(hipStreamWaitEvent(s, c.e_join[0], 0));
@@ -337,7 +344,14 @@ struct packed {
   uint32_t n, K, M;
 };
 
-packed pack_layout(const tbls_set* sets, size_t lo, size_t hi, uint32_t dlen) {
+// keys of a set: 48-byte encodings (tbls_set) or 4-byte table indices (tbls_set_idx)
+inline const void* set_keys(const tbls_set& s) { return s.pks; }
+inline const void* set_keys(const tbls_set_idx& s) { return s.key_idx; }
+template <class SET>
+constexpr size_t key_bytes() { return std::is_same<SET, tbls_set>::value ? 48 : 4; }
+
+template <class SET>
+packed pack_layout(const SET* sets, size_t lo, size_t hi, uint32_t dlen) {
   packed p;
   p.n = (uint32_t)(hi - lo);
   uint64_t K = 0, M = 0;
@@ -348,7 +362,7 @@ packed pack_layout(const tbls_set* sets, size_t lo, size_t hi, uint32_t dlen) {
   p.K = (uint32_t)K;
   p.M = (uint32_t)M;
   size_t o = 0;
-  p.off_pks = o;    o = align_up(o + (size_t)K * 48);
+  p.off_pks = o;    o = align_up(o + (size_t)K * key_bytes<SET>());
   p.off_pkoff = o;  o = align_up(o + ((size_t)p.n + 1) * 4);
   p.off_msgs = o;   o = align_up(o + (M ? M : 1));
   p.off_msgoff = o; o = align_up(o + ((size_t)p.n + 1) * 4);
@@ -359,16 +373,17 @@ packed pack_layout(const tbls_set* sets, size_t lo, size_t hi, uint32_t dlen) {
   return p;
 }
 
-void pack_fill(uint8_t* h, const packed& p, const tbls_set* sets, size_t lo, const uint64_t* rand, const uint8_t* dst, uint32_t dlen) {
+template <class SET>
+void pack_fill(uint8_t* h, const packed& p, const SET* sets, size_t lo, const uint64_t* rand, const uint8_t* dst, uint32_t dlen) {
   uint32_t* pkoff = (uint32_t*)(h + p.off_pkoff);
   uint32_t* moff = (uint32_t*)(h + p.off_msgoff);
   uint64_t* rr = (uint64_t*)(h + p.off_rand);
   uint32_t k = 0, m = 0;
   for (uint32_t i = 0; i < p.n; i++) {
-    const tbls_set& s = sets[lo + i];
+    const SET& s = sets[lo + i];
     pkoff[i] = k;
     moff[i] = m;
-    if (s.n_pks) memcpy(h + p.off_pks + (size_t)k * 48, s.pks, (size_t)s.n_pks * 48);
+    if (s.n_pks) memcpy(h + p.off_pks + (size_t)k * key_bytes<SET>(), set_keys(s), (size_t)s.n_pks * key_bytes<SET>());
     if (s.msg_len) memcpy(h + p.off_msgs + m, s.msg, s.msg_len);
     memcpy(h + p.off_sigs + (size_t)i * 96, s.sig, 96);
     rr[i] = rand ? rand[lo + i] : 1;
@@ -384,8 +399,10 @@ const uint8_t ETH2_DST[] = "BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_POP_";
 
 // Runs sets[lo, hi) on device d; produces the 580-byte partial record on the host.
 // Optionally returns per-set verdict codes (set_code | sig_code) on the host.
-int run_shard(int d, const tbls_set* sets, size_t lo, size_t hi, const uint64_t* rand, const uint8_t* dst, uint32_t dlen,
+template <class SET>
+int run_shard(int d, const SET* sets, size_t lo, size_t hi, const uint64_t* rand, const uint8_t* dst, uint32_t dlen,
               uint8_t* partial_host, uint8_t* codes_host, double* dev_ms) {
+  constexpr bool idx_mode = !std::is_same<SET, tbls_set>::value;
   dev_ctx* c = ctx_for(d);
   if (!c) return TBLS_DEVICE_ERROR;
   std::lock_guard<std::mutex> lk(c->mu);
@@ -412,7 +429,9 @@ int run_shard(int d, const tbls_set* sets, size_t lo, size_t hi, const uint64_t*
   uint8_t* dpart = di + align_up(p.total);
   ws_layout L(0, 0);
   HIPCHK(hipEventRecord(e0, s));
-  int rc = launch_partial(*c, b, s, dpart, L, di + p.off_dst, dlen, codes_host != nullptr);
+  if (idx_mode && !c->tab_n) return TBLS_BAD_ARGUMENT;  // no key table on this device
+  int rc = launch_partial(*c, b, s, dpart, L, di + p.off_dst, dlen, codes_host != nullptr, nullptr, false,
+                          idx_mode ? (const uint32_t*)(di + p.off_pks) : nullptr);
   if (rc) return rc;
   HIPCHK(hipEventRecord(e1, s));
   const size_t outb = TBLS_PARTIAL_BYTES + (codes_host ? 2 * (size_t)p.n : 0);
@@ -565,7 +584,8 @@ extern "C" int tbls_device_count(void) {
   return (int)g_ctx.size();
 }
 
-extern "C" int tbls_batch_verify(const tbls_set* sets, size_t n, const uint64_t* rand, int n_gpus, int* ok, tbls_timing* t) {
+template <class SET>
+int batch_verify_impl(const SET* sets, size_t n, const uint64_t* rand, int n_gpus, int* ok, tbls_timing* t) {
   auto t0 = std::chrono::steady_clock::now();
   *ok = 0;
   if (ensure_init()) return TBLS_DEVICE_ERROR;
@@ -611,6 +631,54 @@ extern "C" int tbls_batch_verify(const tbls_set* sets, size_t n, const uint64_t*
     t->n_devices = (uint32_t)G;
   }
   return rc;
+}
+
+extern "C" int tbls_batch_verify(const tbls_set* sets, size_t n, const uint64_t* rand, int n_gpus, int* ok, tbls_timing* t) {
+  return batch_verify_impl(sets, n, rand, n_gpus, ok, t);
+}
+
+// --------------------------------------------------------------------------
+// device-resident public-key table
+// --------------------------------------------------------------------------
+extern "C" int tbls_pk_table_load(const uint8_t* pks, size_t K, uint8_t* codes) {
+  if (ensure_init()) return TBLS_DEVICE_ERROR;
+  if (K == 0 || K > 0xffffffffu / 96) return TBLS_BAD_ARGUMENT;
+  std::vector<dev_ctx*> devs;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    devs = g_ctx;
+  }
+  for (size_t d = 0; d < devs.size(); d++) {
+    dev_ctx* c = devs[d];
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIPCHK(hipSetDevice(c->dev));
+    c->tab_n = 0;
+    if (c->in.ensure(K * 48) || c->tab_aff.ensure(K * sizeof(g1a)) || c->tab_code.ensure(K)) return TBLS_DEVICE_ERROR;
+    HIPCHK(hipMemcpyAsync(c->in.p, pks, K * 48, hipMemcpyHostToDevice, c->stream));
+    hipLaunchKernelGGL(k_pk_decompress, dim3((uint32_t)((K + TB_BLOCK - 1) / TB_BLOCK)), dim3(TB_BLOCK), 0, c->stream,
+                       c->in.as<const uint8_t>(), (uint32_t)K, c->tab_aff.as<g1a>(), c->tab_code.as<uint8_t>());
+    HIPCHK(hipGetLastError());
+    if (d == 0 && codes) HIPCHK(hipMemcpyAsync(codes, c->tab_code.p, K, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->tab_n = (uint32_t)K;
+  }
+  return TBLS_SUCCESS;
+}
+
+extern "C" size_t tbls_pk_table_size(void) {
+  if (ensure_init()) return 0;
+  dev_ctx* c = ctx_for(0);
+  std::lock_guard<std::mutex> lk(c->mu);
+  return c->tab_n;
+}
+
+extern "C" int tbls_batch_verify_idx(const tbls_set_idx* sets, size_t n, const uint64_t* rand, int n_gpus, int* ok, tbls_timing* t) {
+  *ok = 0;
+  const size_t tn = tbls_pk_table_size();
+  for (size_t i = 0; i < n; i++)
+    for (uint32_t k = 0; k < sets[i].n_pks; k++)
+      if (sets[i].key_idx[k] >= tn) return TBLS_BAD_ARGUMENT;
+  return batch_verify_impl(sets, n, rand, n_gpus, ok, t);
 }
 
 // core_verify through the same pipeline with r = 1 (one set, no randomizer)
@@ -808,6 +876,22 @@ extern "C" int tbls_dev_batch_partial(int device, const tbls_dev_batch* b, void*
   }
   ws_layout L(0, 0);
   return launch_partial(*c, *b, s, partial_out, L, c->dstb.as<uint8_t>(), 43, false);
+}
+
+extern "C" int tbls_dev_batch_partial_idx(int device, const tbls_dev_batch* b, const uint32_t* key_idx, void* stream, void* partial_out) {
+  if (ensure_init()) return TBLS_DEVICE_ERROR;
+  dev_ctx* c = ctx_for(device);
+  if (!c) return TBLS_DEVICE_ERROR;
+  std::lock_guard<std::mutex> lk(c->mu);
+  if (!c->tab_n || !key_idx) return TBLS_BAD_ARGUMENT;
+  HIPCHK(hipSetDevice(c->dev));
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  if (!c->dstb.p) {
+    if (c->dstb.ensure(256)) return TBLS_DEVICE_ERROR;
+    HIPCHK(hipMemcpy(c->dstb.p, ETH2_DST, 43, hipMemcpyHostToDevice));
+  }
+  ws_layout L(0, 0);
+  return launch_partial(*c, *b, s, partial_out, L, c->dstb.as<uint8_t>(), 43, false, nullptr, false, key_idx);
 }
 
 static int partial_timed(int device, const tbls_dev_batch* b, void* stream, void* partial_out, float* stage_ms, bool serial) {

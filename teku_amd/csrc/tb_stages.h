@@ -21,19 +21,24 @@ TB_HD TB_INLINE int stage_pk(const uint8_t* b48, g1a& a) {
   return code;
 }
 
-// aggregate keys [b, e) (any invalid -> PK_IS_INFINITY), P = [r] apk affine
-TB_HD TB_INLINE int stage_set_pk(const g1a* pk_aff, const uint8_t* pk_code, uint32_t b, uint32_t e, uint64_t r, g1a& P) {
+// aggregate keys [b, e) (any invalid -> PK_IS_INFINITY), P = [r] apk affine.
+// idx (nullable): key k of the set is pk_aff[idx[k]] (device-resident key
+// table, tbls_pk_table_load) instead of pk_aff[k].
+TB_HD TB_INLINE int stage_set_pk(const g1a* pk_aff, const uint8_t* pk_code, uint32_t b, uint32_t e, uint64_t r, g1a& P,
+                                 const uint32_t* idx = nullptr) {
   int code = TB_SUCCESS;
   P.x = fp_zero();
   P.y = fp_zero();
   if (e - b == 1) {
-    if (pk_code[b] != TB_SUCCESS) return TB_PK_IS_INFINITY;
-    g1j rp = jac_mul_u64_aff(pk_aff[b], r);
+    const uint32_t k = idx ? idx[b] : b;
+    if (pk_code[k] != TB_SUCCESS) return TB_PK_IS_INFINITY;
+    g1j rp = jac_mul_u64_aff(pk_aff[k], r);
     if (!jac_to_aff(P, rp)) code = TB_PK_IS_INFINITY;
     return code;
   }
   g1j acc = jac_inf<fp>();
-  for (uint32_t k = b; k < e; k++) {
+  for (uint32_t j = b; j < e; j++) {
+    const uint32_t k = idx ? idx[j] : j;
     if (pk_code[k] != TB_SUCCESS) return TB_PK_IS_INFINITY;  // BlstPublicKey.java:58-65
     acc = jac_add_aff(acc, pk_aff[k]);
   }

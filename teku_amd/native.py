@@ -37,6 +37,18 @@ class TblsSet(ctypes.Structure):
     ]
 
 
+class TblsSetIdx(ctypes.Structure):
+    """tbls_set_idx: a set whose keys are indices into the resident key table."""
+
+    _fields_ = [
+        ("key_idx", ctypes.c_void_p),
+        ("n_pks", ctypes.c_uint32),
+        ("msg", ctypes.c_void_p),
+        ("msg_len", ctypes.c_uint32),
+        ("sig", ctypes.c_void_p),
+    ]
+
+
 class TblsTiming(ctypes.Structure):
     _fields_ = [("total_ms", ctypes.c_double), ("device_ms", ctypes.c_double), ("n_devices", ctypes.c_uint32)]
 
@@ -113,6 +125,23 @@ _SIGS = {
         ],
     ),
     "tbls_dev_batch_partial": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(TblsDevBatch), ctypes.c_void_p, ctypes.c_void_p]),
+    "tbls_pk_table_load": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_void_p]),
+    "tbls_pk_table_size": (ctypes.c_size_t, []),
+    "tbls_batch_verify_idx": (
+        ctypes.c_int,
+        [
+            ctypes.POINTER(TblsSetIdx),
+            ctypes.c_size_t,
+            ctypes.POINTER(ctypes.c_uint64),
+            ctypes.c_int,
+            ctypes.POINTER(ctypes.c_int),
+            ctypes.POINTER(TblsTiming),
+        ],
+    ),
+    "tbls_dev_batch_partial_idx": (
+        ctypes.c_int,
+        [ctypes.c_int, ctypes.POINTER(TblsDevBatch), ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p],
+    ),
     "tbls_dev_final_verify": (
         ctypes.c_int,
         [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)],

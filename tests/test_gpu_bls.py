@@ -343,3 +343,37 @@ def test_large_batch_msm_path(hip):
     dup_p, dup_m, dup_s, dup_r = list(pks), list(msgs), list(sigs), list(rands)
     dup_p[1], dup_m[1], dup_s[1], dup_r[1] = pks[0], msgs[0], sigs[0], rands[0]
     assert _raw(bls, dup_p, dup_m, dup_s, dup_r)
+
+
+def test_validator_key_table(hip, sets8):
+    """Device-resident key table (tbls_pk_table_load / tbls_batch_verify_idx,
+    SURVEY.md 8(f) rank 1): per-key codes as tbls_pk_validate; batches by key
+    index give the same booleans as the same batches by key bytes, including
+    multi-key sets, an invalid table key (infinity / 0x9378a6... / not on the
+    curve) and a tampered signature; out-of-range index -> ValueError."""
+    bls, native, L, impl = hip
+    sks, pks, msgs, sigs = sets8
+    pkb = list(pks)  # compressed 48-byte keys
+    inf_pk = bytes([0xC0]) + bytes(47)
+    table = bls.ValidatorKeyTable(pkb + [inf_pk, BAD_PK])
+    assert table.size == 10 and L.tbls_pk_table_size() == 10
+    assert table.codes[:8] == [0] * 8
+    assert table.codes[8] == native.PK_IS_INFINITY and table.codes[9] != 0
+    sets = [([i], msgs[i], sigs[i]) for i in range(8)]
+    rands = [random.getrandbits(64) | 1 for _ in sets]
+    assert table.batch_verify(sets, rands)
+    assert _raw(bls, pkb, msgs, sigs, rands)
+    bad = list(sets)
+    bad[3] = ([3], msgs[3], sigs[4])
+    assert not table.batch_verify(bad, rands)
+    for k in (8, 9):
+        bad = list(sets)
+        bad[2] = ([2, k], msgs[2], sigs[2])
+        assert not table.batch_verify(bad, rands)
+    # one set signed by keys 0..3 on one message (fastAggregateVerify shape)
+    m = b"\x42" * 32
+    agg = O.aggregate_sigs([O.sign(sks[i], m) for i in range(4)])
+    assert table.batch_verify(sets + [([0, 1, 2, 3], m, agg)], rands + [12345])
+    assert not table.batch_verify(sets + [([0, 1, 2, 5], m, agg)], rands + [12345])
+    with pytest.raises(ValueError):
+        table.batch_verify([([10], msgs[0], sigs[0])], [1])
