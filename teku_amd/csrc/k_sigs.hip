@@ -121,7 +121,9 @@ extern "C" __global__ void __launch_bounds__(TB_BLOCK)
 // whole batch (n_bad), so only valid, finite signatures enter the sum;
 // infinity contributes nothing (blst skips it).
 //
-//   k_msm_hist     per set: bucket counts (window w, digit d = byte w of r)
+//   k_msm_hist     per set: bucket counts (window w, digit d = byte w of r);
+//                  hist / scan / scatter depend only on the randomizers, so they
+//                  run on stream b concurrently with k_sig_check
 //   k_msm_scan     exclusive scan of the 8 x 256 counts -> bucket offsets
 //   k_msm_scatter  per set: set index into its 8 bucket lists
 //   k_msm_bucket   per (bucket, chunk): sum of the chunk's affine points
@@ -154,10 +156,10 @@ extern "C" __global__ void __launch_bounds__(TB_BLOCK)
 }
 
 extern "C" __global__ void __launch_bounds__(TB_BLOCK)
-    k_msm_hist(const uint64_t* __restrict__ rand, const uint8_t* __restrict__ use, uint32_t n, uint32_t* __restrict__ cnt) {
+    k_msm_hist(const uint64_t* __restrict__ rand, uint32_t n, uint32_t* __restrict__ cnt) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   tb_latency_prio();
-  if (i >= n || !use[i]) return;
+  if (i >= n) return;
   const uint64_t r = rand[i];
   for (int w = 0; w < TB_MSM_W; w++) {
     const uint32_t d = (uint32_t)(r >> (8 * w)) & 255u;
@@ -195,11 +197,10 @@ extern "C" __global__ void __launch_bounds__(256)
 }
 
 extern "C" __global__ void __launch_bounds__(TB_BLOCK)
-    k_msm_scatter(const uint64_t* __restrict__ rand, const uint8_t* __restrict__ use, uint32_t n, uint32_t* __restrict__ cur,
-                  uint32_t* __restrict__ idx) {
+    k_msm_scatter(const uint64_t* __restrict__ rand, uint32_t n, uint32_t* __restrict__ cur, uint32_t* __restrict__ idx) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   tb_latency_prio();
-  if (i >= n || !use[i]) return;
+  if (i >= n) return;
   const uint64_t r = rand[i];
   for (int w = 0; w < TB_MSM_W; w++) {
     const uint32_t d = (uint32_t)(r >> (8 * w)) & 255u;
@@ -209,8 +210,8 @@ extern "C" __global__ void __launch_bounds__(TB_BLOCK)
 
 // thread (bucket b, chunk c): sum of the affine points of chunk c of list b
 extern "C" __global__ void __launch_bounds__(TB_BLOCK)
-    k_msm_bucket(const g2a* __restrict__ sig_aff, const uint32_t* __restrict__ off, const uint32_t* __restrict__ idx,
-                 g2j* __restrict__ part) {
+    k_msm_bucket(const g2a* __restrict__ sig_aff, const uint8_t* __restrict__ use, const uint32_t* __restrict__ off,
+                 const uint32_t* __restrict__ idx, g2j* __restrict__ part) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   tb_latency_prio();
   if (t >= TB_MSM_W * TB_MSM_NB * TB_MSM_CHUNKS) return;
@@ -220,7 +221,10 @@ extern "C" __global__ void __launch_bounds__(TB_BLOCK)
   uint32_t s = lo + c * chunk, e = s + chunk;
   if (e > hi) e = hi;
   g2j acc = jac_inf<fp2>();
-  for (uint32_t k = s; k < e; k++) acc = jac_add_aff(acc, sig_aff[idx[k]]);
+  for (uint32_t k = s; k < e; k++) {
+    const uint32_t i = idx[k];
+    if (use[i]) acc = jac_add_aff(acc, sig_aff[i]);  // invalid sets fail the batch anyway; infinity adds nothing
+  }
   part[t] = acc;
 }
 

@@ -55,10 +55,10 @@ extern "C" __global__ void k_aggregate_pks(const g1a* __restrict__ pk_aff, const
 extern "C" __global__ void k_sk_to_pk(const uint64_t* __restrict__ sks, uint32_t n, uint8_t* __restrict__ out);
 extern "C" __global__ void k_set_sig(const uint8_t* __restrict__ sigs, const uint64_t* __restrict__ rand, uint32_t n, g2j* __restrict__ rsig, uint8_t* __restrict__ sig_code, uint32_t* __restrict__ n_bad);
 extern "C" __global__ void k_sig_check(const uint8_t* __restrict__ sigs, uint32_t n, g2a* __restrict__ sig_aff, uint8_t* __restrict__ sig_use, uint8_t* __restrict__ sig_code, uint32_t* __restrict__ n_bad);
-extern "C" __global__ void k_msm_hist(const uint64_t* __restrict__ rand, const uint8_t* __restrict__ use, uint32_t n, uint32_t* __restrict__ cnt);
+extern "C" __global__ void k_msm_hist(const uint64_t* __restrict__ rand, uint32_t n, uint32_t* __restrict__ cnt);
 extern "C" __global__ void k_msm_scan(const uint32_t* __restrict__ cnt, uint32_t* __restrict__ off, uint32_t* __restrict__ cur);
-extern "C" __global__ void k_msm_scatter(const uint64_t* __restrict__ rand, const uint8_t* __restrict__ use, uint32_t n, uint32_t* __restrict__ cur, uint32_t* __restrict__ idx);
-extern "C" __global__ void k_msm_bucket(const g2a* __restrict__ sig_aff, const uint32_t* __restrict__ off, const uint32_t* __restrict__ idx, g2j* __restrict__ part);
+extern "C" __global__ void k_msm_scatter(const uint64_t* __restrict__ rand, uint32_t n, uint32_t* __restrict__ cur, uint32_t* __restrict__ idx);
+extern "C" __global__ void k_msm_bucket(const g2a* __restrict__ sig_aff, const uint8_t* __restrict__ use, const uint32_t* __restrict__ off, const uint32_t* __restrict__ idx, g2j* __restrict__ part);
 extern "C" __global__ void k_msm_bsum(const g2j* __restrict__ part, g2j* __restrict__ bucket);
 extern "C" __global__ void k_msm_window(const g2j* __restrict__ bucket, g2j* __restrict__ wseg);
 extern "C" __global__ void k_msm_final(const g2j* __restrict__ wseg, g2j* __restrict__ wsum, uint32_t slot, g1a* __restrict__ P, g2a* __restrict__ Q, uint8_t* __restrict__ skip);

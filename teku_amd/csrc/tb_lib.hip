@@ -192,10 +192,21 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
   const uint32_t nthr = one_pair ? n : (n + 1) / 2;  // Miller values f[0..nthr-1]; f[nthr] = the g1 pair
   HIPCHK(hipMemsetAsync(w + L.set_code, 0, n ? n : 1, s));
   HIPCHK(hipMemsetAsync(w + L.n_bad, 0, 4, s));
-  if (!sig_first) {
+  if (!sig_first || (L.msm && !serial)) {
     HIPCHK(hipEventRecord(c.e_fork, s));
-    HIPCHK(hipStreamWaitEvent(sa, c.e_fork, 0));
+    if (!sig_first) HIPCHK(hipStreamWaitEvent(sa, c.e_fork, 0));
     HIPCHK(hipStreamWaitEvent(sb, c.e_fork, 0));
+  }
+  // MSM bucket sort (randomizers only): on stream b, concurrent with the signature check
+  uint32_t* msm_cnt = (uint32_t*)(w + L.msm_cnt);
+  uint32_t* msm_off = (uint32_t*)(w + L.msm_off);
+  uint32_t* msm_idx = (uint32_t*)(w + L.msm_idx);
+  if (L.msm) {
+    uint32_t* cur = (uint32_t*)(w + L.msm_cur);
+    HIPCHK(hipMemsetAsync(msm_cnt, 0, TB_MSM_BUCKETS * 4, sb));
+    hipLaunchKernelGGL(k_msm_hist, g, blk, 0, sb, b.rand, n, msm_cnt);
+    hipLaunchKernelGGL(k_msm_scan, dim3(1), dim3(256), 0, sb, (const uint32_t*)msm_cnt, msm_off, cur);
+    hipLaunchKernelGGL(k_msm_scatter, g, blk, 0, sb, b.rand, n, cur, msm_idx);
   }
   // signatures: decompress, G2 subgroup check (+ [r]sig per set without the MSM)
   TB_EV(4, ss);
@@ -213,16 +224,8 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
   // stream b: the G2 sum, then the Miller loop of the (-g1, S) pair
   TB_EV(8, sb);
   if (L.msm) {
-    uint32_t* cnt = (uint32_t*)(w + L.msm_cnt);
-    uint32_t* off = (uint32_t*)(w + L.msm_off);
-    uint32_t* cur = (uint32_t*)(w + L.msm_cur);
-    uint32_t* idx = (uint32_t*)(w + L.msm_idx);
-    HIPCHK(hipMemsetAsync(cnt, 0, TB_MSM_BUCKETS * 4, sb));
-    hipLaunchKernelGGL(k_msm_hist, g, blk, 0, sb, b.rand, w + L.sig_use, n, cnt);
-    hipLaunchKernelGGL(k_msm_scan, dim3(1), dim3(256), 0, sb, (const uint32_t*)cnt, off, cur);
-    hipLaunchKernelGGL(k_msm_scatter, g, blk, 0, sb, b.rand, w + L.sig_use, n, cur, idx);
-    hipLaunchKernelGGL(k_msm_bucket, dim3(TB_MSM_PARTS / TB_BLOCK), blk, 0, sb, (const g2a*)(w + L.sig_aff), (const uint32_t*)off,
-                       (const uint32_t*)idx, (g2j*)(w + L.msm_part));
+    hipLaunchKernelGGL(k_msm_bucket, dim3(TB_MSM_PARTS / TB_BLOCK), blk, 0, sb, (const g2a*)(w + L.sig_aff), (const uint8_t*)(w + L.sig_use),
+                       (const uint32_t*)msm_off, (const uint32_t*)msm_idx, (g2j*)(w + L.msm_part));
     hipLaunchKernelGGL(k_msm_bsum, dim3(TB_MSM_BUCKETS / TB_BLOCK), blk, 0, sb, (const g2j*)(w + L.msm_part), (g2j*)(w + L.msm_bucket));
     hipLaunchKernelGGL(k_msm_window, dim3(TB_MSM_WSEGS / TB_BLOCK), blk, 0, sb, (const g2j*)(w + L.msm_bucket), (g2j*)(w + L.msm_wseg));
     hipLaunchKernelGGL(k_msm_final, dim3(1), dim3(64), 0, sb, (const g2j*)(w + L.msm_wseg), (g2j*)(w + L.msm_wsum), n, (g1a*)(w + L.P),
