@@ -141,8 +141,18 @@ typedef struct {
 int tbls_batch_verify_idx(const tbls_set_idx* sets, size_t n, const uint64_t* rand, int n_gpus, int* ok, tbls_timing* t);
 
 /* fastAggregateVerify per set (BLS.java:185-207, BlstSignature.java:125-129):
- * ok_per_set[i] in {0,1}; an empty key list gives 0. */
+ * ok_per_set[i] in {0,1}; an empty key list gives 0.  One batched device pass
+ * (= tbls_verify_each on one device). */
 int tbls_fast_aggregate_verify_many(const tbls_set* sets, size_t n, int* ok_per_set);
+
+/* Per-set verdicts of a whole batch in one pass:
+ * ok_per_set[i] = BLS.fastAggregateVerify(sets[i]) (BLS.java:185-207).
+ * Replaces the recursive halving + per-task SIMPLE.verify fallback of
+ * AggregatingSignatureVerificationService.batchVerifySignatures
+ * (statetransition/.../signatures/AggregatingSignatureVerificationService.java:
+ * 188-227) after a failed randomized batch.  Chunks of 65536 sets are spread
+ * over n_gpus devices (0 = all). */
+int tbls_verify_each(const tbls_set* sets, size_t n, int n_gpus, int* ok_per_set);
 
 /* aggregateVerify (BLS.java:144-170, BlstSignature.java:104-122): n distinct
  * (pk, msg) pairs against one aggregate signature. */

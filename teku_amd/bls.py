@@ -379,6 +379,27 @@ def batch_verify_raw(sets, rands, n_gpus=0, timing=None) -> bool:
     return ok.value == 1
 
 
+def verify_each_raw(sets, n_gpus=0) -> List[bool]:
+    """Per-set fastAggregateVerify verdicts of [(pk_blob, n_pks, msg, sig96)]
+    in one device pass (tbls_verify_each)."""
+    n = len(sets)
+    if n == 0:
+        return []
+    arr = (native.TblsSet * n)()
+    keep = []
+    for i, (blob, npk, msg, sig) in enumerate(sets):
+        bb, mb, sb = _buf(blob), _buf(msg), _buf(sig)
+        keep += [bb, mb, sb]
+        arr[i].pks = ctypes.cast(bb, ctypes.c_void_p)
+        arr[i].n_pks = npk
+        arr[i].msg = ctypes.cast(mb, ctypes.c_void_p)
+        arr[i].msg_len = len(msg)
+        arr[i].sig = ctypes.cast(sb, ctypes.c_void_p)
+    ok = (ctypes.c_int * n)()
+    native.check(native.lib().tbls_verify_each(arr, n, n_gpus, ok), "tbls_verify_each")
+    return [v == 1 for v in ok]
+
+
 class ValidatorKeyTable:
     """Device-resident validator public-key table (SURVEY.md 8(f) rank 1;
     C ABI tbls_pk_table_load / tbls_batch_verify_idx).

@@ -10,6 +10,7 @@
 #include <functional>
 #include <cstring>
 #include <mutex>
+#include <algorithm>
 #include <thread>
 #include <type_traits>
 #include <vector>
@@ -709,18 +710,90 @@ extern "C" int tbls_verify(const uint8_t pk[48], const uint8_t* msg, size_t len,
   return TBLS_SUCCESS;
 }
 
-extern "C" int tbls_fast_aggregate_verify_many(const tbls_set* sets, size_t n, int* ok_per_set) {
-  if (ensure_init()) return TBLS_DEVICE_ERROR;
-  for (size_t i = 0; i < n; i++) {
-    ok_per_set[i] = 0;
-    if (sets[i].n_pks == 0) continue;  // BLS.java:193-195
-    int ok = 0;
-    uint8_t code = 0;
-    int rc = verify_one(sets[i].pks, sets[i].n_pks, sets[i].msg, sets[i].msg_len, sets[i].sig, ETH2_DST, 43, &ok, &code);
-    if (rc) return rc;
-    ok_per_set[i] = ok;
-  }
+// Per-set fastAggregateVerify verdicts for sets[lo, hi) on device d in one
+// pass (k_each.hip): shared per-set stages with r = 1, then one thread per set
+// for its two-pair Miller loop and final exponentiation.
+static int run_each(int d, const tbls_set* sets, size_t lo, size_t hi, uint8_t* ok_host) {
+  dev_ctx* c = ctx_for(d);
+  if (!c) return TBLS_DEVICE_ERROR;
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIPCHK(hipSetDevice(c->dev));
+  packed p = pack_layout(sets, lo, hi, 43);
+  if (c->hin.ensure(p.total + 256) || c->in.ensure(p.total + 256)) return TBLS_DEVICE_ERROR;
+  pack_fill(c->hin.b(), p, sets, lo, nullptr, ETH2_DST, 43);  // r = 1 for every set
+  hipStream_t s = c->stream;
+  HIPCHK(hipMemcpyAsync(c->in.p, c->hin.p, p.total, hipMemcpyHostToDevice, s));
+  const uint8_t* di = c->in.as<uint8_t>();
+  const uint32_t n = p.n, K = p.K;
+  size_t o = 0;
+  const size_t pk_aff = o;   o = align_up(o + (size_t)K * sizeof(g1a));
+  const size_t pk_code = o;  o = align_up(o + (K ? K : 1));
+  const size_t P = o;        o = align_up(o + (size_t)n * sizeof(g1a));
+  const size_t Q = o;        o = align_up(o + (size_t)n * sizeof(g2a));
+  const size_t sig_aff = o;  o = align_up(o + (size_t)n * sizeof(g2a));
+  const size_t skip = o;     o = align_up(o + n);
+  const size_t set_code = o; o = align_up(o + n);
+  const size_t sig_code = o; o = align_up(o + n);
+  const size_t sig_use = o;  o = align_up(o + n);
+  const size_t okd = o;      o = align_up(o + n);
+  const size_t n_bad = o;    o = align_up(o + 4);
+  if (c->ws.ensure(o)) return TBLS_DEVICE_ERROR;
+  uint8_t* w = c->ws.as<uint8_t>();
+  const dim3 blk(TB_BLOCK), g((n + TB_BLOCK - 1) / TB_BLOCK);
+  HIPCHK(hipMemsetAsync(w + n_bad, 0, 4, s));
+  HIPCHK(hipMemsetAsync(w + set_code, 0, n, s));  // k_set_pk writes failures only
+  if (K)
+    hipLaunchKernelGGL(k_pk_decompress, dim3((K + TB_BLOCK - 1) / TB_BLOCK), blk, 0, s, di + p.off_pks, K, (g1a*)(w + pk_aff),
+                       w + pk_code);
+  hipLaunchKernelGGL(k_set_pk, g, blk, 0, s, (const uint32_t*)(di + p.off_pkoff), (const g1a*)(w + pk_aff), (const uint8_t*)(w + pk_code),
+                     (const uint64_t*)(di + p.off_rand), n, (g1a*)(w + P), w + set_code, (uint32_t*)(w + n_bad), nullptr);
+  hipLaunchKernelGGL(k_sig_check, g, blk, 0, s, di + p.off_sigs, n, (g2a*)(w + sig_aff), w + sig_use, w + sig_code, (uint32_t*)(w + n_bad));
+  hipLaunchKernelGGL(k_set_hash, g, blk, 0, s, di + p.off_msgs, (const uint32_t*)(di + p.off_msgoff), di + p.off_dst, 43u, n, (g2a*)(w + Q),
+                     w + skip);
+  hipLaunchKernelGGL(k_verify_each, g, blk, 0, s, (const g1a*)(w + P), (const g2a*)(w + Q), (const uint8_t*)(w + skip),
+                     (const uint8_t*)(w + set_code), (const g2a*)(w + sig_aff), (const uint8_t*)(w + sig_use), (const uint8_t*)(w + sig_code),
+                     n, w + okd);
+  HIPCHK(hipGetLastError());
+  if (c->hout.ensure(n)) return TBLS_DEVICE_ERROR;
+  HIPCHK(hipMemcpyAsync(c->hout.p, w + okd, n, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  memcpy(ok_host, c->hout.p, n);
   return TBLS_SUCCESS;
+}
+
+#define TB_EACH_CHUNK 65536u  // sets per device pass (bounds staging and workspace)
+
+extern "C" int tbls_verify_each(const tbls_set* sets, size_t n, int n_gpus, int* ok_per_set) {
+  if (ensure_init()) return TBLS_DEVICE_ERROR;
+  if (n == 0) return TBLS_SUCCESS;
+  int G = (int)g_ctx.size();
+  if (n_gpus > 0 && n_gpus < G) G = n_gpus;
+  const size_t nchunks = (n + TB_EACH_CHUNK - 1) / TB_EACH_CHUNK;
+  if ((size_t)G > nchunks) G = (int)nchunks;
+  std::vector<uint8_t> ok(n, 0);
+  std::vector<int> rcs(G, 0);
+  // chunk k runs on device k % G; one host thread per device
+  auto work = [&](int dv) {
+    for (size_t k = dv; k < nchunks && !rcs[dv]; k += G) {
+      const size_t lo = k * TB_EACH_CHUNK, hi = std::min(n, lo + TB_EACH_CHUNK);
+      rcs[dv] = run_each(dv, sets, lo, hi, ok.data() + lo);
+    }
+  };
+  if (G == 1) {
+    work(0);
+  } else {
+    std::vector<std::thread> th;
+    for (int dv = 0; dv < G; dv++) th.emplace_back(work, dv);
+    for (auto& x : th) x.join();
+  }
+  for (int dv = 0; dv < G; dv++)
+    if (rcs[dv]) return rcs[dv];
+  for (size_t i = 0; i < n; i++) ok_per_set[i] = (sets[i].n_pks != 0 && ok[i]) ? 1 : 0;  // BLS.java:193-195
+  return TBLS_SUCCESS;
+}
+
+extern "C" int tbls_fast_aggregate_verify_many(const tbls_set* sets, size_t n, int* ok_per_set) {
+  return tbls_verify_each(sets, n, 1, ok_per_set);
 }
 
 extern "C" int tbls_aggregate_verify(const uint8_t* pks, const uint8_t* const* msgs, const uint32_t* msg_lens, size_t n, const uint8_t sig[96],

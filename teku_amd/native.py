@@ -113,6 +113,7 @@ _SIGS = {
         ],
     ),
     "tbls_fast_aggregate_verify_many": (ctypes.c_int, [ctypes.POINTER(TblsSet), ctypes.c_size_t, ctypes.POINTER(ctypes.c_int)]),
+    "tbls_verify_each": (ctypes.c_int, [ctypes.POINTER(TblsSet), ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
     "tbls_aggregate_verify": (
         ctypes.c_int,
         [

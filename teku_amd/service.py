@@ -1,0 +1,215 @@
+"""GPU-aware signature verification service.
+
+Mirrors statetransition/.../validation/signatures/
+AggregatingSignatureVerificationService.java: callers submit
+(public-key lists, messages, signatures) tasks and get a future; worker
+threads drain the queue into batches of up to max_batch_size tasks
+(waitForBatch, l.164-179) and verify each batch with one randomized
+BLS.batchVerify (batchVerifySignatures, l.188-205).
+
+The difference is the failure path.  The reference, when a batch fails,
+halves it recursively down to min_batch_size_to_split tasks and then verifies
+each remaining task alone (l.211-227, splitTasks l.230-233): O(bad * log n)
+extra batch verifications, each a full GPU round trip.  Here a failed batch
+costs ONE more device pass: tbls_verify_each returns every set's
+fastAggregateVerify verdict, and a task is valid iff all its sets are
+(BLSSignatureVerifier.SIMPLE.verify -> BLS.batchVerify over the task's sets,
+BLSSignatureVerifier.java:27-43, which is the same boolean with overwhelming
+probability).  `split_fallback=True` restores the reference's halving, for
+comparison.
+
+Defaults follow the GPU: one submitting thread (the device queue serialises
+anyway; the reference uses up to #cores, P2POptions.java:324-359) and a large
+max batch (the device wants >= 16k sets; the reference default is 250).
+
+Semantics kept from the reference: a full queue completes the future
+exceptionally with ServiceCapacityExceededException (verify, l.143-152);
+verify() before start() raises (assertIsRunning); a one-task failed batch is
+that task's verdict (l.208-210).  A task whose list sizes differ completes
+exceptionally with BlsException (BLS.batchVerify throws, BLS.java:235-237).
+"""
+
+import queue
+import secrets
+import threading
+from concurrent.futures import Future
+from typing import Callable, List, Optional, Sequence
+
+from . import bls as _bls
+
+DEFAULT_MIN_BATCH_SIZE_TO_SPLIT = 25  # AggregatingSignatureVerificationService.java:42
+DEFAULT_MAX_BATCH_SIZE = 16384
+DEFAULT_QUEUE_CAPACITY = 65536
+
+
+class ServiceCapacityExceededException(RuntimeError):
+    """infrastructure/async/.../ServiceCapacityExceededException."""
+
+
+class SignatureTask:
+    """AggregatingSignatureVerificationService.SignatureTask (l.236-258): the
+    task's signature sets as (pk_blob, n_pks, msg, sig96) tuples."""
+
+    def __init__(self, sets):
+        self.sets = sets
+        self.result: Future = Future()
+
+
+def _set_tuple(pks, msg, sig):
+    blob = b"".join(bytes(p.to_bytes_compressed() if hasattr(p, "to_bytes_compressed") else p) for p in pks)
+    sigb = bytes(sig.to_bytes_compressed() if hasattr(sig, "to_bytes_compressed") else sig)
+    return (blob, len(pks), bytes(msg), sigb)
+
+
+def _hip_batch(sets) -> bool:
+    rands = [int.from_bytes(secrets.token_bytes(8), "big") or 1 for _ in sets]  # BlstBLS12381.java:191-195
+    try:
+        return _bls.batch_verify_raw(sets, rands)
+    except ValueError:  # an empty key list in the batch: settle it per set
+        return False
+
+
+class AggregatingSignatureVerificationService:
+    def __init__(
+        self,
+        num_threads: int = 1,
+        queue_capacity: int = DEFAULT_QUEUE_CAPACITY,
+        max_batch_size: int = DEFAULT_MAX_BATCH_SIZE,
+        min_batch_size_to_split: int = DEFAULT_MIN_BATCH_SIZE_TO_SPLIT,
+        split_fallback: bool = False,
+        batch_fn: Optional[Callable[[Sequence], bool]] = None,
+        each_fn: Optional[Callable[[Sequence], List[bool]]] = None,
+    ):
+        self.num_threads = max(1, num_threads)
+        self.max_batch_size = max(1, max_batch_size)
+        self.min_batch_size_to_split = min_batch_size_to_split
+        self.split_fallback = split_fallback
+        self._batch_fn = batch_fn or _hip_batch
+        self._each_fn = each_fn or _bls.verify_each_raw
+        self.batch_signature_tasks: "queue.Queue[SignatureTask]" = queue.Queue(maxsize=queue_capacity)
+        self._running = False
+        self._threads: List[threading.Thread] = []
+        # metrics (signature_verifications_{batch_count,task_count}_total, batch_size histogram)
+        self.batch_count = 0
+        self.task_count = 0
+        self.batch_sizes: List[int] = []
+        self.device_passes = 0
+
+    # -- Service lifecycle -------------------------------------------------
+    def start(self):
+        self._running = True
+        for i in range(self.num_threads):
+            t = threading.Thread(target=self._run, name=f"sigverify-{i}", daemon=True)
+            t.start()
+            self._threads.append(t)
+        return self
+
+    def stop(self):
+        self._running = False
+        for t in self._threads:
+            t.join()
+        self._threads = []
+
+    def is_running(self) -> bool:
+        return self._running
+
+    # -- SignatureVerificationService.verify -----------------------------------
+    def verify(self, public_keys, message, signature) -> Future:
+        """verify(List<BLSPublicKey>, Bytes, BLSSignature) (l.129-133)."""
+        return self.verify_many([public_keys], [message], [signature])
+
+    def verify_many(self, public_keys, messages, signatures) -> Future:
+        """verify(List<List<BLSPublicKey>>, List<Bytes>, List<BLSSignature>) (l.135-153)."""
+        if not self._running:
+            raise RuntimeError("Service must be running to execute action 'verify'")
+        if not (len(public_keys) == len(messages) == len(signatures)):
+            f: Future = Future()
+            f.set_exception(_bls.BlsException("Different collection sizes"))
+            return f
+        task = SignatureTask([_set_tuple(p, m, s) for p, m, s in zip(public_keys, messages, signatures)])
+        try:
+            self.batch_signature_tasks.put_nowait(task)
+        except queue.Full:
+            task.result.set_exception(ServiceCapacityExceededException("Failed to process signature, queue is full."))
+        return task.result
+
+    def queue_size(self) -> int:
+        return self.batch_signature_tasks.qsize()
+
+    # -- worker ---------------------------------------------------------------
+    def _run(self):
+        while self._running:
+            tasks = self._wait_for_batch()
+            if tasks:
+                self.batch_verify_signatures(tasks)
+
+    def _wait_for_batch(self) -> List[SignatureTask]:
+        tasks = []
+        try:
+            tasks.append(self.batch_signature_tasks.get(timeout=0.05))
+        except queue.Empty:
+            return tasks
+        while len(tasks) < self.max_batch_size:
+            try:
+                tasks.append(self.batch_signature_tasks.get_nowait())
+            except queue.Empty:
+                break
+        return tasks
+
+    def batch_verify_signatures(self, tasks: List[SignatureTask]):
+        self.batch_count += 1
+        self.task_count += len(tasks)
+        self.batch_sizes.append(len(tasks))
+        try:
+            self._verify(tasks)
+        except Exception as e:  # device error: fail every pending future loudly
+            for t in tasks:
+                if not t.result.done():
+                    t.result.set_exception(e)
+
+    def _verify(self, tasks: List[SignatureTask]):
+        all_sets = [s for t in tasks for s in t.sets]
+        empty = [t for t in tasks if not t.sets]  # SIMPLE.verify of zero sets -> false (BLS.java:240-241)
+        for t in empty:
+            t.result.set_result(False)
+        tasks = [t for t in tasks if t.sets]
+        if not tasks:
+            return
+        self.device_passes += 1
+        if self._batch_fn(all_sets):
+            for t in tasks:
+                t.result.set_result(True)
+            return
+        if len(tasks) == 1 and not self.split_fallback:
+            tasks[0].result.set_result(False)  # l.208-210
+            return
+        if self.split_fallback:
+            self._split(tasks)
+            return
+        self.device_passes += 1
+        verdicts = self._each_fn(all_sets)
+        k = 0
+        for t in tasks:
+            n = len(t.sets)
+            t.result.set_result(all(verdicts[k : k + n]))
+            k += n
+
+    def _split(self, tasks: List[SignatureTask]):
+        """The reference's fallback (l.208-227): halve down to
+        min_batch_size_to_split tasks, then each task alone."""
+        if len(tasks) == 1:
+            tasks[0].result.set_result(False)
+        elif len(tasks) >= self.min_batch_size_to_split:
+            half = (len(tasks) + 1) // 2
+            for part in (tasks[:half], tasks[half:]):
+                self.device_passes += 1
+                sets = [s for t in part for s in t.sets]
+                if self._batch_fn(sets):
+                    for t in part:
+                        t.result.set_result(True)
+                else:
+                    self._split(part)
+        else:
+            for t in tasks:
+                self.device_passes += 1
+                t.result.set_result(all(self._each_fn(t.sets)))

@@ -377,3 +377,66 @@ def test_validator_key_table(hip, sets8):
     assert not table.batch_verify(sets + [([0, 1, 2, 5], m, agg)], rands + [12345])
     with pytest.raises(ValueError):
         table.batch_verify([([10], msgs[0], sigs[0])], [1])
+
+
+def test_verify_each_and_service(hip, sets8):
+    """Per-set verdicts in one device pass (tbls_verify_each, SURVEY.md 8(f)
+    rank 2) equal the oracle's fastAggregateVerify per set on a mix of valid
+    and tampered sets (wrong message, swapped signature, zero / infinity /
+    non-G2 signature, infinity / invalid / zero key, empty key list,
+    multi-key set); tbls_fast_aggregate_verify_many agrees; the service
+    settles a failed batch with one per-set pass."""
+    from teku_amd.service import AggregatingSignatureVerificationService
+
+    bls, native, L, impl = hip
+    sks, pks, msgs, sigs = sets8
+    m = b"\x42" * 32
+    agg = O.aggregate_sigs([O.sign(sks[i], m) for i in range(3)])
+    sets, exp = [], []
+    for i in range(8):
+        sets.append((pks[i], 1, msgs[i], sigs[i]))
+        exp.append(True)
+    sets += [
+        (pks[0], 1, msgs[1], sigs[0]),
+        (pks[1], 1, msgs[1], sigs[2]),
+        (pks[2], 1, msgs[2], bytes(96)),
+        (pks[3], 1, msgs[3], O.INFINITY_G2),
+        (pks[4], 1, msgs[4], NOT_IN_G2),
+        (O.INFINITY_G1, 1, msgs[5], sigs[5]),
+        (BAD_PK, 1, msgs[6], sigs[6]),
+        (bytes(48), 1, msgs[7], sigs[7]),
+        (b"", 0, msgs[0], sigs[0]),
+        (b"".join(pks[:3]), 3, m, agg),
+        (b"".join(pks[:2]), 2, m, agg),
+        (O.INFINITY_G1, 1, msgs[0], O.INFINITY_G2),
+    ]
+    exp += [False] * 9 + [True, False, False]
+    # oracle per set (non-empty key lists): BLS.batchVerify of (s, s) == fastAggregateVerify(s)
+    for (blob, npk, msg, sig), e in zip(sets, exp):
+        if npk == 0:
+            continue
+        keys = [blob[48 * j : 48 * j + 48] for j in range(npk)]
+        assert O.batch_verify([keys, keys], [msg, msg], [sig, sig]) == e
+    got = bls.verify_each_raw(sets)
+    assert got == exp
+    arr = (native.TblsSet * len(sets))()
+    keep = []
+    for i, (blob, npk, msg, sig) in enumerate(sets):
+        bb, mb, sb = (ctypes.create_string_buffer(bytes(x), max(1, len(x))) for x in (blob, msg, sig))
+        keep += [bb, mb, sb]
+        arr[i].pks = ctypes.cast(bb, ctypes.c_void_p)
+        arr[i].n_pks = npk
+        arr[i].msg = ctypes.cast(mb, ctypes.c_void_p)
+        arr[i].msg_len = len(msg)
+        arr[i].sig = ctypes.cast(sb, ctypes.c_void_p)
+    ok = (ctypes.c_int * len(sets))()
+    native.check(L.tbls_fast_aggregate_verify_many(arr, len(sets), ok), "fav_many")
+    assert [v == 1 for v in ok] == exp
+    # the service on the device backend: one batch, one per-set pass
+    svc = AggregatingSignatureVerificationService(max_batch_size=64)
+    from teku_amd.service import SignatureTask
+
+    tasks = [SignatureTask([s]) for s in sets if s[1] > 0]
+    svc.batch_verify_signatures(tasks)
+    assert [t.result.result() for t in tasks] == [e for s, e in zip(sets, exp) if s[1] > 0]
+    assert svc.device_passes == 2

@@ -1,0 +1,120 @@
+"""Host logic of the GPU-aware AggregatingSignatureVerificationService
+(teku_amd/service.py), with the C oracle as the
+verification backend (CPU; the device backend is covered by
+tests/test_gpu_bls.py::test_verify_each_and_service).
+
+Mirrors the reference's AggregatingSignatureVerificationServiceTest
+(statetransition/src/test/.../signatures/AggregatingSignatureVerificationServiceTest.java):
+valid batches complete true, one invalid task among valid ones completes
+false alone, a full queue fails the future, verify before start raises."""
+
+import random
+
+import pytest
+
+from oracle import c_oracle as C
+from oracle.keys import interop_sk
+from teku_amd.service import AggregatingSignatureVerificationService, ServiceCapacityExceededException
+
+
+@pytest.fixture(scope="module")
+def keyset():
+    sks = [interop_sk(i) for i in range(12)]
+    pks = [C.sk_to_pk(s) for s in sks]
+    msgs = [bytes([i + 7]) * 32 for i in range(12)]
+    sigs = [C.sign(s, m) for s, m in zip(sks, msgs)]
+    return pks, msgs, sigs
+
+
+def _oracle_batch(sets):
+    assert all(npk == 1 for _, npk, _, _ in sets)
+    rng = random.Random(len(sets))
+    if len(sets) == 1:
+        sets = sets * 2  # the oracle's batch takes n >= 2; (s, s) is valid iff s is
+    return C.batch_verify([s[0] for s in sets], [s[2] for s in sets], [s[3] for s in sets], [rng.getrandbits(63) | 1 for _ in sets])
+
+
+def _oracle_each(sets):
+    return [_oracle_batch([s]) for s in sets]
+
+
+def _svc(**kw):
+    calls = {"batch": 0, "each": 0}
+
+    def b(sets):
+        calls["batch"] += 1
+        return _oracle_batch(sets)
+
+    def e(sets):
+        calls["each"] += 1
+        return _oracle_each(sets)
+
+    s = AggregatingSignatureVerificationService(batch_fn=b, each_fn=e, **kw)
+    return s, calls
+
+
+def test_valid_and_invalid_tasks_one_batch(keyset):
+    pks, msgs, sigs = keyset
+    svc, calls = _svc(max_batch_size=64)
+    bad = {3, 8}
+    tasks = []
+    for i in range(12):
+        sig = sigs[(i + 1) % 12] if i in bad else sigs[i]
+        tasks.append(SignatureTaskArgs(pks[i], msgs[i], sig))
+    # drive one batch directly (deterministic batching)
+    from teku_amd.service import SignatureTask, _set_tuple
+
+    ts = [SignatureTask([_set_tuple([t.pk], t.msg, t.sig)]) for t in tasks]
+    svc.batch_verify_signatures(ts)
+    assert [t.result.result() for t in ts] == [i not in bad for i in range(12)]
+    assert calls == {"batch": 1, "each": 1}  # one failed batch -> one per-set pass, no halving
+    assert svc.batch_count == 1 and svc.task_count == 12
+
+
+def test_split_fallback_matches_reference_halving(keyset):
+    pks, msgs, sigs = keyset
+    from teku_amd.service import SignatureTask, _set_tuple
+
+    svc, calls = _svc(split_fallback=True, min_batch_size_to_split=4)
+    ts = [SignatureTask([_set_tuple([pks[i]], msgs[i], sigs[i] if i != 5 else sigs[6])]) for i in range(12)]
+    svc.batch_verify_signatures(ts)
+    assert [t.result.result() for t in ts] == [i != 5 for i in range(12)]
+    assert calls["batch"] > 1  # halving re-verifies sub-batches
+
+
+def test_multi_set_task_and_threads(keyset):
+    pks, msgs, sigs = keyset
+    svc, _ = _svc(max_batch_size=5)
+    svc.start()
+    try:
+        good = svc.verify_many([[pks[0]], [pks[1]]], [msgs[0], msgs[1]], [sigs[0], sigs[1]])
+        mixed = svc.verify_many([[pks[2]], [pks[3]]], [msgs[2], msgs[3]], [sigs[2], sigs[2]])
+        single = [svc.verify([pks[i]], msgs[i], sigs[i]) for i in range(4, 12)]
+        empty = svc.verify_many([], [], [])
+        assert good.result(timeout=60) is True
+        assert mixed.result(timeout=60) is False
+        assert all(f.result(timeout=60) for f in single)
+        assert empty.result(timeout=60) is False
+        with pytest.raises(Exception):
+            svc.verify_many([[pks[0]]], [msgs[0], msgs[1]], [sigs[0]]).result(timeout=5)
+    finally:
+        svc.stop()
+
+
+def test_queue_full_and_not_running(keyset):
+    pks, msgs, sigs = keyset
+    svc, _ = _svc(queue_capacity=1)
+    with pytest.raises(RuntimeError):
+        svc.verify([pks[0]], msgs[0], sigs[0])
+    svc._running = True  # accept without workers draining
+    f1 = svc.verify([pks[0]], msgs[0], sigs[0])
+    f2 = svc.verify([pks[1]], msgs[1], sigs[1])
+    assert not f1.done()
+    with pytest.raises(ServiceCapacityExceededException):
+        f2.result(timeout=1)
+    assert svc.queue_size() == 1
+
+
+class SignatureTaskArgs:
+    def __init__(self, pk, msg, sig):
+        self.pk, self.msg, self.sig = pk, msg, sig
