@@ -154,6 +154,20 @@ int tbls_fast_aggregate_verify_many(const tbls_set* sets, size_t n, int* ok_per_
  * over n_gpus devices (0 = all). */
 int tbls_verify_each(const tbls_set* sets, size_t n, int n_gpus, int* ok_per_set);
 
+/* ---- batched deserialization and aggregation ----
+ * Gossip decoding validates every key / signature it sees (lazy
+ * BLSSignature.getSignature, BLSSignature.java:83-87; the eth reference
+ * tests' deserialization_G1/G2 executors), and aggregators sum signature
+ * groups (BLS.aggregate from AggregateAttestationBuilder.java:74 and
+ * SyncCommitteeMessagePool.java:200).  One device pass for all items:
+ * codes[i] as tbls_pk_validate / tbls_sig_validate (is_inf nullable). */
+int tbls_pk_validate_many(const uint8_t* pks, size_t n, uint8_t* codes);
+int tbls_sig_validate_many(const uint8_t* sigs, size_t n, uint8_t* codes, uint8_t* is_inf);
+/* Group g = sigs[off[g], off[g+1]) (96 B each) -> out[96 g] with
+ * tbls_aggregate_sigs semantics; status[g] = first failing code, 0 = ok
+ * (then out is meaningless).  An empty group gives the infinity signature. */
+int tbls_aggregate_sigs_many(const uint8_t* sigs, const uint32_t* off, size_t groups, uint8_t* out, int* status);
+
 /* aggregateVerify (BLS.java:144-170, BlstSignature.java:104-122): n distinct
  * (pk, msg) pairs against one aggregate signature. */
 int tbls_aggregate_verify(const uint8_t* pks, const uint8_t* const* msgs, const uint32_t* msg_lens, size_t n,

@@ -400,6 +400,50 @@ def verify_each_raw(sets, n_gpus=0) -> List[bool]:
     return [v == 1 for v in ok]
 
 
+def validate_public_keys(pks) -> List[int]:
+    """Per-key status (0 = valid; else as tbls_pk_validate) of 48-byte keys in
+    one device pass (tbls_pk_validate_many)."""
+    n = len(pks)
+    if n == 0:
+        return []
+    codes = ctypes.create_string_buffer(n)
+    native.check(native.lib().tbls_pk_validate_many(b"".join(bytes(p) for p in pks), n, codes), "tbls_pk_validate_many")
+    return list(codes.raw[:n])
+
+
+def validate_signatures(sigs):
+    """(codes, is_infinity) of 96-byte signatures in one device pass
+    (tbls_sig_validate_many): decode + G2 check, as tbls_sig_validate."""
+    n = len(sigs)
+    if n == 0:
+        return [], []
+    codes, inf = ctypes.create_string_buffer(n), ctypes.create_string_buffer(n)
+    native.check(native.lib().tbls_sig_validate_many(b"".join(bytes(s) for s in sigs), n, codes, inf), "tbls_sig_validate_many")
+    return list(codes.raw[:n]), [b == 1 for b in inf.raw[:n]]
+
+
+def aggregate_signature_groups(groups):
+    """BlstSignature.aggregate (BlstSignature.java:57-68) over many groups of
+    96-byte signatures in one device pass (tbls_aggregate_sigs_many).  Returns
+    per group the 96-byte aggregate, or a BlsException for a group holding an
+    undecodable / non-G2 signature."""
+    G = len(groups)
+    if G == 0:
+        return []
+    off = [0]
+    for g in groups:
+        off.append(off[-1] + len(g))
+    offs = (ctypes.c_uint32 * (G + 1))(*off)
+    out = ctypes.create_string_buffer(96 * G)
+    status = (ctypes.c_int * G)()
+    blob = b"".join(bytes(s) for g in groups for s in g) or b"\0"
+    native.check(native.lib().tbls_aggregate_sigs_many(blob, offs, G, out, status), "tbls_aggregate_sigs_many")
+    return [
+        BlsException(f"Failed to aggregate signatures (code {status[g]})") if status[g] else out.raw[96 * g : 96 * g + 96]
+        for g in range(G)
+    ]
+
+
 class ValidatorKeyTable:
     """Device-resident validator public-key table (SURVEY.md 8(f) rank 1;
     C ABI tbls_pk_table_load / tbls_batch_verify_idx).

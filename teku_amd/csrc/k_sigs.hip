@@ -98,6 +98,42 @@ extern "C" __global__ void __launch_bounds__(TB_BLOCK)
   }
 }
 
+// Many BlstSignature.aggregate calls at once: block g
+// sums group g = sigs[off[g], off[g+1]) with the same rules as
+// k_aggregate_sigs (every input decodes and is in G2; infinity adds nothing;
+// an empty group is the infinity signature, AbstractSignatureTest.java:49-52).
+extern "C" __global__ void __launch_bounds__(TB_BLOCK)
+    k_aggregate_sigs_many(const uint8_t* __restrict__ sigs, const uint32_t* __restrict__ off, uint8_t* __restrict__ out,
+                          int* __restrict__ status) {
+  __shared__ g2j sh[TB_BLOCK];
+  __shared__ int bad;
+  const int t = threadIdx.x;
+  const uint32_t g = blockIdx.x, b = off[g], e = off[g + 1];
+  if (t == 0) bad = 0;
+  __syncthreads();
+  g2j acc = jac_inf<fp2>();
+  for (uint32_t i = b + t; i < e; i += blockDim.x) {
+    g2a a;
+    bool inf;
+    int code = g2_decompress(a, inf, sigs + (size_t)i * 96);
+    if (code == TB_SUCCESS && !inf && !g2_in_group(jac_from_aff(a))) code = TB_POINT_NOT_IN_GROUP;
+    if (code != TB_SUCCESS)
+      atomicCAS(&bad, 0, code);
+    else if (!inf)
+      acc = jac_add(acc, jac_from_aff(a));
+  }
+  sh[t] = acc;
+  __syncthreads();
+  for (int s = TB_BLOCK / 2; s > 0; s >>= 1) {
+    if (t < s) sh[t] = jac_add(sh[t], sh[t + s]);
+    __syncthreads();
+  }
+  if (t == 0) {
+    status[g] = bad;
+    g2_compress_jac(out + (size_t)g * 96, sh[0]);
+  }
+}
+
 // per item: signature validity (decode + G2 check); out code | (inf << 8)
 extern "C" __global__ void __launch_bounds__(TB_BLOCK)
     k_sig_validate(const uint8_t* __restrict__ sigs, uint32_t n, uint32_t* __restrict__ out) {

@@ -844,6 +844,67 @@ extern "C" int tbls_sig_validate(const uint8_t sig[96], int* is_inf) {
   });
 }
 
+// ---- batched deserialization / aggregation ----
+extern "C" int tbls_pk_validate_many(const uint8_t* pks, size_t n, uint8_t* codes) {
+  if (n == 0) return TBLS_SUCCESS;
+  return with_device0([&](dev_ctx& c) -> int {
+    upload u;
+    size_t o = u.add(pks, 48 * n);
+    uint8_t* d;
+    int rc = stage_in(c, u, &d);
+    if (rc) return rc;
+    const size_t aff = align_up(n * sizeof(g1a));
+    if (c.ws.ensure(aff + align_up(n))) return (int)TBLS_DEVICE_ERROR;
+    hipLaunchKernelGGL(k_pk_decompress, dim3((uint32_t)((n + TB_BLOCK - 1) / TB_BLOCK)), dim3(TB_BLOCK), 0, c.stream, d + o, (uint32_t)n,
+                       c.ws.as<g1a>(0), c.ws.as<uint8_t>(aff));
+    return fetch(c, codes, c.ws.as<uint8_t>(aff), n);
+  });
+}
+
+extern "C" int tbls_sig_validate_many(const uint8_t* sigs, size_t n, uint8_t* codes, uint8_t* is_inf) {
+  if (n == 0) return TBLS_SUCCESS;
+  return with_device0([&](dev_ctx& c) -> int {
+    upload u;
+    size_t o = u.add(sigs, 96 * n);
+    uint8_t* d;
+    int rc = stage_in(c, u, &d);
+    if (rc) return rc;
+    if (c.ws.ensure(4 * n)) return (int)TBLS_DEVICE_ERROR;
+    hipLaunchKernelGGL(k_sig_validate, dim3((uint32_t)((n + TB_BLOCK - 1) / TB_BLOCK)), dim3(TB_BLOCK), 0, c.stream, d + o, (uint32_t)n,
+                       c.ws.as<uint32_t>(0));
+    std::vector<uint32_t> v(n);
+    rc = fetch(c, v.data(), c.ws.as<uint32_t>(0), 4 * n);
+    if (rc) return rc;
+    for (size_t i = 0; i < n; i++) {
+      codes[i] = (uint8_t)(v[i] & 0xff);
+      if (is_inf) is_inf[i] = (uint8_t)((v[i] >> 8) & 1);
+    }
+    return TBLS_SUCCESS;
+  });
+}
+
+extern "C" int tbls_aggregate_sigs_many(const uint8_t* sigs, const uint32_t* off, size_t groups, uint8_t* out, int* status) {
+  if (groups == 0) return TBLS_SUCCESS;
+  for (size_t g = 0; g < groups; g++)
+    if (off[g + 1] < off[g]) return TBLS_BAD_ARGUMENT;
+  const size_t total = off[groups];
+  return with_device0([&](dev_ctx& c) -> int {
+    upload u;
+    size_t os = u.add(sigs, 96 * total);
+    size_t oo = u.add(off, 4 * (groups + 1));
+    uint8_t* d;
+    int rc = stage_in(c, u, &d);
+    if (rc) return rc;
+    const size_t ob = align_up(96 * groups);
+    if (c.ws.ensure(ob + 4 * groups)) return (int)TBLS_DEVICE_ERROR;
+    hipLaunchKernelGGL(k_aggregate_sigs_many, dim3((uint32_t)groups), dim3(TB_BLOCK), 0, c.stream, d + os, (const uint32_t*)(d + oo),
+                       c.ws.as<uint8_t>(0), c.ws.as<int>(ob));
+    rc = fetch(c, status, c.ws.as<int>(ob), 4 * groups);
+    if (rc) return rc;
+    return fetch(c, out, c.ws.as<uint8_t>(0), 96 * groups);
+  });
+}
+
 extern "C" int tbls_aggregate_pks(const uint8_t* pks, size_t k, uint8_t out[48]) {
   if (k == 0) return TBLS_BAD_ARGUMENT;  // BlstPublicKey.java:56 checkArgument
   return with_device0([&](dev_ctx& c) -> int {

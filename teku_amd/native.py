@@ -114,6 +114,9 @@ _SIGS = {
     ),
     "tbls_fast_aggregate_verify_many": (ctypes.c_int, [ctypes.POINTER(TblsSet), ctypes.c_size_t, ctypes.POINTER(ctypes.c_int)]),
     "tbls_verify_each": (ctypes.c_int, [ctypes.POINTER(TblsSet), ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
+    "tbls_pk_validate_many": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p]),
+    "tbls_sig_validate_many": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_char_p]),
+    "tbls_aggregate_sigs_many": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint32), ctypes.c_size_t, ctypes.c_char_p, ctypes.POINTER(ctypes.c_int)]),
     "tbls_aggregate_verify": (
         ctypes.c_int,
         [

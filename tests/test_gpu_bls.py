@@ -440,3 +440,34 @@ def test_verify_each_and_service(hip, sets8):
     svc.batch_verify_signatures(tasks)
     assert [t.result.result() for t in tasks] == [e for s, e in zip(sets, exp) if s[1] > 0]
     assert svc.device_passes == 2
+
+
+def test_batched_deserialization_and_aggregation(hip, sets8):
+    """Batched key / signature validation and grouped signature aggregation
+     equal the one-at-a-time C ABI calls item by item
+    and the oracle's aggregate bytes: valid keys / sigs, infinity, zero bytes,
+    0x9378a6... key, non-G2 signature, an empty group (-> infinity) and a
+    group holding a non-G2 signature (-> BlsException)."""
+    bls, native, L, impl = hip
+    sks, pks, msgs, sigs = sets8
+    keys = list(pks) + [O.INFINITY_G1, BAD_PK, bytes(48), bytes([0x80]) + bytes(47)]
+    codes = bls.validate_public_keys(keys)
+    assert codes == [L.tbls_pk_validate(k) for k in keys]
+    assert codes[:8] == [0] * 8 and all(c != 0 for c in codes[8:])
+    ss = list(sigs) + [O.INFINITY_G2, bytes(96), NOT_IN_G2]
+    codes, infs = bls.validate_signatures(ss)
+    for s, c, f in zip(ss, codes, infs):
+        inf = ctypes.c_int(0)
+        assert c == L.tbls_sig_validate(s, ctypes.byref(inf)) and f == bool(inf.value)
+    assert codes[:9] == [0] * 9 and infs[8] and codes[9] != 0 and codes[10] != 0
+    groups = [sigs[:3], sigs[3:4], [], sigs[4:8] + [O.INFINITY_G2], [sigs[0], NOT_IN_G2], list(sigs)]
+    got = bls.aggregate_signature_groups(groups)
+    for g, r in zip(groups, got):
+        if NOT_IN_G2 in g:
+            assert isinstance(r, bls.BlsException)
+            continue
+        assert r == (O.aggregate_sigs(g) if g else O.INFINITY_G2)
+        one = ctypes.create_string_buffer(96)
+        if g:
+            native.check(L.tbls_aggregate_sigs(b"".join(g), len(g), one), "aggregate_sigs")
+            assert one.raw == r
