@@ -710,6 +710,10 @@ extern "C" int tbls_verify(const uint8_t pk[48], const uint8_t* msg, size_t len,
   return TBLS_SUCCESS;
 }
 
+// k_each.hip (declared here rather than in tb_kdecl.h)
+extern "C" __global__ void k_each_miller(const g1a* __restrict__ P, const g2a* __restrict__ Q, const uint8_t* __restrict__ skip, const uint8_t* __restrict__ set_code, const g2a* __restrict__ sig_aff, const uint8_t* __restrict__ sig_use, const uint8_t* __restrict__ sig_code, uint32_t n, fp12* __restrict__ f, uint8_t* __restrict__ use);
+extern "C" __global__ void k_each_final_wave(const fp12* __restrict__ f, const uint8_t* __restrict__ use, uint8_t* __restrict__ ok);
+
 // Per-set fastAggregateVerify verdicts for sets[lo, hi) on device d in one
 // pass (k_each.hip): shared per-set stages with r = 1, then one thread per set
 // for its two-pair Miller loop and final exponentiation.
@@ -737,6 +741,8 @@ static int run_each(int d, const tbls_set* sets, size_t lo, size_t hi, uint8_t* 
   const size_t sig_use = o;  o = align_up(o + n);
   const size_t okd = o;      o = align_up(o + n);
   const size_t n_bad = o;    o = align_up(o + 4);
+  const size_t fv = o;       o = align_up(o + (size_t)n * sizeof(fp12));
+  const size_t use = o;      o = align_up(o + n);
   if (c->ws.ensure(o)) return TBLS_DEVICE_ERROR;
   uint8_t* w = c->ws.as<uint8_t>();
   const dim3 blk(TB_BLOCK), g((n + TB_BLOCK - 1) / TB_BLOCK);
@@ -750,9 +756,20 @@ static int run_each(int d, const tbls_set* sets, size_t lo, size_t hi, uint8_t* 
   hipLaunchKernelGGL(k_sig_check, g, blk, 0, s, di + p.off_sigs, n, (g2a*)(w + sig_aff), w + sig_use, w + sig_code, (uint32_t*)(w + n_bad));
   hipLaunchKernelGGL(k_set_hash, g, blk, 0, s, di + p.off_msgs, (const uint32_t*)(di + p.off_msgoff), di + p.off_dst, 43u, n, (g2a*)(w + Q),
                      w + skip);
-  hipLaunchKernelGGL(k_verify_each, g, blk, 0, s, (const g1a*)(w + P), (const g2a*)(w + Q), (const uint8_t*)(w + skip),
-                     (const uint8_t*)(w + set_code), (const g2a*)(w + sig_aff), (const uint8_t*)(w + sig_use), (const uint8_t*)(w + sig_code),
-                     n, w + okd);
+  // A/B (profiles/r01_bench_each_*): the wave final exponentiation runs its
+  // Fp12 inversion serially on lane 0, which at one wave per set costs more
+  // than it saves; TBLS_EACH_WAVE=1 selects it.
+  static const bool wave = getenv("TBLS_EACH_WAVE") && getenv("TBLS_EACH_WAVE")[0] == '1';
+  if (!wave) {
+    hipLaunchKernelGGL(k_verify_each, g, blk, 0, s, (const g1a*)(w + P), (const g2a*)(w + Q), (const uint8_t*)(w + skip),
+                       (const uint8_t*)(w + set_code), (const g2a*)(w + sig_aff), (const uint8_t*)(w + sig_use),
+                       (const uint8_t*)(w + sig_code), n, w + okd);
+  } else {
+    hipLaunchKernelGGL(k_each_miller, g, blk, 0, s, (const g1a*)(w + P), (const g2a*)(w + Q), (const uint8_t*)(w + skip),
+                       (const uint8_t*)(w + set_code), (const g2a*)(w + sig_aff), (const uint8_t*)(w + sig_use),
+                       (const uint8_t*)(w + sig_code), n, (fp12*)(w + fv), w + use);
+    hipLaunchKernelGGL(k_each_final_wave, dim3(n), dim3(64), 0, s, (const fp12*)(w + fv), (const uint8_t*)(w + use), w + okd);
+  }
   HIPCHK(hipGetLastError());
   if (c->hout.ensure(n)) return TBLS_DEVICE_ERROR;
   HIPCHK(hipMemcpyAsync(c->hout.p, w + okd, n, hipMemcpyDeviceToHost, s));
