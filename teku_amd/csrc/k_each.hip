@@ -10,9 +10,11 @@
 //   k_pk_decompress, k_set_pk (r = 1), k_sig_check, k_set_hash   (shared stages)
 //   k_verify_each      per set (one thread): final_exp(Miller(apk_i, H(m_i)) * Miller(-g1, sig_i)) == 1
 //
-// (A/B alternative, TBLS_EACH_WAVE=1: k_each_miller per thread, then
-// k_each_final_wave, one wave per set.  Measured slower at 16384 sets: 150 ms
-// vs 115 ms per pass, because the wave final exponentiation inverts on one lane.)
+// (A/B alternative, TBLS_EACH_WAVE=1: k_each_miller per thread -- Miller loop
+// and the easy part of the final exponentiation, whose Fp12 inversion is
+// serial -- then k_each_final_wave, the hard part with one wave per set.  With
+// the whole final exponentiation in the wave, lane 0's inversion made it slower
+// than one lane per set: 150 ms vs 115 ms per 16384-set pass.)
 //
 // The Miller loop is the two-pair loop (shared f^2 per step); a set that failed any stage (invalid or
 // infinite aggregate key, undecodable / non-G2 signature) is 0 without a
@@ -37,17 +39,43 @@ extern "C" __global__ void __launch_bounds__(TB_BLOCK)
   g1a g;
   g.x = fp_from_const(G1_X);
   g.y = fp_from_const(G1_NEG_Y);
-  f[i] = miller_loop2(P[i], Q[i], false, g, sig_aff[i], sig_use[i] == 0);
+  const fp12 m = miller_loop2(P[i], Q[i], false, g, sig_aff[i], sig_use[i] == 0);
+  // easy part of the final exponentiation in-lane (its Fp12 inversion is serial):
+  // t = m^((p^6 - 1)(p^2 + 1)); the wave kernel runs the hard part
+  fp12 t = fp12_mul(fp12_conj(m), fp12_inv(m));
+  f[i] = fp12_mul(fp12_frob(fp12_frob(t)), t);
   use[i] = 1;
 }
 
-// Final exponentiation part: one 64-lane wave per set (tb_fp12_wave.h
-// final_exp_wave, as the batch's k_final_verify_wave), so n sets keep n waves
-// in flight instead of n lanes.
+// Hard part of the final exponentiation: one 64-lane wave per set, so n sets
+// keep n waves in flight instead of n lanes.
 __device__ TB_INLINE void each_load(fp* dst, const fp12* src) {
   const int l = threadIdx.x;
   if (l < 12) dst[l] = reinterpret_cast<const fp*>(src)[l];
   __syncthreads();
+}
+
+// hard part of tb_fp12_wave.h final_exp_wave (x3), from t = L.T into L.F
+__device__ TB_INLINE void final_exp_hard_wave(final_exp_lds& L) {
+  w_cyc_exp_x(L.E, L.T, L.s);
+  w_conj(L.X, L.T);
+  w_mul(L.A, L.E, L.X, L.s);  // a = t^(x-1)
+  w_cyc_exp_x(L.E, L.A, L.s);
+  w_conj(L.X, L.A);
+  w_mul(L.A, L.E, L.X, L.s);  // a = t^((x-1)^2)
+  w_cyc_exp_x(L.E, L.A, L.s);
+  w_frob(L.X, L.A);
+  w_mul(L.B, L.E, L.X, L.s);  // b = a^(x+p)
+  w_cyc_exp_x(L.E, L.B, L.s);
+  w_cyc_exp_x(L.C, L.E, L.s);
+  w_frob(L.X, L.B);
+  w_frob(L.X, L.X);
+  w_mul(L.C, L.C, L.X, L.s);
+  w_conj(L.X, L.B);
+  w_mul(L.C, L.C, L.X, L.s);  // c = b^(x^2+p^2-1)
+  w_cyc_sqr(L.X, L.T, L.s);
+  w_mul(L.X, L.X, L.T, L.s);  // t^3
+  w_mul(L.F, L.C, L.X, L.s);
 }
 
 extern "C" __global__ void __launch_bounds__(64)
@@ -59,8 +87,8 @@ extern "C" __global__ void __launch_bounds__(64)
     return;
   }
   w12_tabs_load(L.s);
-  each_load(L.F, f + i);
-  final_exp_wave(L);
+  each_load(L.T, f + i);
+  final_exp_hard_wave(L);
   if (threadIdx.x == 0) ok[i] = fp12_is_one(fp12_from_coords(L.F)) ? 1 : 0;
 }
 
