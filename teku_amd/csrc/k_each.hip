@@ -109,3 +109,63 @@ extern "C" __global__ void __launch_bounds__(TB_BLOCK)
   const fp12 f = miller_loop2(P[i], Q[i], false, g, sig_aff[i], sig_use[i] == 0);
   ok[i] = fp12_is_one(final_exp(f)) ? 1 : 0;
 }
+
+// ---------------------------------------------------------------------------
+// Group testing (TBLS_EACH_GROUP=1): randomized Miller values, one final
+// exponentiation per group of sets, then one per member of a failing group.
+// f_i = Miller(r_i apk_i, H(m_i)) * Miller(-g1, r_i sig_i) with the batch's
+// 64-bit randomizers, so a group product is 1 after the final exponentiation
+// iff every member is valid (up to the batch path's 2^-64 soundness).
+// Sets that failed a stage get f_i = 1 and use_i = 0.
+// ---------------------------------------------------------------------------
+extern "C" __global__ void __launch_bounds__(TB_BLOCK)
+    k_each_miller_r(const g1a* __restrict__ P, const g2a* __restrict__ Q, const uint8_t* __restrict__ skip,
+                    const uint8_t* __restrict__ set_code, const g2j* __restrict__ rsig, const uint8_t* __restrict__ sig_code,
+                    uint32_t n, fp12* __restrict__ f, uint8_t* __restrict__ use) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  if (set_code[i] != 0 || sig_code[i] != 0 || skip[i] != 0) {
+    f[i] = fp12_one();
+    use[i] = 0;
+    return;
+  }
+  g1a g;
+  g.x = fp_from_const(G1_X);
+  g.y = fp_from_const(G1_NEG_Y);
+  g2a s;
+  const bool finite = jac_to_aff(s, rsig[i]);  // an infinite signature adds no pair
+  f[i] = miller_loop2(P[i], Q[i], false, g, s, !finite);
+  use[i] = 1;
+}
+
+// block g: gok[g] = final_exp(prod f[g*gsz, min(n, (g+1)*gsz))) == 1
+extern "C" __global__ void __launch_bounds__(64)
+    k_each_group_wave(const fp12* __restrict__ f, uint32_t n, uint32_t gsz, uint8_t* __restrict__ gok) {
+  __shared__ final_exp_lds L;
+  const uint32_t b = blockIdx.x * gsz;
+  const uint32_t e = b + gsz < n ? b + gsz : n;
+  w12_tabs_load(L.s);
+  each_load(L.F, f + b);
+  for (uint32_t i = b + 1; i < e; i++) {
+    each_load(L.X, f + i);
+    w_mul(L.F, L.F, L.X, L.s);
+  }
+  final_exp_wave(L);
+  if (threadIdx.x == 0) gok[blockIdx.x] = fp12_is_one(fp12_from_coords(L.F)) ? 1 : 0;
+}
+
+// block j: ok[idx[j]] = use && final_exp(f[idx[j]]) == 1
+extern "C" __global__ void __launch_bounds__(64)
+    k_each_member_wave(const fp12* __restrict__ f, const uint8_t* __restrict__ use, const uint32_t* __restrict__ idx,
+                       uint8_t* __restrict__ ok) {
+  __shared__ final_exp_lds L;
+  const uint32_t i = idx[blockIdx.x];
+  if (!use[i]) {
+    if (threadIdx.x == 0) ok[i] = 0;
+    return;
+  }
+  w12_tabs_load(L.s);
+  each_load(L.F, f + i);
+  final_exp_wave(L);
+  if (threadIdx.x == 0) ok[i] = fp12_is_one(fp12_from_coords(L.F)) ? 1 : 0;
+}

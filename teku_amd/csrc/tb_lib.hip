@@ -11,6 +11,7 @@
 #include <cstring>
 #include <mutex>
 #include <algorithm>
+#include <random>
 #include <thread>
 #include <type_traits>
 #include <vector>
@@ -713,6 +714,10 @@ extern "C" int tbls_verify(const uint8_t pk[48], const uint8_t* msg, size_t len,
 // k_each.hip (declared here rather than in tb_kdecl.h)
 extern "C" __global__ void k_each_miller(const g1a* __restrict__ P, const g2a* __restrict__ Q, const uint8_t* __restrict__ skip, const uint8_t* __restrict__ set_code, const g2a* __restrict__ sig_aff, const uint8_t* __restrict__ sig_use, const uint8_t* __restrict__ sig_code, uint32_t n, fp12* __restrict__ f, uint8_t* __restrict__ use);
 extern "C" __global__ void k_each_final_wave(const fp12* __restrict__ f, const uint8_t* __restrict__ use, uint8_t* __restrict__ ok);
+extern "C" __global__ void k_each_miller_r(const g1a* __restrict__ P, const g2a* __restrict__ Q, const uint8_t* __restrict__ skip, const uint8_t* __restrict__ set_code, const g2j* __restrict__ rsig, const uint8_t* __restrict__ sig_code, uint32_t n, fp12* __restrict__ f, uint8_t* __restrict__ use);
+extern "C" __global__ void k_each_group_wave(const fp12* __restrict__ f, uint32_t n, uint32_t gsz, uint8_t* __restrict__ gok);
+extern "C" __global__ void k_each_member_wave(const fp12* __restrict__ f, const uint8_t* __restrict__ use, const uint32_t* __restrict__ idx, uint8_t* __restrict__ ok);
+#define TB_EACH_GROUP 64u  // sets per group-tested final exponentiation
 
 // Per-set fastAggregateVerify verdicts for sets[lo, hi) on device d in one
 // pass (k_each.hip): shared per-set stages with r = 1, then one thread per set
@@ -724,7 +729,14 @@ static int run_each(int d, const tbls_set* sets, size_t lo, size_t hi, uint8_t* 
   HIPCHK(hipSetDevice(c->dev));
   packed p = pack_layout(sets, lo, hi, 43);
   if (c->hin.ensure(p.total + 256) || c->in.ensure(p.total + 256)) return TBLS_DEVICE_ERROR;
-  pack_fill(c->hin.b(), p, sets, lo, nullptr, ETH2_DST, 43);  // r = 1 for every set
+  static const bool group = getenv("TBLS_EACH_GROUP") && getenv("TBLS_EACH_GROUP")[0] == '1';
+  std::vector<uint64_t> rnd;
+  if (group) {  // per-call randomizers in [1, 2^64) from the OS entropy source
+    std::random_device rd;
+    rnd.resize(hi);
+    for (size_t i = lo; i < hi; i++) rnd[i] = ((((uint64_t)rd()) << 32) | rd()) | 1u;
+  }
+  pack_fill(c->hin.b(), p, sets, lo, group ? rnd.data() : nullptr, ETH2_DST, 43);  // else r = 1 for every set
   hipStream_t s = c->stream;
   HIPCHK(hipMemcpyAsync(c->in.p, c->hin.p, p.total, hipMemcpyHostToDevice, s));
   const uint8_t* di = c->in.as<uint8_t>();
@@ -743,6 +755,10 @@ static int run_each(int d, const tbls_set* sets, size_t lo, size_t hi, uint8_t* 
   const size_t n_bad = o;    o = align_up(o + 4);
   const size_t fv = o;       o = align_up(o + (size_t)n * sizeof(fp12));
   const size_t use = o;      o = align_up(o + n);
+  const size_t rsig = o;     o = align_up(o + (group ? (size_t)n * sizeof(g2j) : 0));
+  const uint32_t ngrp = (n + TB_EACH_GROUP - 1) / TB_EACH_GROUP;
+  const size_t gok = o;      o = align_up(o + ngrp);
+  const size_t midx = o;     o = align_up(o + (group ? (size_t)n * 4 : 0));
   if (c->ws.ensure(o)) return TBLS_DEVICE_ERROR;
   uint8_t* w = c->ws.as<uint8_t>();
   const dim3 blk(TB_BLOCK), g((n + TB_BLOCK - 1) / TB_BLOCK);
@@ -753,9 +769,44 @@ static int run_each(int d, const tbls_set* sets, size_t lo, size_t hi, uint8_t* 
                        w + pk_code);
   hipLaunchKernelGGL(k_set_pk, g, blk, 0, s, (const uint32_t*)(di + p.off_pkoff), (const g1a*)(w + pk_aff), (const uint8_t*)(w + pk_code),
                      (const uint64_t*)(di + p.off_rand), n, (g1a*)(w + P), w + set_code, (uint32_t*)(w + n_bad), nullptr);
-  hipLaunchKernelGGL(k_sig_check, g, blk, 0, s, di + p.off_sigs, n, (g2a*)(w + sig_aff), w + sig_use, w + sig_code, (uint32_t*)(w + n_bad));
+  if (group)
+    hipLaunchKernelGGL(k_set_sig, g, blk, 0, s, di + p.off_sigs, (const uint64_t*)(di + p.off_rand), n, (g2j*)(w + rsig), w + sig_code,
+                       (uint32_t*)(w + n_bad));
+  else
+    hipLaunchKernelGGL(k_sig_check, g, blk, 0, s, di + p.off_sigs, n, (g2a*)(w + sig_aff), w + sig_use, w + sig_code, (uint32_t*)(w + n_bad));
   hipLaunchKernelGGL(k_set_hash, g, blk, 0, s, di + p.off_msgs, (const uint32_t*)(di + p.off_msgoff), di + p.off_dst, 43u, n, (g2a*)(w + Q),
                      w + skip);
+  if (group) {
+    // randomized Miller values; one final exponentiation per group of sets, then
+    // one per member of each failing group (k_each.hip)
+    hipLaunchKernelGGL(k_each_miller_r, g, blk, 0, s, (const g1a*)(w + P), (const g2a*)(w + Q), (const uint8_t*)(w + skip),
+                       (const uint8_t*)(w + set_code), (const g2j*)(w + rsig), (const uint8_t*)(w + sig_code), n, (fp12*)(w + fv), w + use);
+    hipLaunchKernelGGL(k_each_group_wave, dim3(ngrp), dim3(64), 0, s, (const fp12*)(w + fv), n, TB_EACH_GROUP, w + gok);
+    HIPCHK(hipGetLastError());
+    if (c->hout.ensure(2 * (size_t)n + ngrp)) return TBLS_DEVICE_ERROR;
+    uint8_t* hu = c->hout.b();
+    HIPCHK(hipMemcpyAsync(hu, w + use, n, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(hu + n, w + gok, ngrp, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    std::vector<uint32_t> members;
+    for (uint32_t i = 0; i < n; i++) {
+      if (hu[n + i / TB_EACH_GROUP])
+        ok_host[i] = hu[i];  // group passed: every finite member is valid
+      else
+        members.push_back(i);
+    }
+    if (!members.empty()) {
+      const uint32_t m = (uint32_t)members.size();
+      HIPCHK(hipMemcpyAsync(w + midx, members.data(), 4 * (size_t)m, hipMemcpyHostToDevice, s));
+      hipLaunchKernelGGL(k_each_member_wave, dim3(m), dim3(64), 0, s, (const fp12*)(w + fv), (const uint8_t*)(w + use),
+                         (const uint32_t*)(w + midx), w + okd);
+      HIPCHK(hipGetLastError());
+      HIPCHK(hipMemcpyAsync(hu + n + ngrp, w + okd, n, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));
+      for (uint32_t i : members) ok_host[i] = hu[n + ngrp + i];
+    }
+    return TBLS_SUCCESS;
+  }
   // A/B (profiles/r01_bench_each_*): the wave final exponentiation runs its
   // Fp12 inversion serially on lane 0, which at one wave per set costs more
   // than it saves; TBLS_EACH_WAVE=1 selects it.
