@@ -8,20 +8,26 @@ partials -> rank 0 multiplies them and runs one final exponentiation.  This is
 config 5's per-GPU shard (1,048,576 sets over 8 GPUs = 131,072 per GPU) with
 weak scaling; inputs are resident in HBM before the timed region.
 
-Also reported: p50/p99 latency of a 128-set batchVerify (config 1 shape)
-through the host C ABI (API entry -> boolean, PCIe upload included), the
-per-stage kernel times, the integer-VALU roofline of the dominant kernel, and a
-CPU baseline (the oracle, timed on a bounded sample on this host).
+Also reported on rank 0 (extra keys of the same JSON line):
+  * config 1: p50/p99 latency of a 128-set batchVerify through the host C ABI
+    (API entry -> boolean, PCIe upload included), >= 100 repetitions;
+  * config 2: 64 x 512-key fastAggregateVerify (tbls_fast_aggregate_verify_many);
+  * config 3: 64 x 488-key randomized batchVerify (keys as bytes, and from the
+    device-resident key table), with the aggregation kernel's roofline;
+  * config 4: 16,384 single-signer sets through the host C ABI (the service's
+    batch), and the failure-path settle time with 4 bad signatures;
+  * the per-stage kernel times and the integer-MAC roofline of the dominant
+    kernel on SURVEY.md 8(d)'s model (300 MAC per Fp product);
+  * the CPU baseline: the C oracle timed on this host's cores (N threads and
+    1 thread, CPU model stated) on a bounded sample of the same workload.
 
 python bench.py --gpus N --steps K --warmup W
 """
 
 import argparse
 import ctypes
-import hashlib
 import json
 import os
-import secrets
 import statistics
 import sys
 import time
@@ -32,138 +38,262 @@ sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-from teku_amd import native  # noqa: E402
+from teku_amd import native, synth  # noqa: E402
 from teku_amd.dist import all_gather_partials, shard_bounds  # noqa: E402
 
-R_ORDER = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
-DST = b"BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_POP_"
-
-# Algorithmic work per unit: Fp products (and their v_mad_u64_u32 count),
-# counted by tools/count_muls.py on the hostsim build of the same stage code.
+# ---------------------------------------------------------------------------
+# Roofline: algorithmic work = Fp products (M) per unit,
+# counted by tools/count_muls.py on the host build of the same stage code,
+# x 300 32x32->64 MACs per M (12-limb CIOS Montgomery, 2*12^2 + 12).  Peak =
+# the measured v_mad_u64_u32 issue rate (tools/microbench/fp_rates.hip,
+# profiles/r01_microbench_fp_rates.json: 47.6 lane-ops/CU/clk) x CUs x 2.4 GHz.
+# The kernels' own 14 x 29-bit products issue 392 v_mad_u64_u32 per M (301
+# per squaring); "issue_frac" reports that instruction-level fraction too.
+# ---------------------------------------------------------------------------
+MAC_PER_M = 300
+MAD_RATE_PER_CU_CLK = 47.6
+CLOCK_HZ = 2.4e9
 STAGES = ["pk_decompress", "set_pk", "set_sig", "set_hash", "g2_sum", "miller", "fp12_prod"]
-M_PER_UNIT = json.load(open(os.path.join(ROOT, "tools", "mul_counts.json"))) if os.path.exists(
-    os.path.join(ROOT, "tools", "mul_counts.json")
-) else {}
+STAGE_KERNEL = {
+    "pk_decompress": "k_pk_decompress",
+    "set_pk": "k_set_pk",
+    "set_sig": "k_sig_check",
+    "set_hash": "k_set_hash",
+    "g2_sum": "k_msm_*",
+    "miller": "k_miller2",
+    "fp12_prod": "k_fp12_prod_wave",
+}
+STAGE_UNITS = {"pk_decompress": "keys", "set_pk": "sets", "set_sig": "sets", "set_hash": "sets", "g2_sum": "sets", "miller": "pairs", "fp12_prod": "pairs"}
+_MC = os.path.join(ROOT, "tools", "mul_counts.json")
+M_PER_UNIT = json.load(open(_MC)) if os.path.exists(_MC) else {}
 
 
-def interop_sk(i):
-    h = hashlib.sha256(i.to_bytes(32, "little")).digest()
-    return int.from_bytes(h, "little") % R_ORDER
+def peak_mac_per_s(device):
+    return MAD_RATE_PER_CU_CLK * torch.cuda.get_device_properties(device).multi_processor_count * CLOCK_HZ
 
 
-def bench_message(seed, j):
-    return hashlib.sha256(b"teku-bench" + seed.to_bytes(8, "little") + j.to_bytes(8, "little")).digest()
-
-
-def make_workload(L, first, count, n_keys_uniq=65536):
-    """Synthetic sets [first, first+count): pk/sig generated on the GPU."""
-    kidx = [(first + j) % n_keys_uniq for j in range(count)]
-    uniq = sorted(set(kidx))
-    sk_bytes = {k: interop_sk(k).to_bytes(32, "big") for k in uniq}
-    blob = b"".join(sk_bytes[k] for k in uniq)
-    pk_out = ctypes.create_string_buffer(48 * len(uniq))
-    native.check(L.tbls_sk_to_pk_many(blob, len(uniq), pk_out), "sk_to_pk_many")
-    pk_of = {k: pk_out.raw[48 * i : 48 * i + 48] for i, k in enumerate(uniq)}
-    msgs = [bench_message(0, first + j) for j in range(count)]
-    sks = b"".join(sk_bytes[k] for k in kidx)
-    mb = b"".join(msgs)
-    off = (ctypes.c_uint32 * (count + 1))(*[32 * j for j in range(count + 1)])
-    sig_out = ctypes.create_string_buffer(96 * count)
-    CH = 65536
-    for s in range(0, count, CH):
-        e = min(count, s + CH)
-        o2 = (ctypes.c_uint32 * (e - s + 1))(*[32 * j for j in range(e - s + 1)])
-        tmp = ctypes.create_string_buffer(96 * (e - s))
-        native.check(L.tbls_sign_many(sks[32 * s : 32 * e], mb[32 * s : 32 * e], o2, e - s, DST, len(DST), tmp), "sign_many")
-        ctypes.memmove(ctypes.addressof(sig_out) + 96 * s, tmp, 96 * (e - s))
-    del off
-    pks = b"".join(pk_of[k] for k in kidx)
-    return pks, mb, sig_out.raw
+def roofline_entry(stage_ms, S, device, ms_per_step):
+    peak = peak_mac_per_s(device)
+    mads = M_PER_UNIT.get("mads_per_unit", {})
+    per_stage = {}
+    for i, name in enumerate(STAGES):
+        if name in M_PER_UNIT and stage_ms[i] > 0:
+            per_stage[name] = M_PER_UNIT[name] * MAC_PER_M * S / (stage_ms[i] * 1e-3)
+    dom = max(range(len(STAGES)), key=lambda i: stage_ms[i])  # exclusive times
+    name = STAGES[dom]
+    achieved = per_stage.get(name)
+    kernel = STAGE_KERNEL[name]
+    traffic = None
+    tpath = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(tpath):
+        traffic = json.load(open(tpath)).get(kernel, {}).get("bytes_per_launch")
+    per_set = M_PER_UNIT.get("per_set_total")
+    return {
+        "bound": "valu-int (v_mad_u64_u32 issue)",
+        "kernel": kernel,
+        "achieved": achieved / 1e12 if achieved else None,
+        "peak": peak / 1e12,
+        "unit": "T MAC/s (32x32->64)",
+        "frac": (achieved / peak) if achieved else None,
+        "traffic": traffic,
+        "model": "SURVEY.md 8(d): Fp products per unit (tools/mul_counts.json) x 300 MAC",
+        "units_per_launch": S,
+        "unit_of_work": STAGE_UNITS[name],
+        "fp_products_per_unit": M_PER_UNIT.get(name),
+        "kernel_ms": stage_ms[dom],
+        "issue_frac": (mads[name] * S / (stage_ms[dom] * 1e-3)) / peak if name in mads else None,
+        "stage_frac": {k: v / peak for k, v in per_stage.items()},
+        "pipeline_frac": (per_set * MAC_PER_M * S / (ms_per_step * 1e-3)) / peak if per_set else None,
+    }
 
 
 class DevBatch:
     """A batch resident in HBM (torch tensors) + its tbls_dev_batch descriptor."""
 
-    def __init__(self, pks, msgs, sigs, n, device):
+    def __init__(self, pks, n_pks, msgs, msg_lens, sigs, device, rands=None):
+        n = len(n_pks)
         u8 = lambda b: torch.frombuffer(bytearray(b), dtype=torch.uint8).to(device)  # noqa: E731
+        i32 = lambda v: torch.tensor(v, dtype=torch.int64).to(torch.int32).to(device)  # noqa: E731
         self.pks = u8(pks)
         self.msgs = u8(msgs)
         self.sigs = u8(sigs)
-        self.pk_off = torch.arange(0, n + 1, dtype=torch.int32, device=device)
-        self.msg_off = torch.arange(0, 32 * (n + 1), 32, dtype=torch.int32, device=device)
-        r = [secrets.randbits(64) | 1 for _ in range(n)]  # randomizers in [1, 2^64)
+        off = [0]
+        for k in n_pks:
+            off.append(off[-1] + k)
+        moff = [0]
+        for m in msg_lens:
+            moff.append(moff[-1] + m)
+        self.pk_off = i32(off)
+        self.msg_off = i32(moff)
+        r = rands or synth.random_multipliers(n)
         self.rand = torch.tensor([x - (1 << 64) if x >= (1 << 63) else x for x in r], dtype=torch.int64, device=device)
+        self.n_keys = off[-1]
         self.desc = native.TblsDevBatch(
-            self.pks.data_ptr(), self.pk_off.data_ptr(), n, self.msgs.data_ptr(), self.msg_off.data_ptr(), self.sigs.data_ptr(), self.rand.data_ptr(), n
+            self.pks.data_ptr(), self.pk_off.data_ptr(), self.n_keys, self.msgs.data_ptr(), self.msg_off.data_ptr(), self.sigs.data_ptr(),
+            self.rand.data_ptr(), n
         )
         self.n = n
 
 
-# Integer-MAC roofline.  The bound is the v_mad_u64_u32 issue rate: measured
-# 47.6 lane-ops/CU/clk on MI355X (tools/microbench/fp_rates.hip,
-# profiles/r01_microbench_fp_rates.json) -> x CUs x 2.4 GHz.  Algorithmic work
-# = Fp products per unit (tools/count_muls.py on the same stage code) x 392
-# v_mad_u64_u32 per product (301 per squaring), tools/mul_counts.json.
-MAD_RATE_PER_CU_CLK = 47.6
-CLOCK_HZ = 2.4e9
-STAGE_UNITS = {"pk_decompress": "keys", "set_pk": "sets", "set_sig": "sets", "set_hash": "sets", "g2_sum": "sets", "miller": "pairs", "fp12_prod": "pairs"}
+def timed(fn, reps):
+    out = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        fn()
+        out.append((time.perf_counter() - t0) * 1e3)
+    return sorted(out)
 
 
-def roofline_entry(stage_ms, S, device):
-    props = torch.cuda.get_device_properties(device)
-    peak = MAD_RATE_PER_CU_CLK * props.multi_processor_count * CLOCK_HZ / 1e12  # T mad/s
-    mads = M_PER_UNIT.get("mads_per_unit", {})
-    per_stage = {}
-    for i, name in enumerate(STAGES):
-        if name in mads and stage_ms[i] > 0:
-            per_stage[name] = mads[name] * S / (stage_ms[i] * 1e-3) / 1e12
-    dom = max(range(len(STAGES)), key=lambda i: stage_ms[i])  # exclusive times
-    name = STAGES[dom]
-    achieved = per_stage.get(name)
-    traffic = None
-    tpath = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(tpath):
-        traffic = json.load(open(tpath)).get("k_" + ("miller2" if name == "miller" else name), {}).get("bytes_per_launch")
-    return {
-        "bound": "valu-int (v_mad_u64_u32 issue)",
-        "kernel": "k_" + ("miller2" if name == "miller" else name),
-        "achieved": achieved,
-        "peak": peak,
-        "unit": "T v_mad_u64_u32/s",
-        "frac": (achieved / peak) if achieved else None,
-        "traffic": traffic,
-        "units_per_launch": S,
-        "unit_of_work": STAGE_UNITS[name],
-        "mads_per_unit": mads.get(name),
-        "fp_products_per_unit": M_PER_UNIT.get(name),
-        "kernel_ms": stage_ms[dom],
-        "stage_frac": {k: v / peak for k, v in per_stage.items()},
-    }
+def pct(xs, q):
+    return xs[min(len(xs) - 1, int(q * len(xs)))]
 
 
-def cpu_baseline_oracle(pks, msgs, sigs, sample_sets=4096, threads=16):
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_threads():
+    n = os.cpu_count() or 1
+    for var in ("OMP_NUM_THREADS", "MAX_JOBS"):  # the box's CPU share
+        if os.environ.get(var, "").isdigit():
+            n = min(n, int(os.environ[var]))
+    return max(1, n)
+
+
+def cpu_baseline_oracle(pks, msgs, sigs, sample_sets=4096, sample_1t=512):
     """The C oracle (oracle/c/bls_oracle.c, 'port') timed on this host over a
-    bounded sample of the same workload: the first `sample_sets` sets."""
+    bounded sample of the same workload: the first `sample_sets` sets on every
+    core of this box's share, the first `sample_1t` sets on one thread, and
+    the p50 of a 128-set batch (config 1) on every core."""
     from oracle import c_oracle as C
 
-    threads = max(1, min(threads, os.cpu_count() or 1))
-    n = sample_sets
-    pk = [pks[48 * j : 48 * j + 48] for j in range(n)]
-    ms = [msgs[32 * j : 32 * j + 32] for j in range(n)]
-    sg = [sigs[96 * j : 96 * j + 96] for j in range(n)]
-    rr = [secrets.randbits(64) | 1 for _ in range(n)]
+    T = cpu_threads()
+    pk = [pks[48 * j : 48 * j + 48] for j in range(sample_sets)]
+    ms = [msgs[32 * j : 32 * j + 32] for j in range(sample_sets)]
+    sg = [sigs[96 * j : 96 * j + 96] for j in range(sample_sets)]
+    rr = synth.random_multipliers(sample_sets)
     t0 = time.perf_counter()
-    ok = C.batch_verify(pk, ms, sg, rr, threads=threads)
+    assert C.batch_verify(pk, ms, sg, rr, threads=T), "C oracle rejected the valid sample"
     dt = time.perf_counter() - t0
-    assert ok, "C oracle rejected the valid sample"
+    t0 = time.perf_counter()
+    assert C.batch_verify(pk[:sample_1t], ms[:sample_1t], sg[:sample_1t], rr[:sample_1t], threads=1)
+    dt1 = time.perf_counter() - t0
+    lat = timed(lambda: C.batch_verify(pk[:128], ms[:128], sg[:128], rr[:128], threads=T), 7)
     return {
-        "value": n / dt,
+        "value": sample_sets / dt,
         "unit": "sigs/s",
-        "cores": threads,
+        "cores": T,
         "kind": "port",
-        "sample": f"oracle/c batch_verify of the first {n} sets of this workload, {threads} pthreads, {dt:.1f} s; "
-        "build's own C restatement (6x64-bit CIOS Montgomery), not blst",
+        "sample": f"oracle/c batch_verify of the first {sample_sets} sets of this workload on {T} pthreads ({dt:.1f} s) and of the first "
+        f"{sample_1t} on 1 thread ({dt1:.1f} s); the build's own C restatement (6x64-bit CIOS Montgomery), not blst",
+        "value_1thread": sample_1t / dt1,
+        "cpu_model": cpu_model(),
+        "machine_cpus": os.cpu_count(),
+        "p50_latency_ms_128": statistics.median(lat),
     }
+
+
+def extra_configs(device, stream, reps):
+    """Configs 2, 3, 4 (BASELINE.json) on this rank's GPU; see the module doc."""
+    out = {}
+    peak = peak_mac_per_s(device)
+    # config 2: 64 sync-committee sets x 512 keys, fastAggregateVerify per set
+    keys, msgs, sigs = synth.multi_key(64, 512, first_key=0, seed=2)
+    arr = synth.SetArray.from_lists(keys, msgs, sigs)
+    assert arr.fast_aggregate_verify_many() == [True] * 64
+    lat = timed(arr.fast_aggregate_verify_many, reps)
+    out["cfg2"] = {
+        "what": "64 sets x 512 keys, fastAggregateVerify per set (tbls_fast_aggregate_verify_many, keys as bytes, PCIe included)",
+        "p50_ms": statistics.median(lat),
+        "p99_ms": pct(lat, 0.99),
+        "sets_per_s": 64 / (statistics.median(lat) * 1e-3),
+        "reps": reps,
+    }
+    # config 3: 64 attestation sets x 488 keys, randomized batchVerify
+    keys, msgs, sigs = synth.multi_key(64, 488, first_key=1000, seed=3)
+    arr = synth.SetArray.from_lists(keys, msgs, sigs)
+    assert arr.batch_verify(synth.random_multipliers(64))
+    lat = timed(lambda: arr.batch_verify(synth.random_multipliers(64)), reps)
+    L = native.lib()
+    flat = [k for ks in keys for k in ks]
+    native.check(L.tbls_pk_table_load(b"".join(flat), len(flat), None), "pk_table_load")
+    idx_arrays, keep = (native.TblsSetIdx * 64)(), []
+    for s in range(64):
+        ki = (ctypes.c_uint32 * 488)(*range(488 * s, 488 * (s + 1)))
+        mb, sb = ctypes.create_string_buffer(msgs[s], 32), ctypes.create_string_buffer(sigs[s], 96)
+        keep += [ki, mb, sb]
+        idx_arrays[s].key_idx = ctypes.cast(ki, ctypes.c_void_p)
+        idx_arrays[s].n_pks = 488
+        idx_arrays[s].msg = ctypes.cast(mb, ctypes.c_void_p)
+        idx_arrays[s].msg_len = 32
+        idx_arrays[s].sig = ctypes.cast(sb, ctypes.c_void_p)
+
+    def idx_verify():
+        rr = (ctypes.c_uint64 * 64)(*synth.random_multipliers(64))
+        ok = ctypes.c_int(0)
+        native.check(L.tbls_batch_verify_idx(idx_arrays, 64, rr, 1, ctypes.byref(ok), None), "batch_verify_idx")
+        assert ok.value == 1
+
+    idx_verify()
+    lat_tab = timed(idx_verify, reps)
+    # the aggregation kernel alone (exclusive stage time on a device-resident batch)
+    db = DevBatch(b"".join(flat), [488] * 64, b"".join(msgs), [32] * 64, b"".join(sigs), device)
+    part = torch.empty(native.PARTIAL_BYTES, dtype=torch.uint8, device=device)
+    st = (ctypes.c_float * 8)()
+    agg_ms = []
+    for _ in range(5):
+        native.check(L.tbls_dev_batch_stage_profile(device.index, ctypes.byref(db.desc), stream, part.data_ptr(), st), "profile")
+        agg_ms.append(st[1])
+    agg_ms = statistics.median(agg_ms)
+    agg_m = M_PER_UNIT.get("set_pk_wave_488")
+    out["cfg3"] = {
+        "what": "64 sets x 488 keys, randomized batchVerify (tbls_batch_verify, keys as bytes, PCIe included)",
+        "p50_ms": statistics.median(lat),
+        "p99_ms": pct(lat, 0.99),
+        "sets_per_s": 64 / (statistics.median(lat) * 1e-3),
+        "p50_ms_key_table": statistics.median(lat_tab),
+        "sets_per_s_key_table": 64 / (statistics.median(lat_tab) * 1e-3),
+        "aggregation_kernel": "k_set_pk_wave (one 64-lane wave per set: strided mixed adds, LDS tree, [r] apk)",
+        "aggregation_ms": agg_ms,
+        "aggregation_frac": (agg_m * MAC_PER_M * 64 / (agg_ms * 1e-3)) / peak if agg_m and agg_ms > 0 else None,
+        "aggregation_fp_products_per_set": agg_m,
+        "reps": reps,
+    }
+    # config 4: 16,384 gossip attestations per slot, one service batch (host C ABI)
+    n4 = 16384
+    pks, msgs, sigs = synth.single_signer(0, n4, seed=4)
+    arr = synth.SetArray.single(pks, msgs, sigs)
+    assert arr.batch_verify(synth.random_multipliers(n4))
+    lat4 = timed(lambda: arr.batch_verify(synth.random_multipliers(n4)), max(5, reps // 4))
+    from teku_amd.service import AggregatingSignatureVerificationService, SignatureTask
+
+    sg = [sigs[96 * i : 96 * i + 96] for i in range(n4)]
+    for j, b in {11: sg[12], 5000: bytes(96), 9999: synth.NOT_IN_G2, 16383: sg[0]}.items():
+        sg[j] = b
+    sets = [(pks[48 * i : 48 * i + 48], 1, msgs[32 * i : 32 * i + 32], sg[i]) for i in range(n4)]
+    settle = []
+    for _ in range(3):
+        svc = AggregatingSignatureVerificationService(max_batch_size=n4)
+        tasks = [SignatureTask([s]) for s in sets]
+        t0 = time.perf_counter()
+        svc.batch_verify_signatures(tasks)
+        settle.append((time.perf_counter() - t0) * 1e3)
+        assert sum(1 for t in tasks if not t.result.result()) == 4
+    out["cfg4"] = {
+        "what": "16,384 single-signer sets in one service batch (tbls_batch_verify, PCIe included); failure path: 4 bad sets settled "
+        "by one batch + one per-set pass (tbls_verify_each)",
+        "p50_ms": statistics.median(lat4),
+        "sigs_per_s": n4 / (statistics.median(lat4) * 1e-3),
+        "failure_settle_ms": statistics.median(settle),
+        "failure_device_passes": svc.device_passes,
+    }
+    return out
 
 
 def main():
@@ -172,8 +302,11 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--sets-per-gpu", type=int, default=int(os.environ.get("TBLS_SETS_PER_GPU", 131072)))
-    ap.add_argument("--lat-reps", type=int, default=30)
+    ap.add_argument("--lat-reps", type=int, default=100)
+    ap.add_argument("--extra-reps", type=int, default=20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extra", action="store_true", help="skip configs 2/3/4")
+    ap.add_argument("--serial", action="store_true", help="timed steps with every stage alone on the stream (profiling)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -188,8 +321,8 @@ def main():
     S = args.sets_per_gpu
     t_gen = time.perf_counter()
     lo, hi = shard_bounds(S * world, world, rank)  # weak scaling: S sets per rank
-    pks, msgs, sigs = make_workload(L, lo, hi - lo)
-    batch = DevBatch(pks, msgs, sigs, S, device)
+    pks, msgs, sigs = synth.single_signer(lo, hi - lo)
+    batch = DevBatch(pks, [1] * S, msgs, [32] * S, sigs, device)
     gen_s = time.perf_counter() - t_gen
     partial = torch.empty(native.PARTIAL_BYTES, dtype=torch.uint8, device=device)
     stream = torch.cuda.current_stream(device).cuda_stream
@@ -198,12 +331,15 @@ def main():
     stage = (ctypes.c_float * 8)()
 
     def step(timed_stages):
-        if timed_stages:
+        if args.serial:
+            native.check(L.tbls_dev_batch_stage_profile(local, ctypes.byref(batch.desc), stream, partial.data_ptr(), stage), "profile")
+        elif timed_stages:
             native.check(L.tbls_dev_batch_partial_timed(local, ctypes.byref(batch.desc), stream, partial.data_ptr(), stage), "partial")
-            for i in range(len(STAGES)):
-                stage_acc[i] += stage[i]
         else:
             native.check(L.tbls_dev_batch_partial(local, ctypes.byref(batch.desc), stream, partial.data_ptr()), "partial")
+        if timed_stages or args.serial:
+            for i in range(len(STAGES)):
+                stage_acc[i] += stage[i]
         src = all_gather_partials(partial)
         if rank == 0:
             native.check(L.tbls_dev_final_verify(local, src.data_ptr(), world, stream, ctypes.byref(ok)), "final")
@@ -275,24 +411,19 @@ def main():
         native.check(L.tbls_dev_batch_stage_profile(local, ctypes.byref(batch.desc), stream, partial.data_ptr(), stage), "profile")
         for i in range(len(STAGES)):
             excl[i] += stage[i] / 2
-    roofline = roofline_entry(excl, S, device)
+    ms_per_step = dt / args.steps * 1e3
+    roofline = roofline_entry(excl, S, device, ms_per_step)
 
-    # p50 latency of a 128-set batchVerify through the host C ABI (config 1 shape)
-    from teku_amd import bls
-
+    # config 1: latency of a 128-set batchVerify through the host C ABI
+    arr128 = synth.SetArray.single(pks[: 48 * 128], msgs[: 32 * 128], sigs[: 96 * 128])
     lat = []
-    if args.lat_reps <= 0:
-        lat = [float("nan")]
-    sets128 = [(pks[48 * j : 48 * j + 48], 1, msgs[32 * j : 32 * j + 32], sigs[96 * j : 96 * j + 96]) for j in range(128)]
-    for _ in range(args.lat_reps + 3 if args.lat_reps > 0 else 0):
-        rr = [secrets.randbits(64) | 1 for _ in range(128)]
-        t1 = time.perf_counter()
-        good = bls.batch_verify_raw(sets128, rr, n_gpus=1)
-        lat.append((time.perf_counter() - t1) * 1e3)
-        assert good
-    lat = sorted(lat[3:]) if args.lat_reps > 0 else lat
+    if args.lat_reps > 0:
+        for _ in range(3):
+            assert arr128.batch_verify(synth.random_multipliers(128), n_gpus=1)
+        lat = timed(lambda: arr128.batch_verify(synth.random_multipliers(128), n_gpus=1), args.lat_reps)
+    extra = {} if args.no_extra else extra_configs(device, stream, args.extra_reps)
 
-    cpu = None if args.no_cpu_baseline else cpu_baseline_oracle(pks, msgs, sigs, min(4096, S))
+    cpu = None if args.no_cpu_baseline else cpu_baseline_oracle(pks, msgs, sigs, min(4096, S), min(512, S))
     line = {
         "metric": "BLS sigs verified/sec (batchVerify), 1-8 GPUs; p50 latency @128-sig batch",
         "value": value,
@@ -300,7 +431,7 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": dt / args.steps * 1e3,
+        "ms_per_step": ms_per_step,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -311,15 +442,18 @@ def main():
             "sets_per_gpu": S,
             "parallelism": "data-parallel shards, dp%d" % world,
         },
+        "serial_stages": bool(args.serial),
         "value_key_table": total_sets / dt_tab,
         "ms_per_step_key_table": dt_tab / args.steps * 1e3,
         "key_table": "value_key_table: same steps with keys from the device-resident validator table (%d keys decompressed "
         "and validated once, as Teku memoizes BLSPublicKey); value decodes and group-checks every key per step" % T,
-        "p50_latency_ms_128": statistics.median(lat),
-        "p99_latency_ms_128": lat[min(len(lat) - 1, int(0.99 * len(lat)))],
+        "p50_latency_ms_128": statistics.median(lat) if lat else None,
+        "p99_latency_ms_128": pct(lat, 0.99) if lat else None,
+        "latency_reps_128": len(lat),
         "stage_ms_overlapped": dict(zip(STAGES, stage_ms)),
         "stage_ms_exclusive": dict(zip(STAGES, excl)),
         "roofline": roofline,
+        "configs": extra,
         "cpu_baseline": cpu,
         "workload_gen_s": gen_s,
     }

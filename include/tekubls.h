@@ -217,9 +217,6 @@ int tbls_sk_to_pk_many(const uint8_t* sks, size_t n, uint8_t* out /* n*48 */);
 int tbls_sign_many(const uint8_t* sks, const uint8_t* msgs, const uint32_t* msg_off /* n+1 */, size_t n, const uint8_t* dst,
                    size_t dlen, uint8_t* out /* n*96 */);
 
-/* ---- test hook: primitive ops (tb_testops.h records), run on the GPU ---- */
-int tbls_test_ops(int op, const uint8_t* in, uint8_t* out, size_t n);
-
 #ifdef __cplusplus
 }
 #endif

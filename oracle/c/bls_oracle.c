@@ -895,44 +895,73 @@ int orc_sig_validate(const uint8_t sig[96], int* is_inf) {
   return g2_in_group(g2_aff(x, y)) ? OK : NOT_IN_GROUP;
 }
 
+/* One signature set as BlstBLS12381.prepareBatchVerify sees it
+ * (BlstBLS12381.java:112-143): the keys aggregated by BlstPublicKey.aggregate
+ * (BlstPublicKey.java:55-71: every key decodes, is finite and in G1, else the
+ * set is invalid; an infinite sum is BLST_PK_IS_INFINITY) and the signature
+ * decoded and group-checked (infinity allowed, *sinf).  1 = valid set. */
+static int set_prepare(const uint8_t* pks, uint32_t npk, const uint8_t* sig, fe* ax, fe* ay, fe2* sx, fe2* sy, int* sinf) {
+  if (npk == 0) return 0;
+  g1j acc = g1_inf();
+  for (uint32_t k = 0; k < npk; k++) {
+    fe x, y;
+    int inf;
+    if (g1_decompress(&x, &y, &inf, pks + 48 * (size_t)k) || inf || !g1_in_group(g1_aff(x, y))) return 0;
+    acc = g1_add(acc, g1_aff(x, y));
+  }
+  if (!g1_to_aff(ax, ay, acc)) return 0;
+  if (g2_decompress(sx, sy, sinf, sig)) return 0;
+  if (!*sinf && !g2_in_group(g2_aff(*sx, *sy))) return 0;
+  return 1;
+}
+
 typedef struct {
   const uint8_t *pks, *msgs, *sigs, *dst;
-  const uint32_t* msg_off;
+  const uint32_t *pk_off, *msg_off;
   const uint64_t* rand;
   size_t lo, hi, dlen;
   fe12 f;
   g2j s;
   int ok;
+  uint8_t* each; /* per-set verdicts (verify_each) or NULL (batch) */
 } chunk;
+
+static uint32_t key_lo(const chunk* c, size_t i) { return c->pk_off ? c->pk_off[i] : (uint32_t)i; }
+static uint32_t key_hi(const chunk* c, size_t i) { return c->pk_off ? c->pk_off[i + 1] : (uint32_t)i + 1; }
 
 static void* run_chunk(void* arg) {
   chunk* c = (chunk*)arg;
   c->f = f12_one();
   c->s = g2_inf();
   c->ok = 1;
-  for (size_t i = c->lo; i < c->hi && c->ok; i++) {
-    fe px, py;
-    fe2 sx, sy;
-    int inf;
-    /* prepareBatchVerify: invalid key or signature -> the batch is false */
-    if (g1_decompress(&px, &py, &inf, c->pks + 48 * i) || inf || !g1_in_group(g1_aff(px, py))) {
-      c->ok = 0;
-      break;
-    }
-    if (g2_decompress(&sx, &sy, &inf, c->sigs + 96 * i)) {
-      c->ok = 0;
-      break;
-    }
-    if (!inf) {
-      if (!g2_in_group(g2_aff(sx, sy))) {
-        c->ok = 0;
-        break;
+  for (size_t i = c->lo; i < c->hi && (c->ok || c->each); i++) {
+    fe ax, ay;
+    fe2 sx, sy, hx, hy;
+    int sinf;
+    const uint32_t k0 = key_lo(c, i), k1 = key_hi(c, i);
+    const int valid = set_prepare(c->pks + 48 * (size_t)k0, k1 - k0, c->sigs + 96 * i, &ax, &ay, &sx, &sy, &sinf);
+    if (c->each) {
+      /* fastAggregateVerify (BLS.java:185-207 -> blst core_verify): e(apk, H(m)) e(-g1, sig) == 1 */
+      uint8_t v = 0;
+      if (valid) {
+        fe12 f = f12_one();
+        g2j h = hash_to_g2(c->msgs + c->msg_off[i], c->msg_off[i + 1] - c->msg_off[i], c->dst, c->dlen);
+        if (g2_to_aff(&hx, &hy, h)) f = miller_acc(f, ax, ay, hx, hy);
+        if (!sinf) f = miller_acc(f, G1X, fe_neg(G1Y), sx, sy);
+        v = (uint8_t)final_exp_is_one(f);
       }
-      c->s = g2_add(c->s, g2_mul_u64(g2_aff(sx, sy), c->rand[i]));
+      c->each[i] = v;
+      continue;
     }
+    /* prepareBatchVerify: an invalid set makes the batch false */
+    if (!valid) {
+      c->ok = 0;
+      break;
+    }
+    const u64 r = c->rand[i];
+    if (!sinf) c->s = g2_add(c->s, g2_mul_u64(g2_aff(sx, sy), r));
     fe rx, ry;
-    fe2 hx, hy;
-    if (!g1_to_aff(&rx, &ry, g1_mul_u64(g1_aff(px, py), c->rand[i]))) {
+    if (!g1_to_aff(&rx, &ry, g1_mul_u64(g1_aff(ax, ay), r))) {
       c->ok = 0;
       break;
     }
@@ -942,36 +971,69 @@ static void* run_chunk(void* arg) {
   return NULL;
 }
 
-/* Randomized batch verification of n >= 2 single-key sets (rands in [1, 2^64)).
- * Returns 1 (valid), 0 (invalid). */
-int orc_batch_verify(const uint8_t* pks, const uint8_t* msgs, const uint32_t* msg_off, const uint8_t* sigs, const uint64_t* rand, size_t n,
-                     const uint8_t* dst, size_t dlen, int nthreads) {
-  init();
-  if (n == 0) return 0;
+static void run_chunks(chunk* proto, size_t n, int nthreads, chunk** out) {
   if (nthreads < 1) nthreads = 1;
   if ((size_t)nthreads > n) nthreads = (int)n;
   chunk* cs = (chunk*)calloc(nthreads, sizeof(chunk));
   pthread_t* th = (pthread_t*)calloc(nthreads, sizeof(pthread_t));
   for (int t = 0; t < nthreads; t++) {
-    cs[t] = (chunk){pks, msgs, sigs, dst, msg_off, rand, n * t / nthreads, n * (t + 1) / nthreads, dlen};
+    cs[t] = *proto;
+    cs[t].lo = n * t / nthreads;
+    cs[t].hi = n * (t + 1) / nthreads;
     if (nthreads > 1)
       pthread_create(&th[t], NULL, run_chunk, &cs[t]);
     else
       run_chunk(&cs[t]);
   }
+  if (nthreads > 1)
+    for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+  free(th);
+  *out = cs;
+  proto->lo = (size_t)nthreads; /* chunk count */
+}
+
+/* Randomized batch verification (BLS.batchVerify -> prepareBatchVerify /
+ * completeBatchVerify, BLS.java:275-336, BlstBLS12381.java:112-189) of n >= 2
+ * sets; set i has keys pks[pk_off[i] .. pk_off[i+1]) (48 B each; pk_off NULL:
+ * one key per set), rands in [1, 2^64).  Returns 1 (valid), 0 (invalid). */
+int orc_batch_verify_sets(const uint8_t* pks, const uint32_t* pk_off, const uint8_t* msgs, const uint32_t* msg_off, const uint8_t* sigs,
+                          const uint64_t* rand, size_t n, const uint8_t* dst, size_t dlen, int nthreads) {
+  init();
+  if (n == 0) return 0;
+  chunk proto = {pks, msgs, sigs, dst, pk_off, msg_off, rand, 0, 0, dlen};
+  chunk* cs;
+  run_chunks(&proto, n, nthreads, &cs);
+  const int nt = (int)proto.lo;
   fe12 f = f12_one();
   g2j s = g2_inf();
   int ok = 1;
-  for (int t = 0; t < nthreads; t++) {
-    if (nthreads > 1) pthread_join(th[t], NULL);
+  for (int t = 0; t < nt; t++) {
     ok &= cs[t].ok;
     f = f12_mul(f, cs[t].f);
     s = g2_add(s, cs[t].s);
   }
   free(cs);
-  free(th);
   if (!ok) return 0;
   fe2 sx, sy;
   if (g2_to_aff(&sx, &sy, s)) f = miller_acc(f, G1X, fe_neg(G1Y), sx, sy);
   return final_exp_is_one(f);
+}
+
+int orc_batch_verify(const uint8_t* pks, const uint8_t* msgs, const uint32_t* msg_off, const uint8_t* sigs, const uint64_t* rand, size_t n,
+                     const uint8_t* dst, size_t dlen, int nthreads) {
+  return orc_batch_verify_sets(pks, NULL, msgs, msg_off, sigs, rand, n, dst, dlen, nthreads);
+}
+
+/* Per-set fastAggregateVerify verdicts (BLS.java:185-207): ok[i] = 1 iff set i
+ * (same layout as orc_batch_verify_sets) verifies on its own; an empty key
+ * list gives 0. */
+void orc_verify_each(const uint8_t* pks, const uint32_t* pk_off, const uint8_t* msgs, const uint32_t* msg_off, const uint8_t* sigs, size_t n,
+                     const uint8_t* dst, size_t dlen, int nthreads, uint8_t* ok) {
+  init();
+  if (n == 0) return;
+  chunk proto = {pks, msgs, sigs, dst, pk_off, msg_off, NULL, 0, 0, dlen};
+  proto.each = ok;
+  chunk* cs;
+  run_chunks(&proto, n, nthreads, &cs);
+  free(cs);
 }

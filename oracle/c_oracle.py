@@ -23,7 +23,11 @@ def lib():
         L.orc_sign.argtypes = [cp, cp, sz, cp, sz, cp]
         L.orc_pk_validate.argtypes = [cp]
         L.orc_sig_validate.argtypes = [cp, ctypes.POINTER(ctypes.c_int)]
-        L.orc_batch_verify.argtypes = [cp, cp, ctypes.POINTER(ctypes.c_uint32), cp, ctypes.POINTER(ctypes.c_uint64), sz, cp, sz, ctypes.c_int]
+        u32p, u64p = ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint64)
+        L.orc_batch_verify.argtypes = [cp, cp, u32p, cp, u64p, sz, cp, sz, ctypes.c_int]
+        L.orc_batch_verify_sets.argtypes = [cp, u32p, cp, u32p, cp, u64p, sz, cp, sz, ctypes.c_int]
+        L.orc_verify_each.argtypes = [cp, u32p, cp, u32p, cp, sz, cp, sz, ctypes.c_int, ctypes.c_void_p]
+        L.orc_verify_each.restype = None
         _lib = L
     return _lib
 
@@ -67,3 +71,40 @@ def batch_verify(pks, msgs, sigs, rands, threads=1, dst=ETH2_DST):
     off[n] = acc
     rr = (ctypes.c_uint64 * n)(*rands)
     return lib().orc_batch_verify(b"".join(pks), b"".join(msgs) or b"\0", off, b"".join(sigs), rr, n, dst, len(dst), threads) == 1
+
+
+def _offsets(items, size_of):
+    off = (ctypes.c_uint32 * (len(items) + 1))()
+    acc = 0
+    for i, x in enumerate(items):
+        off[i] = acc
+        acc += size_of(x)
+    off[len(items)] = acc
+    return off
+
+
+def batch_verify_sets(pks_list, msgs, sigs, rands, threads=1, dst=ETH2_DST):
+    """Randomized batch verification of n >= 2 sets, set i signed by the keys
+    pks_list[i] (a list of 48-byte keys: BlstPublicKey.aggregate semantics)."""
+    n = len(pks_list)
+    pk_off = _offsets(pks_list, len)
+    m_off = _offsets(msgs, len)
+    rr = (ctypes.c_uint64 * n)(*rands)
+    blob = b"".join(b"".join(p) for p in pks_list)
+    return (
+        lib().orc_batch_verify_sets(blob or b"\0", pk_off, b"".join(msgs) or b"\0", m_off, b"".join(sigs), rr, n, dst, len(dst), threads)
+        == 1
+    )
+
+
+def verify_each(pks_list, msgs, sigs, threads=1, dst=ETH2_DST):
+    """Per-set fastAggregateVerify verdicts (BLS.java:185-207) as a list of bools."""
+    n = len(pks_list)
+    if n == 0:
+        return []
+    pk_off = _offsets(pks_list, len)
+    m_off = _offsets(msgs, len)
+    out = (ctypes.c_uint8 * n)()
+    blob = b"".join(b"".join(p) for p in pks_list)
+    lib().orc_verify_each(blob or b"\0", pk_off, b"".join(msgs) or b"\0", m_off, b"".join(sigs), n, dst, len(dst), threads, out)
+    return [bool(v) for v in out]

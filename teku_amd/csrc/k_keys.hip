@@ -18,19 +18,83 @@ extern "C" __global__ void __launch_bounds__(TB_BLOCK)
 }
 
 // per set: aggregate keys (BlstPublicKey.aggregate semantics), P = [r] apk (affine);
-// key_idx (nullable): keys come from the device-resident table (pk_aff/pk_code = the table)
+// key_idx (nullable): keys come from the device-resident table (pk_aff/pk_code =
+// the table, tab_n entries).  multi_wave: sets with more than one key are left
+// to k_set_pk_wave (one 64-lane wave per set) and skipped here.
 extern "C" __global__ void __launch_bounds__(TB_BLOCK)
     k_set_pk(const uint32_t* __restrict__ pk_off, const g1a* __restrict__ pk_aff, const uint8_t* __restrict__ pk_code,
              const uint64_t* __restrict__ rand, uint32_t n, g1a* __restrict__ P, uint8_t* __restrict__ set_code,
-             uint32_t* __restrict__ n_bad, const uint32_t* __restrict__ key_idx) {
+             uint32_t* __restrict__ n_bad, const uint32_t* __restrict__ key_idx, uint32_t tab_n, uint32_t multi_wave) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
+  const uint32_t b = pk_off[i], e = pk_off[i + 1];
+  if (multi_wave && e - b > 1) return;
   g1a out;
-  int code = stage_set_pk(pk_aff, pk_code, pk_off[i], pk_off[i + 1], rand[i], out, key_idx);
+  int code = stage_set_pk(pk_aff, pk_code, b, e, rand[i], out, key_idx, tab_n);
   P[i] = out;
   if (code != TB_SUCCESS) {
     set_code[i] = (uint8_t)code;
     atomicAdd(n_bad, 1u);
+  }
+}
+
+// Compaction of the multi-key sets (pk_off[i+1] - pk_off[i] > 1) into list[],
+// count in cnt[0] (zeroed by the host): the work list of k_set_pk_wave.
+extern "C" __global__ void __launch_bounds__(TB_BLOCK)
+    k_multi_list(const uint32_t* __restrict__ pk_off, uint32_t n, uint32_t* __restrict__ list, uint32_t* __restrict__ cnt) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  if (pk_off[i + 1] - pk_off[i] > 1) list[atomicAdd(cnt, 1u)] = i;
+}
+
+// Wave-level G1 public-key aggregation (BlstPublicKey.aggregate,
+// BlstPublicKey.java:55-71) for multi-key sets (configs 2/3: 488-512 keys per
+// set): one 64-lane workgroup per set.  Lane l sums keys l, l+64, ... with
+// mixed additions, the 64 partial sums meet in a 6-level LDS tree, and lane 0
+// forms P = [r] apk.  Any invalid key (or an index past the table) makes the
+// set invalid, as the one-thread stage_set_pk.  Workgroups stride over the
+// compacted list (its length is only known on the device).
+extern "C" __global__ void __launch_bounds__(64)
+    k_set_pk_wave(const uint32_t* __restrict__ pk_off, const g1a* __restrict__ pk_aff, const uint8_t* __restrict__ pk_code,
+                  const uint64_t* __restrict__ rand, const uint32_t* __restrict__ list, const uint32_t* __restrict__ cnt,
+                  g1a* __restrict__ P, uint8_t* __restrict__ set_code, uint32_t* __restrict__ n_bad,
+                  const uint32_t* __restrict__ key_idx, uint32_t tab_n) {
+  __shared__ g1j sh[64];
+  __shared__ int bad;
+  const uint32_t t = threadIdx.x, total = cnt[0];
+  for (uint32_t w = blockIdx.x; w < total; w += gridDim.x) {
+    const uint32_t i = list[w], b = pk_off[i], e = pk_off[i + 1];
+    if (t == 0) bad = TB_SUCCESS;
+    __syncthreads();
+    g1j acc = jac_inf<fp>();
+    for (uint32_t j = b + t; j < e; j += 64) {
+      uint32_t k;
+      if (!set_key(key_idx, tab_n, j, k))
+        bad = TB_BAD_ENCODING;
+      else if (pk_code[k] != TB_SUCCESS)
+        bad = TB_PK_IS_INFINITY;  // BlstPublicKey.java:58-65 (any racing writer stores a failure)
+      else
+        acc = jac_add_aff(acc, pk_aff[k]);
+    }
+    sh[t] = acc;
+    __syncthreads();
+    for (uint32_t s = 32; s > 0; s >>= 1) {
+      if (t < s) sh[t] = jac_add(sh[t], sh[t + s]);
+      __syncthreads();
+    }
+    if (t == 0) {
+      g1a out;
+      int code = bad;
+      if (code == TB_SUCCESS) code = stage_set_pk_finish(sh[0], rand[i], out);
+      if (code != TB_SUCCESS) {
+        out.x = fp_zero();
+        out.y = fp_zero();
+        set_code[i] = (uint8_t)code;
+        atomicAdd(n_bad, 1u);
+      }
+      P[i] = out;
+    }
+    __syncthreads();
   }
 }
 

@@ -21,7 +21,6 @@
 // in LDS, then one block over the block partials).
 #pragma once
 #include "tb_stages.h"
-#include "tb_testops.h"
 #include "tb_fp12_wave.h"
 
 using namespace tb;
@@ -50,7 +49,9 @@ __device__ TB_INLINE jac<F> jac_mul_u256(const jac<F>& P, const uint64_t* k) {
 // Kernel declarations (definitions in k_keys / k_sigs / k_hash / k_pair / k_test .hip),
 // for the host code in tb_lib.hip.
 extern "C" __global__ void k_pk_decompress(const uint8_t* __restrict__ pks, uint32_t K, g1a* __restrict__ pk_aff, uint8_t* __restrict__ pk_code);
-extern "C" __global__ void k_set_pk(const uint32_t* __restrict__ pk_off, const g1a* __restrict__ pk_aff, const uint8_t* __restrict__ pk_code, const uint64_t* __restrict__ rand, uint32_t n, g1a* __restrict__ P, uint8_t* __restrict__ set_code, uint32_t* __restrict__ n_bad, const uint32_t* __restrict__ key_idx);
+extern "C" __global__ void k_set_pk(const uint32_t* __restrict__ pk_off, const g1a* __restrict__ pk_aff, const uint8_t* __restrict__ pk_code, const uint64_t* __restrict__ rand, uint32_t n, g1a* __restrict__ P, uint8_t* __restrict__ set_code, uint32_t* __restrict__ n_bad, const uint32_t* __restrict__ key_idx, uint32_t tab_n, uint32_t multi_wave);
+extern "C" __global__ void k_multi_list(const uint32_t* __restrict__ pk_off, uint32_t n, uint32_t* __restrict__ list, uint32_t* __restrict__ cnt);
+extern "C" __global__ void k_set_pk_wave(const uint32_t* __restrict__ pk_off, const g1a* __restrict__ pk_aff, const uint8_t* __restrict__ pk_code, const uint64_t* __restrict__ rand, const uint32_t* __restrict__ list, const uint32_t* __restrict__ cnt, g1a* __restrict__ P, uint8_t* __restrict__ set_code, uint32_t* __restrict__ n_bad, const uint32_t* __restrict__ key_idx, uint32_t tab_n);
 extern "C" __global__ void k_aggregate_pks(const g1a* __restrict__ pk_aff, const uint8_t* __restrict__ pk_code, uint32_t K, uint8_t* __restrict__ out);
 extern "C" __global__ void k_sk_to_pk(const uint64_t* __restrict__ sks, uint32_t n, uint8_t* __restrict__ out);
 extern "C" __global__ void k_set_sig(const uint8_t* __restrict__ sigs, const uint64_t* __restrict__ rand, uint32_t n, g2j* __restrict__ rsig, uint8_t* __restrict__ sig_code, uint32_t* __restrict__ n_bad);
@@ -78,6 +79,3 @@ extern "C" __global__ void k_miller_one_wave(const g1a* __restrict__ P, const g2
 extern "C" __global__ void k_fp12_prod_wave(const fp12* __restrict__ in, uint32_t n, uint32_t chunk, fp12* __restrict__ out);
 extern "C" __global__ void k_final_verify_wave(const fp12* __restrict__ f, uint32_t g, const uint32_t* __restrict__ n_bad, int* __restrict__ result);
 extern "C" __global__ void k_final_verify(const fp12* __restrict__ f, const uint32_t* __restrict__ n_bad, int* __restrict__ result);
-extern "C" __global__ void k_test_ops(int op, const uint8_t* in, uint8_t* out, uint32_t n);
-extern "C" __global__ void k_test_final_exp_wave(const uint8_t* in, uint8_t* out);
-extern "C" __global__ void k_test_miller_wave(const uint8_t* in, uint8_t* out);

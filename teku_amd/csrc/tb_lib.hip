@@ -11,7 +11,7 @@
 #include <cstring>
 #include <mutex>
 #include <algorithm>
-#include <random>
+#include <sys/random.h>
 #include <thread>
 #include <type_traits>
 #include <vector>
@@ -81,8 +81,19 @@ struct dev_ctx {
   dbuf tab_aff, tab_code;                    // device-resident public-key table (tbls_pk_table_load)
   uint32_t tab_n = 0;
   hipEvent_t e_fork = nullptr, e_join[2] = {nullptr, nullptr}, e_sig = nullptr;
+  hipEvent_t e_t0 = nullptr, e_t1 = nullptr;  // per-call device timing (run_shard), created once
+  // Last use of `ws` on any stream.  The device-resident API queues work on the
+  // caller's stream and returns; every later user of `ws` (on whatever stream)
+  // first waits for this event, then records it after its own work.
+  hipEvent_t e_ws = nullptr;
+  dbuf recs;  // partial records gathered for the final exponentiation (final_on_device0)
   hbuf hin, hout;
 };
+
+// Order a new user of c.ws (on stream s) after the previous one; call
+// ws_release after queueing the new work.
+inline hipError_t ws_acquire(dev_ctx& c, hipStream_t s) { return hipStreamWaitEvent(s, c.e_ws, 0); }
+inline hipError_t ws_release(dev_ctx& c, hipStream_t s) { return hipEventRecord(c.e_ws, s); }
 
 std::mutex g_mu;
 std::vector<dev_ctx*> g_ctx;
@@ -103,7 +114,7 @@ size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
 #define TB_MSM_WSEGS 512u      // 8 windows x 64 digit segments
 struct ws_layout {
   size_t pk_aff, pk_code, P, Q, skip, set_code, sig_code, rsig, f, gpart, fpart, fpart2, n_bad, result;
-  size_t sig_aff, sig_use, msm_cnt, msm_off, msm_cur, msm_idx, msm_part, msm_bucket, msm_wseg, msm_wsum, total;
+  size_t sig_aff, sig_use, msm_cnt, msm_off, msm_cur, msm_idx, msm_part, msm_bucket, msm_wseg, msm_wsum, mlist, mcnt, total;
   uint32_t nb_g2, nb_f;
   bool msm;
   ws_layout(uint32_t n, uint32_t K) {
@@ -133,6 +144,8 @@ struct ws_layout {
     msm_bucket = o; o = align_up(o + (msm ? (size_t)TB_MSM_BUCKETS * sizeof(g2j) : 0));
     msm_wseg = o; o = align_up(o + (msm ? TB_MSM_WSEGS * sizeof(g2j) : 0));
     msm_wsum = o; o = align_up(o + (msm ? 8 * sizeof(g2j) : 0));
+    mlist = o;    o = align_up(o + (size_t)n * 4);
+    mcnt = o;     o = align_up(o + 4);
     f = o;        o = align_up(o + (size_t)np * sizeof(fp12));
     gpart = o;    o = align_up(o + (size_t)nb_g2 * sizeof(g2j));
     fpart = o;    o = align_up(o + (size_t)nb_f * sizeof(fp12));
@@ -170,6 +183,24 @@ static uint32_t miller_wave_max() {
   static const uint32_t v = getenv("TBLS_MILLER_WAVE_MAX") ? (uint32_t)atoi(getenv("TBLS_MILLER_WAVE_MAX")) : 1024u;
   return v;
 }
+// Per-set aggregate key and P_i = [r_i] apk_i on stream s.  Single-key sets:
+// one thread per set (k_set_pk).  When some set has several keys (n_entries >
+// n: configs 2/3), those sets go to the wave-level aggregation k_set_pk_wave
+// through a device-built work list (mlist / mcnt: n + 1 words of workspace).
+void launch_set_pk(hipStream_t s, uint32_t n, uint32_t n_entries, const uint32_t* pk_off, const g1a* aff, const uint8_t* code,
+                   const uint64_t* rand, g1a* P, uint8_t* set_code, uint32_t* n_bad, const uint32_t* key_idx, uint32_t tab_n,
+                   uint32_t* mlist, uint32_t* mcnt) {
+  if (!n) return;
+  const dim3 blk(TB_BLOCK), g((n + TB_BLOCK - 1) / TB_BLOCK);
+  const uint32_t multi = n_entries > n ? 1u : 0u;
+  hipLaunchKernelGGL(k_set_pk, g, blk, 0, s, pk_off, aff, code, rand, n, P, set_code, n_bad, key_idx, tab_n, multi);
+  if (!multi) return;
+  (void)hipMemsetAsync(mcnt, 0, 4, s);
+  hipLaunchKernelGGL(k_multi_list, g, blk, 0, s, pk_off, n, mlist, mcnt);
+  hipLaunchKernelGGL(k_set_pk_wave, dim3(std::min<uint32_t>(n, 4096u)), dim3(64), 0, s, pk_off, aff, code, rand,
+                     (const uint32_t*)mlist, (const uint32_t*)mcnt, P, set_code, n_bad, key_idx, tab_n);
+}
+
 int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* partial_out, ws_layout& L,
                    const uint8_t* dst, uint32_t dlen, bool keep_codes, hipEvent_t* ev = nullptr, bool serial_req = false,
                    const uint32_t* key_idx = nullptr) {
@@ -177,7 +208,11 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
   const bool use_tab = key_idx != nullptr;  // keys = indices into the resident table: no decompression
   const uint32_t K = use_tab ? 0 : b.n_keys;
   L = ws_layout(n, K);
-  if (c.ws.ensure(L.total)) return TBLS_DEVICE_ERROR;
+  HIPCHK(ws_acquire(c, s));
+  if (L.total > c.ws.cap) {  // growing frees the old buffer: drain its users first
+    HIPCHK(hipStreamSynchronize(s));
+    if (c.ws.ensure(L.total)) return TBLS_DEVICE_ERROR;
+  }
   uint8_t* w = c.ws.as<uint8_t>();
   (void)keep_codes;
   static const bool serial_env = getenv("TBLS_SERIAL") && getenv("TBLS_SERIAL")[0] == '1';
@@ -254,10 +289,9 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
   if (K) hipLaunchKernelGGL(k_pk_decompress, dim3((K + TB_BLOCK - 1) / TB_BLOCK), blk, 0, sk, b.pks, K, (g1a*)(w + L.pk_aff), w + L.pk_code);
   TB_EV(1, sk);
   TB_EV(2, sk);
-  if (n)
-    hipLaunchKernelGGL(k_set_pk, g, blk, 0, sk, b.pk_off, use_tab ? c.tab_aff.as<const g1a>() : (const g1a*)(w + L.pk_aff),
-                       use_tab ? c.tab_code.as<const uint8_t>() : (const uint8_t*)(w + L.pk_code), b.rand, n, (g1a*)(w + L.P),
-                       w + L.set_code, (uint32_t*)(w + L.n_bad), key_idx);
+  launch_set_pk(sk, n, b.n_keys, b.pk_off, use_tab ? c.tab_aff.as<const g1a>() : (const g1a*)(w + L.pk_aff),
+                use_tab ? c.tab_code.as<const uint8_t>() : (const uint8_t*)(w + L.pk_code), b.rand, (g1a*)(w + L.P), w + L.set_code,
+                (uint32_t*)(w + L.n_bad), key_idx, use_tab ? c.tab_n : 0u, (uint32_t*)(w + L.mlist), (uint32_t*)(w + L.mcnt));
   TB_EV(3, sk);
   HIPCHK(hipEventRecord(c.e_join[0], sig_first ? sa : sh));
   HIPCHK(hipStreamWaitEvent(s, c.e_join[0], 0));
@@ -297,6 +331,7 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
   TB_EV(13, s);
   HIPCHK(hipMemcpyAsync((uint8_t*)partial_out + sizeof(fp12), w + L.n_bad, 4, hipMemcpyDeviceToDevice, s));
   HIPCHK(hipGetLastError());
+  HIPCHK(ws_release(c, s));
   return TBLS_SUCCESS;
 }
 
@@ -352,6 +387,8 @@ struct packed {
 // keys of a set: 48-byte encodings (tbls_set) or 4-byte table indices (tbls_set_idx)
 inline const void* set_keys(const tbls_set& s) { return s.pks; }
 inline const void* set_keys(const tbls_set_idx& s) { return s.key_idx; }
+inline uint32_t idx_of(const tbls_set& s, uint32_t k) { return (void)s, k; }
+inline uint32_t idx_of(const tbls_set_idx& s, uint32_t k) { return s.key_idx[k]; }
 template <class SET>
 constexpr size_t key_bytes() { return std::is_same<SET, tbls_set>::value ? 48 : 4; }
 
@@ -412,14 +449,18 @@ int run_shard(int d, const SET* sets, size_t lo, size_t hi, const uint64_t* rand
   if (!c) return TBLS_DEVICE_ERROR;
   std::lock_guard<std::mutex> lk(c->mu);
   HIPCHK(hipSetDevice(c->dev));
+  if (idx_mode) {  // key indices against this device's table, under its lock (a reload cannot interleave)
+    if (!c->tab_n) return TBLS_BAD_ARGUMENT;
+    for (size_t i = lo; i < hi; i++)
+      for (uint32_t k = 0; k < sets[i].n_pks; k++)
+        if (idx_of(sets[i], k) >= c->tab_n) return TBLS_BAD_ARGUMENT;
+  }
   packed p = pack_layout(sets, lo, hi, dlen);
   const size_t in_total = p.total + TBLS_PARTIAL_BYTES + 256;
   if (c->hin.ensure(in_total) || c->in.ensure(in_total)) return TBLS_DEVICE_ERROR;
   pack_fill(c->hin.b(), p, sets, lo, rand, dst, dlen);
   hipStream_t s = c->stream;
-  hipEvent_t e0, e1;
-  HIPCHK(hipEventCreate(&e0));
-  HIPCHK(hipEventCreate(&e1));
+  hipEvent_t e0 = c->e_t0, e1 = c->e_t1;
   HIPCHK(hipMemcpyAsync(c->in.p, c->hin.p, p.total, hipMemcpyHostToDevice, s));
   uint8_t* di = c->in.as<uint8_t>();
   tbls_dev_batch b;
@@ -434,7 +475,6 @@ int run_shard(int d, const SET* sets, size_t lo, size_t hi, const uint64_t* rand
   uint8_t* dpart = di + align_up(p.total);
   ws_layout L(0, 0);
   HIPCHK(hipEventRecord(e0, s));
-  if (idx_mode && !c->tab_n) return TBLS_BAD_ARGUMENT;  // no key table on this device
   int rc = launch_partial(*c, b, s, dpart, L, di + p.off_dst, dlen, codes_host != nullptr, nullptr, false,
                           idx_mode ? (const uint32_t*)(di + p.off_pks) : nullptr);
   if (rc) return rc;
@@ -449,8 +489,6 @@ int run_shard(int d, const SET* sets, size_t lo, size_t hi, const uint64_t* rand
   HIPCHK(hipStreamSynchronize(s));
   float ms = 0;
   (void)hipEventElapsedTime(&ms, e0, e1);
-  (void)hipEventDestroy(e0);
-  (void)hipEventDestroy(e1);
   if (dev_ms) *dev_ms = ms;
   memcpy(partial_host, c->hout.p, TBLS_PARTIAL_BYTES);
   if (codes_host) {
@@ -467,16 +505,11 @@ int final_on_device0(const uint8_t* recs_host, uint32_t g, int* ok) {
   if (!c) return TBLS_DEVICE_ERROR;
   std::lock_guard<std::mutex> lk(c->mu);
   HIPCHK(hipSetDevice(c->dev));
-  // partial records go to a dedicated region past the final-exp scratch
-  dbuf recs;
-  if (recs.ensure((size_t)g * TBLS_PARTIAL_BYTES)) return TBLS_DEVICE_ERROR;
-  int rc = TBLS_SUCCESS;
-  if (hipMemcpyAsync(recs.p, recs_host, (size_t)g * TBLS_PARTIAL_BYTES, hipMemcpyHostToDevice, c->stream) != hipSuccess)
-    rc = TBLS_DEVICE_ERROR;
-  if (!rc) rc = launch_final(*c, recs.p, g, c->stream, ok);
-  (void)hipStreamSynchronize(c->stream);
-  (void)hipFree(recs.p);
-  return rc;
+  // partial records go to a persistent region (no per-call allocation); the
+  // stream is idle here (every user of c->recs synchronizes before returning)
+  if (c->recs.ensure((size_t)g * TBLS_PARTIAL_BYTES)) return TBLS_DEVICE_ERROR;
+  HIPCHK(hipMemcpyAsync(c->recs.p, recs_host, (size_t)g * TBLS_PARTIAL_BYTES, hipMemcpyHostToDevice, c->stream));
+  return launch_final(*c, c->recs.p, g, c->stream, ok);
 }
 
 // generic single-kernel helpers: upload bytes, run, download
@@ -495,7 +528,12 @@ int with_device0(const std::function<int(dev_ctx&)>& fn) {
   dev_ctx* c = ctx_for(0);
   std::lock_guard<std::mutex> lk(c->mu);
   HIPCHK(hipSetDevice(c->dev));
-  return fn(*c);
+  // ws may still be in use by device-API work queued on a caller's stream
+  HIPCHK(ws_acquire(*c, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  const int rc = fn(*c);
+  (void)ws_release(*c, c->stream);
+  return rc;
 }
 
 int stage_in(dev_ctx& c, const upload& u, uint8_t** d) {
@@ -521,6 +559,24 @@ void sk_to_words(const uint8_t sk[32], uint64_t w[4]) {
 }
 
 // sk < r (BLSSecretKey.fromBytes range, BLSSecretKey.java:30-40)
+// n randomizers in [1, 2^64) from the OS entropy source (one getrandom call
+// per 32 MiB), as BlstBLS12381.nextBatchRandomMultiplier draws from
+// SecureRandom (l.191-195); 0 is redrawn (2^64 itself does not fit a u64).
+int fill_random(uint64_t* r, size_t n) {
+  uint8_t* p = reinterpret_cast<uint8_t*>(r);
+  size_t left = n * 8;
+  while (left) {
+    const ssize_t got = getrandom(p, left < (32u << 20) ? left : (32u << 20), 0);
+    if (got <= 0) return TBLS_DEVICE_ERROR;
+    p += got;
+    left -= (size_t)got;
+  }
+  for (size_t i = 0; i < n; i++)
+    while (r[i] == 0)
+      if (getrandom(&r[i], 8, 0) != 8) return TBLS_DEVICE_ERROR;
+  return TBLS_SUCCESS;
+}
+
 bool sk_in_range(const uint8_t sk[32]) {
   static const uint8_t R_BE[32] = {0x73, 0xed, 0xa7, 0x53, 0x29, 0x9d, 0x7d, 0x48, 0x33, 0x39, 0xd8, 0x08, 0x09, 0xa1, 0xd8, 0x05,
                                    0x53, 0xbd, 0xa4, 0x02, 0xff, 0xfe, 0x5b, 0xfe, 0xff, 0xff, 0xff, 0xff, 0x00, 0x00, 0x00, 0x01};
@@ -551,7 +607,9 @@ extern "C" int tbls_init(int n_devices, uint32_t flags) {
         hipEventCreateWithFlags(&c->e_fork, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->e_join[0], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->e_join[1], hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->e_sig, hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&c->e_sig, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->e_ws, hipEventDisableTiming) != hipSuccess || hipEventCreate(&c->e_t0) != hipSuccess ||
+        hipEventCreate(&c->e_t1) != hipSuccess) {
       delete c;
       break;
     }
@@ -569,6 +627,9 @@ extern "C" void tbls_shutdown(void) {
     if (c->ws.p) (void)hipFree(c->ws.p);
     if (c->fin.p) (void)hipFree(c->fin.p);
     if (c->dstb.p) (void)hipFree(c->dstb.p);
+    if (c->recs.p) (void)hipFree(c->recs.p);
+    if (c->tab_aff.p) (void)hipFree(c->tab_aff.p);
+    if (c->tab_code.p) (void)hipFree(c->tab_code.p);
     if (c->hin.p) (void)hipHostFree(c->hin.p);
     if (c->hout.p) (void)hipHostFree(c->hout.p);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -576,6 +637,8 @@ extern "C" void tbls_shutdown(void) {
       if (c->aux[i]) (void)hipStreamDestroy(c->aux[i]);
     if (c->e_fork) (void)hipEventDestroy(c->e_fork);
     if (c->e_sig) (void)hipEventDestroy(c->e_sig);
+    for (hipEvent_t e : {c->e_ws, c->e_t0, c->e_t1})
+      if (e) (void)hipEventDestroy(e);
     for (int i = 0; i < 2; i++)
       if (c->e_join[i]) (void)hipEventDestroy(c->e_join[i]);
     delete c;
@@ -610,7 +673,7 @@ int batch_verify_impl(const SET* sets, size_t n, const uint64_t* rand, int n_gpu
     int g = 1;
     for (size_t i = 0; i < n && g < G; i++) {
       acc += sets[i].n_pks + 1;
-      if (acc * G >= totalK * (uint64_t)g) cut[g++] = i + 1;
+      while (g < G && acc * G >= totalK * (uint64_t)g) cut[g++] = i + 1;  // as dist.shard_bounds
     }
   }
   std::vector<uint8_t> recs((size_t)G * TBLS_PARTIAL_BYTES);
@@ -657,6 +720,9 @@ extern "C" int tbls_pk_table_load(const uint8_t* pks, size_t K, uint8_t* codes) 
     dev_ctx* c = devs[d];
     std::lock_guard<std::mutex> lk(c->mu);
     HIPCHK(hipSetDevice(c->dev));
+    // device-API partials queued on a caller's stream may still read the old table
+    HIPCHK(ws_acquire(*c, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
     c->tab_n = 0;
     if (c->in.ensure(K * 48) || c->tab_aff.ensure(K * sizeof(g1a)) || c->tab_code.ensure(K)) return TBLS_DEVICE_ERROR;
     HIPCHK(hipMemcpyAsync(c->in.p, pks, K * 48, hipMemcpyHostToDevice, c->stream));
@@ -678,11 +744,7 @@ extern "C" size_t tbls_pk_table_size(void) {
 }
 
 extern "C" int tbls_batch_verify_idx(const tbls_set_idx* sets, size_t n, const uint64_t* rand, int n_gpus, int* ok, tbls_timing* t) {
-  *ok = 0;
-  const size_t tn = tbls_pk_table_size();
-  for (size_t i = 0; i < n; i++)
-    for (uint32_t k = 0; k < sets[i].n_pks; k++)
-      if (sets[i].key_idx[k] >= tn) return TBLS_BAD_ARGUMENT;
+  // indices are checked against each device's table under that device's lock (run_shard)
   return batch_verify_impl(sets, n, rand, n_gpus, ok, t);
 }
 
@@ -732,12 +794,13 @@ static int run_each(int d, const tbls_set* sets, size_t lo, size_t hi, uint8_t* 
   static const bool group = getenv("TBLS_EACH_GROUP") && getenv("TBLS_EACH_GROUP")[0] == '1';
   std::vector<uint64_t> rnd;
   if (group) {  // per-call randomizers in [1, 2^64) from the OS entropy source
-    std::random_device rd;
     rnd.resize(hi);
-    for (size_t i = lo; i < hi; i++) rnd[i] = ((((uint64_t)rd()) << 32) | rd()) | 1u;
+    if (fill_random(rnd.data() + lo, hi - lo)) return TBLS_DEVICE_ERROR;
   }
   pack_fill(c->hin.b(), p, sets, lo, group ? rnd.data() : nullptr, ETH2_DST, 43);  // else r = 1 for every set
   hipStream_t s = c->stream;
+  HIPCHK(ws_acquire(*c, s));
+  HIPCHK(hipStreamSynchronize(s));  // ws may be reallocated below
   HIPCHK(hipMemcpyAsync(c->in.p, c->hin.p, p.total, hipMemcpyHostToDevice, s));
   const uint8_t* di = c->in.as<uint8_t>();
   const uint32_t n = p.n, K = p.K;
@@ -759,6 +822,7 @@ static int run_each(int d, const tbls_set* sets, size_t lo, size_t hi, uint8_t* 
   const uint32_t ngrp = (n + TB_EACH_GROUP - 1) / TB_EACH_GROUP;
   const size_t gok = o;      o = align_up(o + ngrp);
   const size_t midx = o;     o = align_up(o + (group ? (size_t)n * 4 : 0));
+  const size_t mlist = o;    o = align_up(o + (size_t)n * 4 + 4);
   if (c->ws.ensure(o)) return TBLS_DEVICE_ERROR;
   uint8_t* w = c->ws.as<uint8_t>();
   const dim3 blk(TB_BLOCK), g((n + TB_BLOCK - 1) / TB_BLOCK);
@@ -767,8 +831,9 @@ static int run_each(int d, const tbls_set* sets, size_t lo, size_t hi, uint8_t* 
   if (K)
     hipLaunchKernelGGL(k_pk_decompress, dim3((K + TB_BLOCK - 1) / TB_BLOCK), blk, 0, s, di + p.off_pks, K, (g1a*)(w + pk_aff),
                        w + pk_code);
-  hipLaunchKernelGGL(k_set_pk, g, blk, 0, s, (const uint32_t*)(di + p.off_pkoff), (const g1a*)(w + pk_aff), (const uint8_t*)(w + pk_code),
-                     (const uint64_t*)(di + p.off_rand), n, (g1a*)(w + P), w + set_code, (uint32_t*)(w + n_bad), nullptr);
+  launch_set_pk(s, n, K, (const uint32_t*)(di + p.off_pkoff), (const g1a*)(w + pk_aff), (const uint8_t*)(w + pk_code),
+                (const uint64_t*)(di + p.off_rand), (g1a*)(w + P), w + set_code, (uint32_t*)(w + n_bad), nullptr, 0u,
+                (uint32_t*)(w + mlist), (uint32_t*)(w + mlist) + n);
   if (group)
     hipLaunchKernelGGL(k_set_sig, g, blk, 0, s, di + p.off_sigs, (const uint64_t*)(di + p.off_rand), n, (g2j*)(w + rsig), w + sig_code,
                        (uint32_t*)(w + n_bad));
@@ -805,6 +870,7 @@ static int run_each(int d, const tbls_set* sets, size_t lo, size_t hi, uint8_t* 
       HIPCHK(hipStreamSynchronize(s));
       for (uint32_t i : members) ok_host[i] = hu[n + ngrp + i];
     }
+    HIPCHK(ws_release(*c, s));
     return TBLS_SUCCESS;
   }
   // A/B (profiles/r01_bench_each_*): the wave final exponentiation runs its
@@ -825,6 +891,7 @@ static int run_each(int d, const tbls_set* sets, size_t lo, size_t hi, uint8_t* 
   if (c->hout.ensure(n)) return TBLS_DEVICE_ERROR;
   HIPCHK(hipMemcpyAsync(c->hout.p, w + okd, n, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
+  HIPCHK(ws_release(*c, s));
   memcpy(ok_host, c->hout.p, n);
   return TBLS_SUCCESS;
 }
@@ -860,7 +927,34 @@ extern "C" int tbls_verify_each(const tbls_set* sets, size_t n, int n_gpus, int*
   return TBLS_SUCCESS;
 }
 
+// fastAggregateVerify of every set (config 2: sync-committee sets of 512 keys).
+// A randomized batch over the sets with keys settles the common all-valid
+// case with one final exponentiation: it accepts iff every set verifies (with
+// probability 1 - 2^-64 per forged set), and then every such set's verdict is
+// 1.  Otherwise the per-set pass (tbls_verify_each) gives the verdicts.
 extern "C" int tbls_fast_aggregate_verify_many(const tbls_set* sets, size_t n, int* ok_per_set) {
+  if (ensure_init()) return TBLS_DEVICE_ERROR;
+  if (n == 0) return TBLS_SUCCESS;
+  std::vector<tbls_set> keyed;
+  std::vector<size_t> pos;
+  for (size_t i = 0; i < n; i++) {
+    ok_per_set[i] = 0;  // empty key list -> false (BLS.java:193-195)
+    if (sets[i].n_pks) {
+      keyed.push_back(sets[i]);
+      pos.push_back(i);
+    }
+  }
+  if (keyed.size() >= 2) {
+    std::vector<uint64_t> rnd(keyed.size());
+    if (fill_random(rnd.data(), rnd.size())) return TBLS_DEVICE_ERROR;
+    int ok = 0;
+    const int rc = batch_verify_impl(keyed.data(), keyed.size(), rnd.data(), 1, &ok, nullptr);
+    if (rc != TBLS_SUCCESS) return rc;
+    if (ok) {
+      for (size_t p : pos) ok_per_set[p] = 1;
+      return TBLS_SUCCESS;
+    }
+  }
   return tbls_verify_each(sets, n, 1, ok_per_set);
 }
 
@@ -1179,23 +1273,4 @@ extern "C" int tbls_dev_final_verify(int device, const void* partials, uint32_t 
   HIPCHK(hipSetDevice(c->dev));
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
   return launch_final(*c, partials, g, s, ok);
-}
-
-extern "C" int tbls_test_ops(int op, const uint8_t* in, uint8_t* out, size_t n) {
-  return with_device0([&](dev_ctx& c) -> int {
-    if (c.in.ensure(n * TB_TEST_IN + 256) || c.ws.ensure(n * TB_TEST_OUT + 256)) return (int)TBLS_DEVICE_ERROR;
-    HIPCHK(hipMemcpyAsync(c.in.p, in, n * TB_TEST_IN, hipMemcpyHostToDevice, c.stream));
-    HIPCHK(hipMemsetAsync(c.ws.p, 0, n * TB_TEST_OUT, c.stream));
-    if (op == 29) {  // TOP_FINAL_EXP_WAVE: one 64-lane block per record
-      hipLaunchKernelGGL(k_test_final_exp_wave, dim3(n), dim3(64), 0, c.stream, c.in.as<uint8_t>(), c.ws.as<uint8_t>());
-      return fetch(c, out, c.ws.p, n * TB_TEST_OUT);
-    }
-    if (op == 31) {  // TOP_MILLER_WAVE: one 64-lane block per record
-      hipLaunchKernelGGL(k_test_miller_wave, dim3(n), dim3(64), 0, c.stream, c.in.as<uint8_t>(), c.ws.as<uint8_t>());
-      return fetch(c, out, c.ws.p, n * TB_TEST_OUT);
-    }
-    hipLaunchKernelGGL(k_test_ops, dim3((n + TB_BLOCK - 1) / TB_BLOCK), dim3(TB_BLOCK), 0, c.stream, op, c.in.as<uint8_t>(), c.ws.as<uint8_t>(),
-                       (uint32_t)n);
-    return fetch(c, out, c.ws.p, n * TB_TEST_OUT);
-  });
 }

@@ -21,16 +21,33 @@ TB_HD TB_INLINE int stage_pk(const uint8_t* b48, g1a& a) {
   return code;
 }
 
+// Key k of a set: pk_aff[idx[k]] when idx is given (device-resident key table,
+// tbls_pk_table_load; indices >= tab_n make the set invalid), else pk_aff[k].
+TB_HD TB_INLINE bool set_key(const uint32_t* idx, uint32_t tab_n, uint32_t j, uint32_t& k) {
+  k = idx ? idx[j] : j;
+  return !idx || k < tab_n;
+}
+
+// P = [r] apk affine for an aggregate key already summed (Jacobian); infinity
+// (including an all-cancelling sum) -> PK_IS_INFINITY.
+TB_HD TB_INLINE int stage_set_pk_finish(const g1j& acc, uint64_t r, g1a& P) {
+  P.x = fp_zero();
+  P.y = fp_zero();
+  if (jac_is_inf(acc)) return TB_PK_IS_INFINITY;
+  g1j rp = r == 1 ? acc : jac_mul_u64(acc, r);
+  if (!jac_to_aff(P, rp)) return TB_PK_IS_INFINITY;
+  return TB_SUCCESS;
+}
+
 // aggregate keys [b, e) (any invalid -> PK_IS_INFINITY), P = [r] apk affine.
-// idx (nullable): key k of the set is pk_aff[idx[k]] (device-resident key
-// table, tbls_pk_table_load) instead of pk_aff[k].
 TB_HD TB_INLINE int stage_set_pk(const g1a* pk_aff, const uint8_t* pk_code, uint32_t b, uint32_t e, uint64_t r, g1a& P,
-                                 const uint32_t* idx = nullptr) {
+                                 const uint32_t* idx = nullptr, uint32_t tab_n = 0) {
   int code = TB_SUCCESS;
   P.x = fp_zero();
   P.y = fp_zero();
   if (e - b == 1) {
-    const uint32_t k = idx ? idx[b] : b;
+    uint32_t k;
+    if (!set_key(idx, tab_n, b, k)) return TB_BAD_ENCODING;
     if (pk_code[k] != TB_SUCCESS) return TB_PK_IS_INFINITY;
     g1j rp = jac_mul_u64_aff(pk_aff[k], r);
     if (!jac_to_aff(P, rp)) code = TB_PK_IS_INFINITY;
@@ -38,14 +55,12 @@ TB_HD TB_INLINE int stage_set_pk(const g1a* pk_aff, const uint8_t* pk_code, uint
   }
   g1j acc = jac_inf<fp>();
   for (uint32_t j = b; j < e; j++) {
-    const uint32_t k = idx ? idx[j] : j;
+    uint32_t k;
+    if (!set_key(idx, tab_n, j, k)) return TB_BAD_ENCODING;
     if (pk_code[k] != TB_SUCCESS) return TB_PK_IS_INFINITY;  // BlstPublicKey.java:58-65
     acc = jac_add_aff(acc, pk_aff[k]);
   }
-  if (jac_is_inf(acc)) return TB_PK_IS_INFINITY;
-  g1j rp = jac_mul_u64(acc, r);
-  if (!jac_to_aff(P, rp)) code = TB_PK_IS_INFINITY;
-  return code;
+  return stage_set_pk_finish(acc, r, P);
 }
 
 // decode signature, G2 check, [r] sig (infinity allowed and skipped)

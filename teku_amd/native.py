@@ -163,7 +163,6 @@ _SIGS = {
         ctypes.c_int,
         [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p],
     ),
-    "tbls_test_ops": (ctypes.c_int, [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]),
 }
 
 EXPORTED = tuple(_SIGS)

@@ -36,6 +36,7 @@ from concurrent.futures import Future
 from typing import Callable, List, Optional, Sequence
 
 from . import bls as _bls
+from .synth import SetArray
 
 DEFAULT_MIN_BATCH_SIZE_TO_SPLIT = 25  # AggregatingSignatureVerificationService.java:42
 DEFAULT_MAX_BATCH_SIZE = 16384
@@ -64,9 +65,13 @@ def _set_tuple(pks, msg, sig):
 def _hip_batch(sets) -> bool:
     rands = [int.from_bytes(secrets.token_bytes(8), "big") or 1 for _ in sets]  # BlstBLS12381.java:191-195
     try:
-        return _bls.batch_verify_raw(sets, rands)
+        return SetArray.from_tuples(sets).batch_verify(rands)
     except ValueError:  # an empty key list in the batch: settle it per set
         return False
+
+
+def _hip_each(sets) -> List[bool]:
+    return SetArray.from_tuples(sets).verify_each()
 
 
 class AggregatingSignatureVerificationService:
@@ -85,7 +90,7 @@ class AggregatingSignatureVerificationService:
         self.min_batch_size_to_split = min_batch_size_to_split
         self.split_fallback = split_fallback
         self._batch_fn = batch_fn or _hip_batch
-        self._each_fn = each_fn or _bls.verify_each_raw
+        self._each_fn = each_fn or _hip_each
         self.batch_signature_tasks: "queue.Queue[SignatureTask]" = queue.Queue(maxsize=queue_capacity)
         self._running = False
         self._threads: List[threading.Thread] = []

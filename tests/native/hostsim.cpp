@@ -10,7 +10,7 @@ unsigned long long tb_mul_count = 0;
 unsigned long long tb_sqr_count = 0;
 }
 #endif
-#include "../../teku_amd/csrc/tb_testops.h"
+#include "tb_testops.h"
 
 extern "C" int tbls_hostsim_test_ops(int op, const uint8_t* in, uint8_t* out, size_t n) {
   for (size_t i = 0; i < n; i++) tb::test_op(op, in + i * TB_TEST_IN, out + i * TB_TEST_OUT);

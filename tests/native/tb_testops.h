@@ -7,7 +7,7 @@
 // big-endian plain integers; Fp2 = c0||c1; Fp6 = c0||c1||c2; Fp12 = c0||c1;
 // affine points x||y.
 #pragma once
-#include "tb_stages.h"
+#include "../../teku_amd/csrc/tb_stages.h"
 
 namespace tb {
 

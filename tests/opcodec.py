@@ -1,10 +1,11 @@
-"""Record codec for the primitive test ops (teku_amd/csrc/tb_testops.h).
+"""Record codec for the primitive test ops (tests/native/tb_testops.h).
 
 Used by the CPU hostsim tests and by the -m gpu tests (same records, same
 expected values from the oracle).
 """
 
 import ctypes
+import os
 
 import numpy as np
 
@@ -76,3 +77,21 @@ def run_ops(fn, op, records):
     rc = fn(OPS[op], inb.ctypes.data_as(ctypes.c_void_p), outb.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(n))
     assert rc == 0, rc
     return unpack(outb.tobytes(), n)
+
+
+TEST_LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "native", "_build", "libtekubls_test.so")
+
+
+def load_test_lib():
+    """libtekubls_test.so (tests/native/k_test.hip): the primitive-op kernels,
+    kept out of the product library.  The product library is initialised first
+    so both share one HIP runtime and device."""
+    from teku_amd import native
+
+    native.lib()
+    if not os.path.exists(TEST_LIB_PATH):
+        raise RuntimeError("test library not built: __graft_entry__.build()")
+    L = ctypes.CDLL(TEST_LIB_PATH)
+    L.tbls_test_ops.restype = ctypes.c_int
+    L.tbls_test_ops.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
+    return L

@@ -1,0 +1,144 @@
+"""GPU parity at every BASELINE.json config size, checked against the C oracle
+(oracle/c/bls_oracle.c, pinned by the reference's KATs in tests/test_oracle_c.py).
+
+  config 1  BLS.batchVerify of 128 single-signer interop-key sets on distinct
+            messages (BLSBenchmark.java:41-57), valid and every SURVEY.md 8(d)
+            tamper, through tbls_batch_verify
+  config 2  64 sync-committee sets x 512 keys, fastAggregateVerify per set
+            (BLS.java:185-207) through tbls_fast_aggregate_verify_many, 3 tampered
+  config 3  64 attestation sets x 488 keys, randomized batchVerify, valid / one
+            bad key / one bad signature (BlstPublicKey.java:55-71)
+  config 4  16,384 single-signer sets through the service semantics
+            (AggregatingSignatureVerificationService.java:171-227), 4 bad, per-task
+            verdicts
+  config 5  one GPU's 131,072-set shard of the 1,048,576-set batch, valid and
+            tampered in the first, middle and last MSM chunk
+
+Inputs are the synthetic sets of SURVEY.md 8(d) (teku_amd/synth.py: interop keys,
+sha256 messages, GPU-signed); the oracle verifies the same bytes.
+"""
+
+import os
+
+import pytest
+
+from oracle import c_oracle as C
+
+pytestmark = pytest.mark.gpu
+
+THREADS = max(1, min(16, os.cpu_count() or 1))
+
+
+@pytest.fixture(scope="module")
+def S():
+    import torch  # noqa: F401  (share torch's HIP runtime)
+
+    from teku_amd import native, synth
+
+    native.lib()
+    return synth
+
+
+def _split(pks, msgs, sigs):
+    n = len(sigs) // 96
+    return [pks[48 * i : 48 * i + 48] for i in range(n)], [msgs[32 * i : 32 * i + 32] for i in range(n)], [sigs[96 * i : 96 * i + 96] for i in range(n)]
+
+
+def _tampers(S, pk, ms, sg, j, sk_j):
+    """SURVEY.md 8(d) tampered-set list at position j (each expects false)."""
+    out = {}
+    s = list(sg)
+    s[j] = S.sign_blob([sk_j], [bytes([ms[j][0] ^ 1]) + ms[j][1:]])
+    out["sig on m^1"] = (pk, ms, s)
+    m = list(ms)
+    m[j], m[j + 1] = m[j + 1], m[j]
+    out["two messages swapped"] = (pk, m, sg)
+    for name, bad in [("zero sig", bytes(96)), ("infinity sig", S.INFINITY_G2), ("non-G2 sig", S.NOT_IN_G2)]:
+        s = list(sg)
+        s[j] = bad
+        out[name] = (pk, ms, s)
+    for name, bad in [("infinity key", S.INFINITY_G1), ("0x9378a6 key", S.BAD_PK)]:
+        p = list(pk)
+        p[j] = bad
+        out[name] = (p, ms, sg)
+    return out
+
+
+def test_config1_128_sets(S):
+    pks, msgs, sigs = S.single_signer(0, 128)
+    pk, ms, sg = _split(pks, msgs, sigs)
+    r = S.random_multipliers(128)
+    assert S.SetArray.single(pks, msgs, sigs).batch_verify(r) is True
+    assert C.batch_verify(pk, ms, sg, r, threads=THREADS) is True
+    for j in (0, 77, 126):
+        for name, (p, m, s) in _tampers(S, pk, ms, sg, j, S.interop_sk(j)).items():
+            got = S.SetArray.single(b"".join(p), b"".join(m), b"".join(s)).batch_verify(r)
+            exp = C.batch_verify(p, m, s, r, threads=THREADS)
+            assert got is exp is False, (name, j)
+
+
+def test_config2_64x512_fast_aggregate_verify(S):
+    keys, msgs, sigs = S.multi_key(64, 512, first_key=0, seed=2)
+    arr = S.SetArray.from_lists(keys, msgs, sigs)
+    assert arr.fast_aggregate_verify_many() == [True] * 64
+    # three tampered sets: a signature over another message, a key swapped for
+    # a non-signer, an infinity key (BlstPublicKey.aggregate -> infinity)
+    k2, m2, s2 = [list(k) for k in keys], list(msgs), list(sigs)
+    s2[5] = sigs[6]
+    k2[20][100] = S.pubkeys([S.interop_sk(40000)])[0]
+    k2[63][511] = S.INFINITY_G1
+    got = S.SetArray.from_lists(k2, m2, s2).fast_aggregate_verify_many()
+    exp = C.verify_each(k2, m2, s2, threads=THREADS)
+    assert got == exp
+    assert [i for i, v in enumerate(got) if not v] == [5, 20, 63]
+
+
+def test_config3_64x488_randomized_batch(S):
+    keys, msgs, sigs = S.multi_key(64, 488, first_key=1000, seed=3)
+    r = S.random_multipliers(64)
+    assert S.SetArray.from_lists(keys, msgs, sigs).batch_verify(r) is True
+    assert C.batch_verify_sets(keys, msgs, sigs, r, threads=THREADS) is True
+    k2 = [list(k) for k in keys]
+    k2[31][7] = S.pubkeys([S.interop_sk(50000)])[0]  # one bad key
+    assert S.SetArray.from_lists(k2, msgs, sigs).batch_verify(r) is False
+    assert C.batch_verify_sets(k2, msgs, sigs, r, threads=THREADS) is False
+    s2 = list(sigs)
+    s2[40] = sigs[41]  # one bad signature
+    assert S.SetArray.from_lists(keys, msgs, s2).batch_verify(r) is False
+    assert C.batch_verify_sets(keys, msgs, s2, r, threads=THREADS) is False
+
+
+def test_config4_16k_through_service(S):
+    from teku_amd.service import AggregatingSignatureVerificationService, SignatureTask
+
+    n = 16384
+    pks, msgs, sigs = S.single_signer(0, n, seed=4)
+    pk, ms, sg = _split(pks, msgs, sigs)
+    bad = {11: sg[12], 5000: bytes(96), 9999: S.NOT_IN_G2, 16383: sg[0]}
+    for j, b in bad.items():
+        sg[j] = b
+    svc = AggregatingSignatureVerificationService(max_batch_size=n)
+    tasks = [SignatureTask([(pk[i], 1, ms[i], sg[i])]) for i in range(n)]
+    svc.batch_verify_signatures(tasks)
+    got = [t.result.result() for t in tasks]
+    exp = C.verify_each([[p] for p in pk], ms, sg, threads=THREADS)
+    assert got == exp
+    assert [i for i, v in enumerate(got) if not v] == sorted(bad)
+    assert svc.device_passes == 2
+
+
+def test_config5_131k_shard(S):
+    n = 131072
+    pks, msgs, sigs = S.single_signer(0, n, seed=0)
+    r = S.random_multipliers(n)
+    arr = S.SetArray.single(pks, msgs, sigs)
+    assert arr.batch_verify(r) is True
+    pk, ms, sg = _split(pks, msgs, sigs)
+    assert C.batch_verify(pk, ms, sg, r, threads=THREADS) is True
+    # tampered sets in the first, middle and last chunk of the MSM bucket lists
+    for j in (3, n // 2 + 1, n - 2):
+        for name, (p, m, s) in _tampers(S, pk, ms, sg, j, S.interop_sk(j % 65536)).items():
+            got = S.SetArray.single(b"".join(p), b"".join(m), b"".join(s)).batch_verify(r)
+            # the oracle's verdict on the tampered set alone decides the batch
+            assert C.verify_each([[p[j]]], [m[j]], [s[j]])[0] is False, (name, j)
+            assert got is False, (name, j)

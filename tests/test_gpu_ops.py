@@ -1,4 +1,4 @@
-"""GPU parity of the primitive kernels (tb_testops.h via tbls_test_ops) against the oracle."""
+"""GPU parity of the primitive kernels (tests/native/tb_testops.h via the test library libtekubls_test.so) against the oracle."""
 
 import random
 
@@ -13,9 +13,7 @@ pytestmark = pytest.mark.gpu
 
 @pytest.fixture(scope="module")
 def run():
-    from teku_amd import native
-
-    L = native.lib()
+    L = load_test_lib()
     return lambda op, recs: run_ops(L.tbls_test_ops, op, recs)
 
 

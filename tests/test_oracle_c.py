@@ -14,6 +14,9 @@ import pytest
 from oracle import bls12_381 as O
 from oracle.keys import blstestutil_sk, interop_sk
 from tests.test_oracle_kats import (
+    KAT_FAV4_MSG,
+    KAT_FAV4_PKS,
+    KAT_FAV4_SIG,
     KAT_AGGSLOT_SIG,
     KAT_INTEROP_PK,
     KAT_INTEROP_SK,
@@ -91,3 +94,37 @@ def test_batch_verify_real_values_and_tampered(C):
     assert C.batch_verify(pks, msgs, bad, r) is False
     assert C.batch_verify(pks, msgs, sigs[:5] + [NOT_IN_G2], r) is False
     assert C.batch_verify(pks[:5] + [BAD_PK], msgs, sigs, r) is False
+
+
+def test_multikey_sets_and_verify_each_match_python_oracle(C):
+    """Multi-key sets (configs 2/3 shape: BlstPublicKey.aggregate semantics,
+    BlstPublicKey.java:55-71) and per-set fastAggregateVerify verdicts
+    (BLS.java:185-207): the C oracle equals the Python restatement on the
+    reference's FAV-4 KAT (BLSTest.java:106-126) and on valid / tampered sets
+    (wrong key count, swapped signature, infinity / invalid / zero key,
+    infinity / non-G2 / zero signature, empty key list)."""
+    sks = [interop_sk(20 + i) for i in range(6)]
+    pks = [C.sk_to_pk(s) for s in sks]
+    m = b"\x42" * 32
+    agg3 = O.aggregate_sigs([C.sign(s, m) for s in sks[:3]])
+    agg2 = O.aggregate_sigs([C.sign(s, b"two") for s in sks[3:5]])
+    sets = [KAT_FAV4_PKS, pks[:3], pks[3:5], [pks[5]]]
+    msgs = [KAT_FAV4_MSG, m, b"two", b"one"]
+    sigs = [KAT_FAV4_SIG, agg3, agg2, C.sign(sks[5], b"one")]
+    assert C.batch_verify_sets(sets, msgs, sigs, [3, 5, 7, 11], threads=2) is True
+    assert C.verify_each(sets, msgs, sigs, threads=2) == [True] * 4
+    cases = [
+        (pks[:2], m, agg3),
+        (pks[:3], m, agg2),
+        (pks[:2] + [O.INFINITY_G1], m, agg3),
+        (pks[:2] + [BAD_PK], m, agg3),
+        (pks[:2] + [bytes(48)], m, agg3),
+        ([pks[0]], b"x", O.INFINITY_G2),
+        ([pks[0]], b"x", NOT_IN_G2),
+        ([pks[0]], b"x", bytes(96)),
+        ([], b"x", sigs[3]),
+    ]
+    got = C.verify_each([c[0] for c in cases], [c[1] for c in cases], [c[2] for c in cases], threads=3)
+    assert got == [O.fast_aggregate_verify(*c) for c in cases] == [False] * len(cases)
+    for c in cases[:-1]:
+        assert C.batch_verify_sets(sets + [c[0]], msgs + [c[1]], sigs + [c[2]], [3, 5, 7, 11, 13]) is False

@@ -69,6 +69,15 @@ def main():
     reduce_ += (64 * 7 + 8 * 7 + 7) * ADD + 56 * DBL  # k_msm_final: segment sums, Horner
     res["g2_sum"] = per_set + reduce_ / MSM_N
     sq["g2_sum"] = (8 * 255 / 256 * 4 * 2 + (2048 * 15 + 512 * 12 + 511) * 5 * 2 / MSM_N + (512 * 7 + 56) * 5 * 2 / MSM_N)
+    # k_set_pk_wave (configs 2/3): one wave per set of k keys -- (k - 64) mixed
+    # additions (a lane's first key costs nothing), a 63-addition LDS tree, then
+    # [r] apk on the Jacobian sum and the affine conversion.  G1 costs from the
+    # tb_curve.h formulas: madd-2007-bl 7M+4S = 11, add-2007-bl 11M+5S = 16,
+    # [r]P for a 64-bit r: 63 dbl-2009-l (2M+5S = 7) + ~32 additions.
+    G1_MADD, G1_ADD, G1_DBL = 11, 16, 7
+    finish = 63 * G1_DBL + 32 * G1_ADD + (res["set_pk"] - 63 * G1_DBL - 32 * G1_MADD)  # + inversion/affine as measured
+    for k in (488, 512):
+        res[f"set_pk_wave_{k}"] = (k - 64) * G1_MADD + 63 * G1_ADD + finish
     # k_miller2: two pairs per Fp12 accumulator -> work per pair = MILLER2 / 2
     pair = [enc_fp(a[0]) + enc_fp(a[1]) + enc_fp2(b[0]) + enc_fp2(b[1]) for a, b in zip(aff, q)]
     res["miller"] = per_unit("MILLER2", [pair[i] + pair[i + 1] for i in range(0, N, 2)], units_per_rec=2, name="miller")
