@@ -59,8 +59,8 @@ STAGE_KERNEL = {
     "set_pk": "k_set_pk",
     "set_sig": "k_sig_check",
     "set_hash": "k_set_hash",
-    "g2_sum": "k_msm_*",
-    "miller": "k_miller2",
+    "g2_sum": "k_msm_bucket + k_msm_bucket_pairs",
+    "miller": "k_miller_lines + k_miller_acc2",
     "fp12_prod": "k_fp12_prod_wave",
 }
 STAGE_UNITS = {"pk_decompress": "keys", "set_pk": "sets", "set_sig": "sets", "set_hash": "sets", "g2_sum": "sets", "miller": "pairs", "fp12_prod": "pairs"}
@@ -76,9 +76,11 @@ def roofline_entry(stage_ms, S, device, ms_per_step):
     peak = peak_mac_per_s(device)
     mads = M_PER_UNIT.get("mads_per_unit", {})
     per_stage = {}
+    pairs = M_PER_UNIT.get("pairs_per_set", 1.0)  # set pairs + the signature side's bucket pairs
+    units = {k: S * (pairs if STAGE_UNITS[k] == "pairs" else 1.0) for k in STAGES}
     for i, name in enumerate(STAGES):
         if name in M_PER_UNIT and stage_ms[i] > 0:
-            per_stage[name] = M_PER_UNIT[name] * MAC_PER_M * S / (stage_ms[i] * 1e-3)
+            per_stage[name] = M_PER_UNIT[name] * MAC_PER_M * units[name] / (stage_ms[i] * 1e-3)
     dom = max(range(len(STAGES)), key=lambda i: stage_ms[i])  # exclusive times
     name = STAGES[dom]
     achieved = per_stage.get(name)
@@ -97,11 +99,11 @@ def roofline_entry(stage_ms, S, device, ms_per_step):
         "frac": (achieved / peak) if achieved else None,
         "traffic": traffic,
         "model": "SURVEY.md 8(d): Fp products per unit (tools/mul_counts.json) x 300 MAC",
-        "units_per_launch": S,
+        "units_per_launch": round(units[name]),
         "unit_of_work": STAGE_UNITS[name],
         "fp_products_per_unit": M_PER_UNIT.get(name),
         "kernel_ms": stage_ms[dom],
-        "issue_frac": (mads[name] * S / (stage_ms[dom] * 1e-3)) / peak if name in mads else None,
+        "issue_frac": (mads[name] * units[name] / (stage_ms[dom] * 1e-3)) / peak if name in mads else None,
         "stage_frac": {k: v / peak for k, v in per_stage.items()},
         "pipeline_frac": (per_set * MAC_PER_M * S / (ms_per_step * 1e-3)) / peak if per_set else None,
     }

@@ -17,16 +17,38 @@ extern "C" __global__ void __launch_bounds__(TB_BLOCK)
   pk_code[i] = (uint8_t)code;
 }
 
+// -[r] g1 from the precomputed multiples comb[w * 256 + d] = (d 2^(8w)) g1
+// (k_g1_comb_init): at most 8 mixed additions, one per nonzero byte of r.  The
+// partial sums never meet an exceptional case (each window's multiple exceeds
+// the sum of the lower ones, all far below the group order).
+__device__ TB_INLINE g1a neg_r_g1(const g1a* __restrict__ comb, uint64_t r) {
+  g1j acc = jac_inf<fp>();
+  for (int w = 0; w < 8; w++) {
+    const uint32_t d = (uint32_t)(r >> (8 * w)) & 255u;
+    if (d) acc = jac_add_aff(acc, comb[w * 256 + d]);
+  }
+  g1a out;
+  if (!jac_to_aff(out, acc)) {
+    out.x = fp_zero();
+    out.y = fp_zero();
+  }
+  out.y = fp_neg(out.y);
+  return out;
+}
+
 // per set: aggregate keys (BlstPublicKey.aggregate semantics), P = [r] apk (affine);
 // key_idx (nullable): keys come from the device-resident table (pk_aff/pk_code =
 // the table, tab_n entries).  multi_wave: sets with more than one key are left
-// to k_set_pk_wave (one 64-lane wave per set) and skipped here.
+// to k_set_pk_wave (one 64-lane wave per set) and skipped here.  P2 (nullable):
+// the set's signature pair's G1 point, P2[i] = -[r_i] g1 (k_sigs.hip).
 extern "C" __global__ void __launch_bounds__(TB_BLOCK)
     k_set_pk(const uint32_t* __restrict__ pk_off, const g1a* __restrict__ pk_aff, const uint8_t* __restrict__ pk_code,
              const uint64_t* __restrict__ rand, uint32_t n, g1a* __restrict__ P, uint8_t* __restrict__ set_code,
-             uint32_t* __restrict__ n_bad, const uint32_t* __restrict__ key_idx, uint32_t tab_n, uint32_t multi_wave) {
+             uint32_t* __restrict__ n_bad, const uint32_t* __restrict__ key_idx, uint32_t tab_n, uint32_t multi_wave,
+             g1a* __restrict__ P2, const g1a* __restrict__ comb) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
+  if (P2) P2[i] = neg_r_g1(comb, rand[i]);
   const uint32_t b = pk_off[i], e = pk_off[i + 1];
   if (multi_wave && e - b > 1) return;
   g1a out;

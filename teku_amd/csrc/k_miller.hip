@@ -25,23 +25,6 @@ extern "C" __global__ void __launch_bounds__(64)
   if (threadIdx.x < 12) out[threadIdx.x] = L.F[threadIdx.x];
 }
 
-// The batch's (-g1, sum r_i sig_i) pair, wave-parallel, launched on the
-// signature stream right after the G2 sum.
-extern "C" __global__ void __launch_bounds__(64)
-    k_miller_one_wave(const g1a* __restrict__ P, const g2a* __restrict__ Q, const uint8_t* __restrict__ skip, uint32_t slot,
-                      fp12* __restrict__ f) {
-  __shared__ miller_lds L;
-  tb_latency_prio();
-  fp* out = reinterpret_cast<fp*>(f);
-  if (skip[slot]) {
-    if (threadIdx.x < 12) out[threadIdx.x] = threadIdx.x == 0 ? fp_one() : fp_zero();
-    return;
-  }
-  w12_tabs_load(L.s);
-  miller_loop_wave(L, P[slot], Q[slot]);
-  if (threadIdx.x < 12) out[threadIdx.x] = L.F[threadIdx.x];
-}
-
 // ---------------------------------------------------------------------------
 // One-pair-per-thread and two-pairs-per-thread Miller loops with every step
 // inlined into the kernel loop.  Measured on MI355X at 131072 pairs

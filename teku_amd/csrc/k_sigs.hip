@@ -4,68 +4,6 @@
 
 using namespace tb;
 
-// per set: decode signature, G2 check, [r] sig (Jacobian; infinity allowed)
-extern "C" __global__ void __launch_bounds__(TB_BLOCK)
-    k_set_sig(const uint8_t* __restrict__ sigs, const uint64_t* __restrict__ rand, uint32_t n, g2j* __restrict__ rsig,
-              uint8_t* __restrict__ sig_code, uint32_t* __restrict__ n_bad) {
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  g2j r;
-  int code = stage_set_sig(sigs + (size_t)i * 96, rand[i], r);
-  rsig[i] = r;
-  sig_code[i] = (uint8_t)code;
-  if (code != TB_SUCCESS) atomicAdd(n_bad, 1u);
-}
-
-// ---------------------------------------------------------------------------
-// S = sum rsig_i  (two-level reduction)
-// ---------------------------------------------------------------------------
-__device__ TB_INLINE void g2_block_reduce(g2j& v) {
-  __shared__ g2j sh[TB_BLOCK];
-  const int t = threadIdx.x;
-  sh[t] = v;
-  __syncthreads();
-  for (int s = TB_BLOCK / 2; s > 0; s >>= 1) {
-    if (t < s) sh[t] = jac_add(sh[t], sh[t + s]);
-    __syncthreads();
-  }
-  v = sh[0];
-}
-
-extern "C" __global__ void __launch_bounds__(TB_BLOCK)
-    k_g2_sum_partial(const g2j* __restrict__ in, uint32_t n, g2j* __restrict__ part) {
-  tb_latency_prio();
-  const uint32_t stride = gridDim.x * blockDim.x;
-  g2j acc = jac_inf<fp2>();
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) acc = jac_add(acc, in[i]);
-  g2_block_reduce(acc);
-  if (threadIdx.x == 0) part[blockIdx.x] = acc;
-}
-
-// final: S = sum of partials; writes pair index `slot`: P = -g1, Q = S (affine)
-extern "C" __global__ void __launch_bounds__(TB_BLOCK)
-    k_g2_sum_final(const g2j* __restrict__ part, uint32_t nparts, uint32_t slot, g1a* __restrict__ P, g2a* __restrict__ Q,
-                   uint8_t* __restrict__ skip) {
-  tb_latency_prio();
-  g2j acc = jac_inf<fp2>();
-  for (uint32_t i = threadIdx.x; i < nparts; i += blockDim.x) acc = jac_add(acc, part[i]);
-  g2_block_reduce(acc);
-  if (threadIdx.x == 0) {
-    g2a a;
-    bool ok = jac_to_aff(a, acc);
-    if (!ok) {
-      a.x = fp2_zero();
-      a.y = fp2_zero();
-    }
-    g1a g;
-    g.x = fp_from_const(G1_X);
-    g.y = fp_from_const(G1_NEG_Y);
-    P[slot] = g;
-    Q[slot] = a;
-    skip[slot] = ok ? 0 : 1;  // infinite aggregate signature: no pair (blst skips it)
-  }
-}
-
 // BlstSignature.aggregate: every input must decode and be in G2.
 // out[0..95] = compressed sum; status[0] = first failing code (0 = ok)
 extern "C" __global__ void __launch_bounds__(TB_BLOCK)
@@ -147,46 +85,75 @@ extern "C" __global__ void __launch_bounds__(TB_BLOCK)
 }
 
 // ---------------------------------------------------------------------------
-// Large batches: S = sum r_i sig_i as a bucket multi-scalar multiplication
-// (Pippenger) instead of one 64-bit [r_i] sig_i per set.  The per-set kernel
-// only decodes and group-checks (k_sig_check); the MSM then costs ~8 mixed
-// additions per signature (8-bit windows, 8 windows for the 64-bit
-// randomizers of BlstBLS12381.nextBatchRandomMultiplier, l.191-195) instead
-// of 63 doublings + ~32 additions, and runs on the signature stream
-// underneath the hash / key / Miller stages.  Any invalid signature fails the
-// whole batch (n_bad), so only valid, finite signatures enter the sum;
-// infinity contributes nothing (blst skips it).
+// The signature side of the randomized batch equation
+//     prod_i e(r_i apk_i, H(m_i)) * e(-g1, sum_i r_i sig_i) == 1
+// without any G2 scalar multiplication.  g1 is a fixed base, so the scalar
+// can move to G1 with precomputed multiples C[w][d] = (d 2^(8w)) g1
+// (k_g1_comb_init, once per device):
+//
+//  * small batches (n < TB_MSM_MIN): one extra pair per set,
+//      e(-g1, r_i sig_i) = e(-[r_i] g1, sig_i),  [r_i] g1 = sum_w C[w][byte w of r_i]
+//    (at most 8 mixed additions, k_set_pk), so a set costs one more Miller
+//    pair instead of a 64-bit G2 scalar multiplication (~2,000 Fp products,
+//    a serial chain in one lane -- the config-1 latency);
+//  * large batches: a bucket sum by the randomizers' bytes,
+//      sum_i r_i sig_i = sum_w sum_d (d 2^(8w)) B[w][d],  B[w][d] = sum of the
+//      sig_i whose byte w is d,
+//    and each bucket sum becomes one extra pair e(-C[w][d], B[w][d]): 8 x 255
+//    = 2040 pairs for the whole batch.  The bucket sums cost 8 mixed
+//    additions per signature; the weighting by d 2^(8w) -- the latency chain
+//    of a Pippenger reduction (running sums, 56 doublings of Horner) -- is
+//    replaced by the precomputed G1 multiples, and the 2040 pairs ride in the
+//    batch's Miller kernel.
 //
 //   k_msm_hist     per set: bucket counts (window w, digit d = byte w of r);
-//                  hist / scan / scatter depend only on the randomizers, so they
-//                  run on stream b concurrently with k_sig_check
-//   k_msm_scan     exclusive scan of the 8 x 256 counts -> bucket offsets
-//   k_msm_scatter  per set: set index into its 8 bucket lists
-//   k_msm_bucket   per (bucket, chunk): sum of the chunk's affine points
-//   k_msm_bsum     per bucket: sum of its chunk partials
-//   k_msm_window   per (window, 4-digit segment): sum_d d * B_d (running sums)
-//   k_msm_final    per window: sum of segments (two levels); then Horner over
-//                  the windows, affine S into pair slot n (with P = -g1)
-// The chain is latency-bound (few threads per kernel) and runs under the
-// throughput kernels, so every MSM kernel takes top wave priority.
+//   k_msm_scan     exclusive scan -> bucket offsets          (randomizers only:
+//   k_msm_scatter  per set: set index into its 8 bucket lists  run beside k_sig_check)
+//   k_msm_bucket   per (bucket, chunk): sum of the chunk's affine signatures
+//   k_msm_bucket_pairs  per bucket: 64-lane LDS tree over its chunk sums,
+//                  affine B[w][d] and the pair (-C[w][d], B[w][d])
+// Any invalid signature fails the whole batch (n_bad), so only valid, finite
+// signatures enter the buckets; infinity contributes nothing (blst skips it).
 // ---------------------------------------------------------------------------
 #define TB_MSM_W 8          // windows
 #define TB_MSM_NB 256       // buckets per window (digit 0 unused)
-#define TB_MSM_CHUNKS 16    // chunks per bucket list
-#define TB_MSM_SEGS 64      // digit segments per window (4 digits each)
+#define TB_MSM_CHUNKS 64    // chunks per bucket list (131072 threads at 2048 buckets)
 
-// per set: decode + G2 check; affine sig and use flag (valid and finite)
+// thread (w, d): comb[w * 256 + d] = (d 2^(8w)) g1, affine (d = 0: unused)
+extern "C" __global__ void __launch_bounds__(TB_BLOCK) k_g1_comb_init(g1a* __restrict__ comb) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= TB_MSM_W * TB_MSM_NB) return;
+  const uint32_t w = t / TB_MSM_NB, d = t % TB_MSM_NB;
+  g1a out;
+  out.x = fp_zero();
+  out.y = fp_zero();
+  if (d) {
+    g1j g = {fp_from_const(G1_X), fp_from_const(G1_Y), fp_one()};
+    for (uint32_t k = 0; k < 8 * w; k++) g = jac_dbl(g);
+    (void)jac_to_aff(out, jac_mul_u64(g, d));
+  }
+  comb[t] = out;
+}
+
+// per set: decode + G2 check.  skip_mode = 0: sig_aff + sig_use (1 = valid and
+// finite: the bucket input); skip_mode = 1: sig_aff = Q of the set's signature
+// pair and sig_use = its skip flag (1 = no pair: infinite or invalid).
 extern "C" __global__ void __launch_bounds__(TB_BLOCK)
     k_sig_check(const uint8_t* __restrict__ sigs, uint32_t n, g2a* __restrict__ sig_aff, uint8_t* __restrict__ sig_use,
-                uint8_t* __restrict__ sig_code, uint32_t* __restrict__ n_bad) {
+                uint8_t* __restrict__ sig_code, uint32_t* __restrict__ n_bad, uint32_t skip_mode) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   g2a a;
   bool inf;
   int code = g2_decompress(a, inf, sigs + (size_t)i * 96);
   if (code == TB_SUCCESS && !inf && !g2_in_group(jac_from_aff(a))) code = TB_POINT_NOT_IN_GROUP;
+  const bool use = code == TB_SUCCESS && !inf;
+  if (!use) {
+    a.x = fp2_zero();
+    a.y = fp2_zero();
+  }
   sig_aff[i] = a;
-  sig_use[i] = (code == TB_SUCCESS && !inf) ? 1 : 0;
+  sig_use[i] = (use != (skip_mode != 0)) ? 1 : 0;
   sig_code[i] = (uint8_t)code;
   if (code != TB_SUCCESS) atomicAdd(n_bad, 1u);
 }
@@ -194,7 +161,6 @@ extern "C" __global__ void __launch_bounds__(TB_BLOCK)
 extern "C" __global__ void __launch_bounds__(TB_BLOCK)
     k_msm_hist(const uint64_t* __restrict__ rand, uint32_t n, uint32_t* __restrict__ cnt) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  tb_latency_prio();
   if (i >= n) return;
   const uint64_t r = rand[i];
   for (int w = 0; w < TB_MSM_W; w++) {
@@ -206,7 +172,6 @@ extern "C" __global__ void __launch_bounds__(TB_BLOCK)
 // one block of 256 threads: off[b] = sum_{b' < b} cnt[b'], off[2048] = total; cur = off
 extern "C" __global__ void __launch_bounds__(256)
     k_msm_scan(const uint32_t* __restrict__ cnt, uint32_t* __restrict__ off, uint32_t* __restrict__ cur) {
-  tb_latency_prio();
   __shared__ uint32_t sh[256];
   const int t = threadIdx.x;
   const int per = TB_MSM_W * TB_MSM_NB / 256;  // 8 entries per thread
@@ -235,7 +200,6 @@ extern "C" __global__ void __launch_bounds__(256)
 extern "C" __global__ void __launch_bounds__(TB_BLOCK)
     k_msm_scatter(const uint64_t* __restrict__ rand, uint32_t n, uint32_t* __restrict__ cur, uint32_t* __restrict__ idx) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  tb_latency_prio();
   if (i >= n) return;
   const uint64_t r = rand[i];
   for (int w = 0; w < TB_MSM_W; w++) {
@@ -244,12 +208,11 @@ extern "C" __global__ void __launch_bounds__(TB_BLOCK)
   }
 }
 
-// thread (bucket b, chunk c): sum of the affine points of chunk c of list b
+// thread (bucket b, chunk c): sum of the affine signatures of chunk c of list b
 extern "C" __global__ void __launch_bounds__(TB_BLOCK)
     k_msm_bucket(const g2a* __restrict__ sig_aff, const uint8_t* __restrict__ use, const uint32_t* __restrict__ off,
                  const uint32_t* __restrict__ idx, g2j* __restrict__ part) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  tb_latency_prio();
   if (t >= TB_MSM_W * TB_MSM_NB * TB_MSM_CHUNKS) return;
   const uint32_t b = t / TB_MSM_CHUNKS, c = t % TB_MSM_CHUNKS;
   const uint32_t lo = off[b], hi = off[b + 1];
@@ -264,75 +227,31 @@ extern "C" __global__ void __launch_bounds__(TB_BLOCK)
   part[t] = acc;
 }
 
-// thread b: B_b = sum of its chunk partials
-extern "C" __global__ void __launch_bounds__(TB_BLOCK) k_msm_bsum(const g2j* __restrict__ part, g2j* __restrict__ bucket) {
-  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-  tb_latency_prio();
-  if (b >= TB_MSM_W * TB_MSM_NB) return;
-  g2j acc = part[b * TB_MSM_CHUNKS];
-  for (int c = 1; c < TB_MSM_CHUNKS; c++) acc = jac_add(acc, part[b * TB_MSM_CHUNKS + c]);
-  bucket[b] = acc;
-}
-
-// thread (w, seg): sum_{d in seg} d * B_{w,d} = running-sum total + (lo - 1) * sum B_d
-extern "C" __global__ void __launch_bounds__(TB_BLOCK) k_msm_window(const g2j* __restrict__ bucket, g2j* __restrict__ wseg) {
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= TB_MSM_W * TB_MSM_SEGS) return;
-  tb_latency_prio();
-  const uint32_t w = t / TB_MSM_SEGS, seg = t % TB_MSM_SEGS;
-  const uint32_t per = TB_MSM_NB / TB_MSM_SEGS;
-  uint32_t lo = seg * per;
-  if (lo == 0) lo = 1;  // digit 0 carries no weight
-  const uint32_t hi = (seg + 1) * per;
-  g2j acc = jac_inf<fp2>(), sum = jac_inf<fp2>();
-  for (uint32_t d = hi; d-- > lo;) {
-    acc = jac_add(acc, bucket[w * TB_MSM_NB + d]);
-    sum = jac_add(sum, acc);  // sum = sum_{d'} (d' - lo + 1) B_d'
-  }
-  if (lo > 1) sum = jac_add(sum, jac_mul_u64(acc, (uint64_t)(lo - 1)));
-  wseg[t] = sum;
-}
-
-// one block of 64 lanes: lane (w, j) sums 8 of window w's 64 segments, lanes
-// w < 8 sum those 8 partials, lane 0 combines S = sum_w 2^(8w) G_w (Horner)
-// and writes pair slot `slot`: P = -g1, Q = S
+// block (w, d != 0): B = sum of the bucket's 64 chunk sums (LDS tree); pair
+// slot w * 255 + d - 1 = (-C[w][d], B), skipped when B is infinity
 extern "C" __global__ void __launch_bounds__(64)
-    k_msm_final(const g2j* __restrict__ wseg, g2j* __restrict__ wsum, uint32_t slot, g1a* __restrict__ P, g2a* __restrict__ Q,
-                uint8_t* __restrict__ skip) {
+    k_msm_bucket_pairs(const g2j* __restrict__ part, const g1a* __restrict__ comb, g1a* __restrict__ P, g2a* __restrict__ Q,
+                       uint8_t* __restrict__ skip) {
   __shared__ g2j sh[64];
-  tb_latency_prio();
-  const int t = threadIdx.x;
-  {
-    const int w = t >> 3, j = t & 7;
-    const g2j* src = wseg + w * TB_MSM_SEGS + 8 * j;
-    g2j acc = src[0];
-    for (int s = 1; s < 8; s++) acc = jac_add(acc, src[s]);
-    sh[t] = acc;
-  }
+  const uint32_t t = threadIdx.x;
+  const uint32_t w = blockIdx.x / (TB_MSM_NB - 1), d = blockIdx.x % (TB_MSM_NB - 1) + 1, b = w * TB_MSM_NB + d;
+  sh[t] = part[b * TB_MSM_CHUNKS + t];
   __syncthreads();
-  if (t < TB_MSM_W) {
-    g2j acc = sh[8 * t];
-    for (int j = 1; j < 8; j++) acc = jac_add(acc, sh[8 * t + j]);
-    wsum[t] = acc;
+  for (uint32_t s = 32; s > 0; s >>= 1) {
+    if (t < s) sh[t] = jac_add(sh[t], sh[t + s]);
+    __syncthreads();
   }
-  __syncthreads();
   if (t == 0) {
-    g2j S = wsum[TB_MSM_W - 1];
-    for (int w = TB_MSM_W - 2; w >= 0; --w) {
-      for (int k = 0; k < 8; k++) S = jac_dbl(S);
-      S = jac_add(S, wsum[w]);
-    }
     g2a a;
-    const bool ok = jac_to_aff(a, S);
+    const bool ok = jac_to_aff(a, sh[0]);
     if (!ok) {
       a.x = fp2_zero();
       a.y = fp2_zero();
     }
-    g1a g;
-    g.x = fp_from_const(G1_X);
-    g.y = fp_from_const(G1_NEG_Y);
-    P[slot] = g;
-    Q[slot] = a;
-    skip[slot] = ok ? 0 : 1;
+    g1a c = comb[b];
+    c.y = fp_neg(c.y);
+    P[blockIdx.x] = c;
+    Q[blockIdx.x] = a;
+    skip[blockIdx.x] = ok ? 0 : 1;
   }
 }

@@ -20,6 +20,7 @@ struct fp {
 #if !TB_DEVICE_PASS && defined(TB_COUNT_MULS)
 extern "C" unsigned long long tb_mul_count;  // host instrumentation (tools/count_muls.py)
 extern "C" unsigned long long tb_sqr_count;  // the squarings among them (301 vs 392 v_mad_u64_u32)
+extern "C" unsigned long long tb_fp2mul_count;  // lazy Fp2 products (3 M, 980 v_mad_u64_u32 each)
 #define TB_COUNT_MUL() (++tb_mul_count)
 #define TB_COUNT_SQR() (++tb_mul_count, ++tb_sqr_count)
 #else

@@ -7,13 +7,15 @@
 //
 //   k_pk_decompress   48-B key -> affine G1 + validity (decode, !inf, in G1)
 //   k_set_pk          per set: sum keys (any invalid -> set invalid), [r]apk -> affine P_i
-//   k_set_sig         per set: decode sig, G2 check, [r]sig (Jacobian)
 //   k_set_hash        per set: H(m_i) = hash_to_G2 -> affine Q_i
-//   k_g2_sum_*        S = sum [r_i]sig_i ; pair n = (-g1, S)
-//   k_sig_check, k_msm_*  large batches: decode + G2 check per set, S as a bucket MSM
+//   k_sig_check       per set: decode sig, G2 check
+//   signature side    small batches: pair (-[r_i] g1, sig_i) per set (k_set_pk);
+//                     large batches: bucket sums by randomizer byte, one pair
+//                     (-(d 2^(8w)) g1, B[w][d]) per bucket (k_msm_*, k_sigs.hip)
 //   k_miller2         per 2 pairs: f_t = Miller(P_2t, Q_2t) Miller(P_2t+1, Q_2t+1)
 //   k_miller1         per pair (small batches)
-//   k_miller_wave     per pair, one 64-lane wave (small batches; k_miller_one_wave: the (-g1, S) pair)
+//   k_miller_wave     per pair, one 64-lane wave (small batches)
+//   k_miller_lines + k_miller_acc*   large batches: G2 line precompute, then the Fp12 accumulation
 //   k_fp12_prod_wave  F = prod f_i  (chunked wave-parallel levels; the per-GPU partial, 576 B)
 //   k_final_verify    final_exp(F) == 1 && no invalid set
 //
@@ -49,22 +51,18 @@ __device__ TB_INLINE jac<F> jac_mul_u256(const jac<F>& P, const uint64_t* k) {
 // Kernel declarations (definitions in k_keys / k_sigs / k_hash / k_pair / k_test .hip),
 // for the host code in tb_lib.hip.
 extern "C" __global__ void k_pk_decompress(const uint8_t* __restrict__ pks, uint32_t K, g1a* __restrict__ pk_aff, uint8_t* __restrict__ pk_code);
-extern "C" __global__ void k_set_pk(const uint32_t* __restrict__ pk_off, const g1a* __restrict__ pk_aff, const uint8_t* __restrict__ pk_code, const uint64_t* __restrict__ rand, uint32_t n, g1a* __restrict__ P, uint8_t* __restrict__ set_code, uint32_t* __restrict__ n_bad, const uint32_t* __restrict__ key_idx, uint32_t tab_n, uint32_t multi_wave);
+extern "C" __global__ void k_set_pk(const uint32_t* __restrict__ pk_off, const g1a* __restrict__ pk_aff, const uint8_t* __restrict__ pk_code, const uint64_t* __restrict__ rand, uint32_t n, g1a* __restrict__ P, uint8_t* __restrict__ set_code, uint32_t* __restrict__ n_bad, const uint32_t* __restrict__ key_idx, uint32_t tab_n, uint32_t multi_wave, g1a* __restrict__ P2, const g1a* __restrict__ comb);
 extern "C" __global__ void k_multi_list(const uint32_t* __restrict__ pk_off, uint32_t n, uint32_t* __restrict__ list, uint32_t* __restrict__ cnt);
 extern "C" __global__ void k_set_pk_wave(const uint32_t* __restrict__ pk_off, const g1a* __restrict__ pk_aff, const uint8_t* __restrict__ pk_code, const uint64_t* __restrict__ rand, const uint32_t* __restrict__ list, const uint32_t* __restrict__ cnt, g1a* __restrict__ P, uint8_t* __restrict__ set_code, uint32_t* __restrict__ n_bad, const uint32_t* __restrict__ key_idx, uint32_t tab_n);
 extern "C" __global__ void k_aggregate_pks(const g1a* __restrict__ pk_aff, const uint8_t* __restrict__ pk_code, uint32_t K, uint8_t* __restrict__ out);
 extern "C" __global__ void k_sk_to_pk(const uint64_t* __restrict__ sks, uint32_t n, uint8_t* __restrict__ out);
-extern "C" __global__ void k_set_sig(const uint8_t* __restrict__ sigs, const uint64_t* __restrict__ rand, uint32_t n, g2j* __restrict__ rsig, uint8_t* __restrict__ sig_code, uint32_t* __restrict__ n_bad);
-extern "C" __global__ void k_sig_check(const uint8_t* __restrict__ sigs, uint32_t n, g2a* __restrict__ sig_aff, uint8_t* __restrict__ sig_use, uint8_t* __restrict__ sig_code, uint32_t* __restrict__ n_bad);
+extern "C" __global__ void k_g1_comb_init(g1a* __restrict__ comb);
+extern "C" __global__ void k_sig_check(const uint8_t* __restrict__ sigs, uint32_t n, g2a* __restrict__ sig_aff, uint8_t* __restrict__ sig_use, uint8_t* __restrict__ sig_code, uint32_t* __restrict__ n_bad, uint32_t skip_mode);
+extern "C" __global__ void k_msm_bucket_pairs(const g2j* __restrict__ part, const g1a* __restrict__ comb, g1a* __restrict__ P, g2a* __restrict__ Q, uint8_t* __restrict__ skip);
 extern "C" __global__ void k_msm_hist(const uint64_t* __restrict__ rand, uint32_t n, uint32_t* __restrict__ cnt);
 extern "C" __global__ void k_msm_scan(const uint32_t* __restrict__ cnt, uint32_t* __restrict__ off, uint32_t* __restrict__ cur);
 extern "C" __global__ void k_msm_scatter(const uint64_t* __restrict__ rand, uint32_t n, uint32_t* __restrict__ cur, uint32_t* __restrict__ idx);
 extern "C" __global__ void k_msm_bucket(const g2a* __restrict__ sig_aff, const uint8_t* __restrict__ use, const uint32_t* __restrict__ off, const uint32_t* __restrict__ idx, g2j* __restrict__ part);
-extern "C" __global__ void k_msm_bsum(const g2j* __restrict__ part, g2j* __restrict__ bucket);
-extern "C" __global__ void k_msm_window(const g2j* __restrict__ bucket, g2j* __restrict__ wseg);
-extern "C" __global__ void k_msm_final(const g2j* __restrict__ wseg, g2j* __restrict__ wsum, uint32_t slot, g1a* __restrict__ P, g2a* __restrict__ Q, uint8_t* __restrict__ skip);
-extern "C" __global__ void k_g2_sum_partial(const g2j* __restrict__ in, uint32_t n, g2j* __restrict__ part);
-extern "C" __global__ void k_g2_sum_final(const g2j* __restrict__ part, uint32_t nparts, uint32_t slot, g1a* __restrict__ P, g2a* __restrict__ Q, uint8_t* __restrict__ skip);
 extern "C" __global__ void k_aggregate_sigs(const uint8_t* __restrict__ sigs, uint32_t K, uint8_t* __restrict__ out, int* __restrict__ status);
 extern "C" __global__ void k_sig_validate(const uint8_t* __restrict__ sigs, uint32_t n, uint32_t* __restrict__ out);
 extern "C" __global__ void k_set_hash(const uint8_t* __restrict__ msgs, const uint32_t* __restrict__ msg_off, const uint8_t* __restrict__ dst, uint32_t dlen, uint32_t n, g2a* __restrict__ Q, uint8_t* __restrict__ skip);
@@ -74,8 +72,12 @@ extern "C" __global__ void k_hash_to_g2(const uint8_t* __restrict__ msgs, const 
 extern "C" __global__ void k_sign(const uint64_t* __restrict__ sks, const uint8_t* __restrict__ msgs, const uint32_t* __restrict__ msg_off, const uint8_t* __restrict__ dst, uint32_t dlen, uint32_t n, uint8_t* __restrict__ out);
 extern "C" __global__ void k_miller2(const g1a* __restrict__ P, const g2a* __restrict__ Q, const uint8_t* __restrict__ skip, const uint8_t* __restrict__ code_a, const uint8_t* __restrict__ code_b, uint32_t n, fp12* __restrict__ f);
 extern "C" __global__ void k_miller1(const g1a* __restrict__ P, const g2a* __restrict__ Q, const uint8_t* __restrict__ skip, const uint8_t* __restrict__ code_a, const uint8_t* __restrict__ code_b, uint32_t n, fp12* __restrict__ f);
+extern "C" __global__ void k_miller_lines(const g1a* __restrict__ P, const g2a* __restrict__ Q, const uint8_t* __restrict__ skip, const uint8_t* __restrict__ code_a, const uint8_t* __restrict__ code_b, uint32_t n, uint4* __restrict__ lines);
+extern "C" __global__ void k_miller_acc1(const uint4* __restrict__ lines, const uint8_t* __restrict__ skip, const uint8_t* __restrict__ code_a, const uint8_t* __restrict__ code_b, uint32_t n, fp12* __restrict__ f);
+extern "C" __global__ void k_miller_acc2(const uint4* __restrict__ lines, const uint8_t* __restrict__ skip, const uint8_t* __restrict__ code_a, const uint8_t* __restrict__ code_b, uint32_t n, fp12* __restrict__ f);
+#define TB_LINE_BYTES_PER_PAIR (68u * 288u)  // k_miller_lines output per pair
 extern "C" __global__ void k_miller_wave(const g1a* __restrict__ P, const g2a* __restrict__ Q, const uint8_t* __restrict__ skip, const uint8_t* __restrict__ code_a, const uint8_t* __restrict__ code_b, uint32_t n, fp12* __restrict__ f);
-extern "C" __global__ void k_miller_one_wave(const g1a* __restrict__ P, const g2a* __restrict__ Q, const uint8_t* __restrict__ skip, uint32_t slot, fp12* __restrict__ f);
+extern "C" __global__ void k_fp12_one(fp12* __restrict__ f);
 extern "C" __global__ void k_fp12_prod_wave(const fp12* __restrict__ in, uint32_t n, uint32_t chunk, fp12* __restrict__ out);
 extern "C" __global__ void k_final_verify_wave(const fp12* __restrict__ f, uint32_t g, const uint32_t* __restrict__ n_bad, int* __restrict__ result);
 extern "C" __global__ void k_final_verify(const fp12* __restrict__ f, const uint32_t* __restrict__ n_bad, int* __restrict__ result);

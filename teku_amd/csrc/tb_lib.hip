@@ -87,6 +87,7 @@ struct dev_ctx {
   // first waits for this event, then records it after its own work.
   hipEvent_t e_ws = nullptr;
   dbuf recs;  // partial records gathered for the final exponentiation (final_on_device0)
+  dbuf comb;  // (d 2^(8w)) g1 for w < 8, d < 256 (k_g1_comb_init): the signature pairs' G1 side
   hbuf hin, hout;
 };
 
@@ -106,33 +107,66 @@ size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
 // --------------------------------------------------------------------------
 // Fp12 product levels: each wave multiplies TB_PROD_CHUNK values (k_fp12_prod_wave)
 #define TB_PROD_CHUNK 16u
-// From this many sets on, S = sum r_i sig_i is a bucket MSM (k_msm_*, k_sigs.hip)
-// instead of one [r_i] sig_i per set plus a tree sum.
+// From this many sets on, the signature side of the batch equation is a
+// bucket sum by randomizer byte with 2040 bucket pairs (k_msm_*, k_sigs.hip);
+// below it, one signature pair (-[r_i] g1, sig_i) per set.
 #define TB_MSM_MIN 32768u
-#define TB_MSM_BUCKETS 2048u   // 8 windows x 256 digits
-#define TB_MSM_PARTS 32768u    // buckets x 16 chunks
-#define TB_MSM_WSEGS 512u      // 8 windows x 64 digit segments
-struct ws_layout {
-  size_t pk_aff, pk_code, P, Q, skip, set_code, sig_code, rsig, f, gpart, fpart, fpart2, n_bad, result;
-  size_t sig_aff, sig_use, msm_cnt, msm_off, msm_cur, msm_idx, msm_part, msm_bucket, msm_wseg, msm_wsum, mlist, mcnt, total;
-  uint32_t nb_g2, nb_f;
-  bool msm;
-  ws_layout(uint32_t n, uint32_t K) {
+#define TB_MSM_BUCKETS 2048u  // 8 windows x 256 digits (digit 0 unused)
+#define TB_MSM_BPAIRS 2040u   // 8 x 255 bucket pairs
+#define TB_MSM_PARTS (TB_MSM_BUCKETS * 64u)  // buckets x 64 chunks (k_msm_bucket)
+// Split Miller loop (k_miller_lines + k_miller_acc*, k_lines.hip): pairs per
+// line-buffer chunk (19,584 B of lines per pair: 2.6 GB per chunk), and the
+// pair count from which two pairs share an accumulator (the GPU is full at one
+// accumulator wave per SIMD: 1024 waves x 64 lanes x 2 pairs).
+#define TB_LINE_CHUNK 131072u
+#define TB_MILLER_PER2_MIN 131072u
+#define TB_MILLER1_MAX 4096u
+static bool miller_split() {
+  static const bool v = !(getenv("TBLS_MILLER_SPLIT") && getenv("TBLS_MILLER_SPLIT")[0] == '0');
+  return v;
+}
+// up to this many pairs, one pair per 64-lane workgroup (k_miller_wave);
+// TBLS_MILLER_WAVE_MAX overrides (tuning)
+static uint32_t miller_wave_max() {
+  static const uint32_t v = getenv("TBLS_MILLER_WAVE_MAX") ? (uint32_t)atoi(getenv("TBLS_MILLER_WAVE_MAX")) : 2048u;
+  return v;
+}
+
+// Pairs of a batch of n sets: [0, n) the sets' (r_i apk_i, H(m_i)), then the
+// signature side -- n pairs (-[r_i] g1, sig_i) below TB_MSM_MIN sets, else
+// TB_MSM_BPAIRS bucket pairs.
+struct pair_plan {
+  uint32_t n, n_extra, n_pairs, per;
+  bool msm, wave, split;
+  explicit pair_plan(uint32_t n_) : n(n_) {
     msm = n >= TB_MSM_MIN;
-    const uint32_t np = n + 1;
-    nb_g2 = (n + TB_BLOCK - 1) / TB_BLOCK;
-    if (nb_g2 > 256) nb_g2 = 256;
-    if (nb_g2 == 0) nb_g2 = 1;
-    nb_f = (np + TB_PROD_CHUNK - 1) / TB_PROD_CHUNK;  // first product level
+    n_extra = msm ? TB_MSM_BPAIRS : n;
+    n_pairs = n + n_extra;
+    wave = n_pairs <= miller_wave_max();
+    split = !wave && miller_split();
+    per = wave ? 1u : split ? (n_pairs >= TB_MILLER_PER2_MIN ? 2u : 1u) : (n_pairs <= TB_MILLER1_MAX ? 1u : 2u);
+  }
+  uint32_t n_f() const { return (n_pairs + per - 1) / per; }  // Miller values
+  uint32_t line_pairs() const { return split ? std::min(n_pairs, TB_LINE_CHUNK) : 0u; }
+};
+
+struct ws_layout {
+  size_t pk_aff, pk_code, P, Q, skip, set_code, sig_code, f, fpart, fpart2, n_bad, result;
+  size_t sig_aff, sig_use, msm_cnt, msm_off, msm_cur, msm_idx, msm_part, mlist, mcnt, lines, total;
+  uint32_t nb_f;
+  ws_layout() : total(0) {}
+  ws_layout(const pair_plan& pp, uint32_t K) {
+    const uint32_t n = pp.n, np = pp.n_pairs, nf = pp.n_f();
+    const bool msm = pp.msm;
+    nb_f = (nf + TB_PROD_CHUNK - 1) / TB_PROD_CHUNK;  // first product level
     size_t o = 0;
     pk_aff = o;   o = align_up(o + (size_t)K * sizeof(g1a));
     pk_code = o;  o = align_up(o + K);
     P = o;        o = align_up(o + (size_t)np * sizeof(g1a));
     Q = o;        o = align_up(o + (size_t)np * sizeof(g2a));
     skip = o;     o = align_up(o + np);
-    set_code = o; o = align_up(o + n);
-    sig_code = o; o = align_up(o + n);
-    rsig = o;     o = align_up(o + (msm ? 0 : (size_t)n * sizeof(g2j)));
+    set_code = o; o = align_up(o + np);  // extra pairs: zero codes
+    sig_code = o; o = align_up(o + np);
     const size_t nm = msm ? n : 0;
     sig_aff = o;  o = align_up(o + nm * sizeof(g2a));
     sig_use = o;  o = align_up(o + nm);
@@ -141,13 +175,10 @@ struct ws_layout {
     msm_cur = o;  o = align_up(o + (msm ? TB_MSM_BUCKETS * 4 : 0));
     msm_idx = o;  o = align_up(o + nm * 8 * 4);
     msm_part = o; o = align_up(o + (msm ? (size_t)TB_MSM_PARTS * sizeof(g2j) : 0));
-    msm_bucket = o; o = align_up(o + (msm ? (size_t)TB_MSM_BUCKETS * sizeof(g2j) : 0));
-    msm_wseg = o; o = align_up(o + (msm ? TB_MSM_WSEGS * sizeof(g2j) : 0));
-    msm_wsum = o; o = align_up(o + (msm ? 8 * sizeof(g2j) : 0));
     mlist = o;    o = align_up(o + (size_t)n * 4);
     mcnt = o;     o = align_up(o + 4);
-    f = o;        o = align_up(o + (size_t)np * sizeof(fp12));
-    gpart = o;    o = align_up(o + (size_t)nb_g2 * sizeof(g2j));
+    lines = o;    o = align_up(o + (size_t)pp.line_pairs() * TB_LINE_BYTES_PER_PAIR);
+    f = o;        o = align_up(o + (size_t)(nf ? nf : 1) * sizeof(fp12));
     fpart = o;    o = align_up(o + (size_t)nb_f * sizeof(fp12));
     fpart2 = o;   o = align_up(o + (size_t)((nb_f + TB_PROD_CHUNK - 1) / TB_PROD_CHUNK) * sizeof(fp12));
     n_bad = o;    o = align_up(o + 4);
@@ -158,42 +189,31 @@ struct ws_layout {
 
 // Launch the partial pipeline for one device.  All pointers in `b` are
 // device pointers.  Writes the 580-byte partial record at `partial_out`.
-// Optionally leaves per-set codes in the workspace (set_code/sig_code).
+// Leaves per-set codes in the workspace (set_code/sig_code).
 // Per-stage timing (optional): ev[2*i] / ev[2*i+1] bracket stage i on the
-// stream that runs it.  Stages: 0 pk decompress, 1 set pk, 2 set sig, 3 set
-// hash, 4 G2 sum, 5 Miller, 6 Fp12 product.
+// stream that runs it.  Stages: 0 pk decompress, 1 set pk (+ -[r] g1), 2
+// signature decode + G2 check, 3 hash, 4 bucket sums (large batches), 5
+// Miller, 6 Fp12 product.
 #define TB_NSTAGE 7
 #define TB_NSTAGE_EV (2 * TB_NSTAGE)
-// Stage order.  The chain  signatures -> G2 sum -> Miller loop of the
-// (-g1, sum r_i sig_i) pair  is latency-bound after its first kernel (one block,
-// then one thread), so:
-//  * large batches (n >= TB_SIG_FIRST_MIN) run k_set_sig alone first; the
-//    G2 sum and the single Miller loop then run on stream b underneath the
-//    hash / key stages and the set pairs' Miller loops, which fill the GPU;
-//  * small batches (GPU mostly idle) run the three per-set stages
-//    concurrently on three streams and use one pair per thread in the Miller
-//    loop (half the latency of the two-pair accumulator).
-// TBLS_SERIAL=1 (or `serial`) runs everything on the caller's stream, for
-// exclusive per-stage timings.
-#define TB_SIG_FIRST_MIN TB_MSM_MIN
-#define TB_MILLER1_MAX 4096u
-// up to this many sets, one pair per 64-lane workgroup (k_miller_wave);
-// TBLS_MILLER_WAVE_MAX overrides (tuning)
-static uint32_t miller_wave_max() {
-  static const uint32_t v = getenv("TBLS_MILLER_WAVE_MAX") ? (uint32_t)atoi(getenv("TBLS_MILLER_WAVE_MAX")) : 1024u;
-  return v;
-}
+// Streams: keys on aux[0], signatures (+ bucket sums) on aux[1], hash_to_G2
+// on the caller's stream; all three join before the Miller loops.  At large n
+// every stage fills the GPU; at small n (config 1) the three per-set chains
+// run side by side.  TBLS_SERIAL=1 (or `serial`) runs everything on the
+// caller's stream, for exclusive per-stage timings.
+
 // Per-set aggregate key and P_i = [r_i] apk_i on stream s.  Single-key sets:
 // one thread per set (k_set_pk).  When some set has several keys (n_entries >
 // n: configs 2/3), those sets go to the wave-level aggregation k_set_pk_wave
 // through a device-built work list (mlist / mcnt: n + 1 words of workspace).
+// P2 (nullable): signature-pair points -[r_i] g1 (comb: the device's table).
 void launch_set_pk(hipStream_t s, uint32_t n, uint32_t n_entries, const uint32_t* pk_off, const g1a* aff, const uint8_t* code,
                    const uint64_t* rand, g1a* P, uint8_t* set_code, uint32_t* n_bad, const uint32_t* key_idx, uint32_t tab_n,
-                   uint32_t* mlist, uint32_t* mcnt) {
+                   uint32_t* mlist, uint32_t* mcnt, g1a* P2, const g1a* comb) {
   if (!n) return;
   const dim3 blk(TB_BLOCK), g((n + TB_BLOCK - 1) / TB_BLOCK);
   const uint32_t multi = n_entries > n ? 1u : 0u;
-  hipLaunchKernelGGL(k_set_pk, g, blk, 0, s, pk_off, aff, code, rand, n, P, set_code, n_bad, key_idx, tab_n, multi);
+  hipLaunchKernelGGL(k_set_pk, g, blk, 0, s, pk_off, aff, code, rand, n, P, set_code, n_bad, key_idx, tab_n, multi, P2, comb);
   if (!multi) return;
   (void)hipMemsetAsync(mcnt, 0, 4, s);
   hipLaunchKernelGGL(k_multi_list, g, blk, 0, s, pk_off, n, mlist, mcnt);
@@ -202,121 +222,114 @@ void launch_set_pk(hipStream_t s, uint32_t n, uint32_t n_entries, const uint32_t
 }
 
 int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* partial_out, ws_layout& L,
-                   const uint8_t* dst, uint32_t dlen, bool keep_codes, hipEvent_t* ev = nullptr, bool serial_req = false,
+                   const uint8_t* dst, uint32_t dlen, hipEvent_t* ev = nullptr, bool serial_req = false,
                    const uint32_t* key_idx = nullptr) {
   const uint32_t n = b.n;
   const bool use_tab = key_idx != nullptr;  // keys = indices into the resident table: no decompression
   const uint32_t K = use_tab ? 0 : b.n_keys;
-  L = ws_layout(n, K);
+  const pair_plan pp(n);
+  L = ws_layout(pp, K);
   HIPCHK(ws_acquire(c, s));
   if (L.total > c.ws.cap) {  // growing frees the old buffer: drain its users first
     HIPCHK(hipStreamSynchronize(s));
     if (c.ws.ensure(L.total)) return TBLS_DEVICE_ERROR;
   }
   uint8_t* w = c.ws.as<uint8_t>();
-  (void)keep_codes;
   static const bool serial_env = getenv("TBLS_SERIAL") && getenv("TBLS_SERIAL")[0] == '1';
   const bool serial = serial_env || serial_req;
-  const bool sig_first = !serial && n >= TB_SIG_FIRST_MIN;
   hipStream_t sa = serial ? s : c.aux[0], sb = serial ? s : c.aux[1];
-  // the hash stage runs on the caller's stream when signatures go first
-  hipStream_t sh = sig_first ? s : sa, ss = sig_first ? s : sb;
 #define TB_EV(i, st) \
   if (ev) HIPCHK(hipEventRecord(ev[i], st))
   const dim3 blk(TB_BLOCK);
   const dim3 g((n + TB_BLOCK - 1) / TB_BLOCK);
-  const bool one_pair = n <= TB_MILLER1_MAX;
-  const uint32_t nthr = one_pair ? n : (n + 1) / 2;  // Miller values f[0..nthr-1]; f[nthr] = the g1 pair
-  HIPCHK(hipMemsetAsync(w + L.set_code, 0, n ? n : 1, s));
+  g1a* P = (g1a*)(w + L.P);
+  g2a* Q = (g2a*)(w + L.Q);
+  uint8_t* skip = w + L.skip;
+  HIPCHK(hipMemsetAsync(w + L.set_code, 0, 2 * align_up(pp.n_pairs), s));  // set_code and sig_code (adjacent)
   HIPCHK(hipMemsetAsync(w + L.n_bad, 0, 4, s));
-  if (!sig_first || (L.msm && !serial)) {
+  if (!serial) {
     HIPCHK(hipEventRecord(c.e_fork, s));
-    if (!sig_first) HIPCHK(hipStreamWaitEvent(sa, c.e_fork, 0));
+    HIPCHK(hipStreamWaitEvent(sa, c.e_fork, 0));
     HIPCHK(hipStreamWaitEvent(sb, c.e_fork, 0));
   }
-  // MSM bucket sort (randomizers only): on stream b, concurrent with the signature check
+  // --- stream b: signatures, then (large batches) the bucket sums -----------
   uint32_t* msm_cnt = (uint32_t*)(w + L.msm_cnt);
   uint32_t* msm_off = (uint32_t*)(w + L.msm_off);
   uint32_t* msm_idx = (uint32_t*)(w + L.msm_idx);
-  if (L.msm) {
+  if (pp.msm) {  // bucket sort by randomizer byte (randomizers only)
     uint32_t* cur = (uint32_t*)(w + L.msm_cur);
     HIPCHK(hipMemsetAsync(msm_cnt, 0, TB_MSM_BUCKETS * 4, sb));
     hipLaunchKernelGGL(k_msm_hist, g, blk, 0, sb, b.rand, n, msm_cnt);
     hipLaunchKernelGGL(k_msm_scan, dim3(1), dim3(256), 0, sb, (const uint32_t*)msm_cnt, msm_off, cur);
     hipLaunchKernelGGL(k_msm_scatter, g, blk, 0, sb, b.rand, n, cur, msm_idx);
   }
-  // signatures: decompress, G2 subgroup check (+ [r]sig per set without the MSM)
-  TB_EV(4, ss);
-  if (L.msm)
-    hipLaunchKernelGGL(k_sig_check, g, blk, 0, ss, b.sigs, n, (g2a*)(w + L.sig_aff), w + L.sig_use, w + L.sig_code,
-                       (uint32_t*)(w + L.n_bad));
-  else if (n)
-    hipLaunchKernelGGL(k_set_sig, g, blk, 0, ss, b.sigs, b.rand, n, (g2j*)(w + L.rsig), w + L.sig_code, (uint32_t*)(w + L.n_bad));
-  TB_EV(5, ss);
-  HIPCHK(hipEventRecord(c.e_sig, ss));
-  if (sig_first) {
-    HIPCHK(hipStreamWaitEvent(sa, c.e_sig, 0));
-    HIPCHK(hipStreamWaitEvent(sb, c.e_sig, 0));
+  TB_EV(4, sb);
+  if (n) {
+    if (pp.msm)
+      hipLaunchKernelGGL(k_sig_check, g, blk, 0, sb, b.sigs, n, (g2a*)(w + L.sig_aff), w + L.sig_use, w + L.sig_code,
+                         (uint32_t*)(w + L.n_bad), 0u);
+    else  // the set's signature pair: Q[n + i] = sig_i, skip[n + i] = infinite / invalid
+      hipLaunchKernelGGL(k_sig_check, g, blk, 0, sb, b.sigs, n, Q + n, skip + n, w + L.sig_code, (uint32_t*)(w + L.n_bad), 1u);
   }
-  // stream b: the G2 sum, then the Miller loop of the (-g1, S) pair
+  TB_EV(5, sb);
   TB_EV(8, sb);
-  if (L.msm) {
+  if (pp.msm) {
     hipLaunchKernelGGL(k_msm_bucket, dim3(TB_MSM_PARTS / TB_BLOCK), blk, 0, sb, (const g2a*)(w + L.sig_aff), (const uint8_t*)(w + L.sig_use),
                        (const uint32_t*)msm_off, (const uint32_t*)msm_idx, (g2j*)(w + L.msm_part));
-    hipLaunchKernelGGL(k_msm_bsum, dim3(TB_MSM_BUCKETS / TB_BLOCK), blk, 0, sb, (const g2j*)(w + L.msm_part), (g2j*)(w + L.msm_bucket));
-    hipLaunchKernelGGL(k_msm_window, dim3(TB_MSM_WSEGS / TB_BLOCK), blk, 0, sb, (const g2j*)(w + L.msm_bucket), (g2j*)(w + L.msm_wseg));
-    hipLaunchKernelGGL(k_msm_final, dim3(1), dim3(64), 0, sb, (const g2j*)(w + L.msm_wseg), (g2j*)(w + L.msm_wsum), n, (g1a*)(w + L.P),
-                       (g2a*)(w + L.Q), w + L.skip);
-  } else {
-  if (n)
-    hipLaunchKernelGGL(k_g2_sum_partial, dim3(L.nb_g2), blk, 0, sb, (const g2j*)(w + L.rsig), n, (g2j*)(w + L.gpart));
-  else
-    HIPCHK(hipMemsetAsync(w + L.gpart, 0, sizeof(g2j), sb));  // z = 0 -> infinity
-  hipLaunchKernelGGL(k_g2_sum_final, dim3(1), blk, 0, sb, (const g2j*)(w + L.gpart), L.nb_g2, n, (g1a*)(w + L.P), (g2a*)(w + L.Q),
-                     w + L.skip);
+    hipLaunchKernelGGL(k_msm_bucket_pairs, dim3(TB_MSM_BPAIRS), dim3(64), 0, sb, (const g2j*)(w + L.msm_part), c.comb.as<const g1a>(),
+                       P + n, Q + n, skip + n);
   }
   TB_EV(9, sb);
-  hipLaunchKernelGGL(k_miller_one_wave, dim3(1), dim3(64), 0, sb, (const g1a*)(w + L.P), (const g2a*)(w + L.Q), w + L.skip, n,
-                     (fp12*)(w + L.f) + nthr);
   HIPCHK(hipEventRecord(c.e_join[1], sb));
-  // hash_to_G2 per set
-  TB_EV(6, sh);
-  if (n) hipLaunchKernelGGL(k_set_hash, g, blk, 0, sh, b.msgs, b.msg_off, dst, dlen, n, (g2a*)(w + L.Q), w + L.skip);
-  TB_EV(7, sh);
-  // public keys (stream a when signatures go first, else the caller's stream)
-  hipStream_t sk = sig_first ? sa : s;
-  TB_EV(0, sk);
-  if (K) hipLaunchKernelGGL(k_pk_decompress, dim3((K + TB_BLOCK - 1) / TB_BLOCK), blk, 0, sk, b.pks, K, (g1a*)(w + L.pk_aff), w + L.pk_code);
-  TB_EV(1, sk);
-  TB_EV(2, sk);
-  launch_set_pk(sk, n, b.n_keys, b.pk_off, use_tab ? c.tab_aff.as<const g1a>() : (const g1a*)(w + L.pk_aff),
-                use_tab ? c.tab_code.as<const uint8_t>() : (const uint8_t*)(w + L.pk_code), b.rand, (g1a*)(w + L.P), w + L.set_code,
-                (uint32_t*)(w + L.n_bad), key_idx, use_tab ? c.tab_n : 0u, (uint32_t*)(w + L.mlist), (uint32_t*)(w + L.mcnt));
-  TB_EV(3, sk);
-  HIPCHK(hipEventRecord(c.e_join[0], sig_first ? sa : sh));
+  // --- stream a: public keys, [r] apk (+ -[r] g1 for the signature pairs) -----
+  TB_EV(0, sa);
+  if (K) hipLaunchKernelGGL(k_pk_decompress, dim3((K + TB_BLOCK - 1) / TB_BLOCK), blk, 0, sa, b.pks, K, (g1a*)(w + L.pk_aff), w + L.pk_code);
+  TB_EV(1, sa);
+  TB_EV(2, sa);
+  launch_set_pk(sa, n, b.n_keys, b.pk_off, use_tab ? c.tab_aff.as<const g1a>() : (const g1a*)(w + L.pk_aff),
+                use_tab ? c.tab_code.as<const uint8_t>() : (const uint8_t*)(w + L.pk_code), b.rand, P, w + L.set_code,
+                (uint32_t*)(w + L.n_bad), key_idx, use_tab ? c.tab_n : 0u, (uint32_t*)(w + L.mlist), (uint32_t*)(w + L.mcnt),
+                pp.msm ? nullptr : P + n, c.comb.as<const g1a>());
+  TB_EV(3, sa);
+  HIPCHK(hipEventRecord(c.e_join[0], sa));
+  // --- caller's stream: hash_to_G2 per set ------------------------------------
+  TB_EV(6, s);
+  if (n) hipLaunchKernelGGL(k_set_hash, g, blk, 0, s, b.msgs, b.msg_off, dst, dlen, n, Q, skip);
+  TB_EV(7, s);
   HIPCHK(hipStreamWaitEvent(s, c.e_join[0], 0));
-  if (!sig_first) HIPCHK(hipStreamWaitEvent(s, c.e_sig, 0));
-  // Miller loops of the set pairs (invalid sets contribute 1)
+  HIPCHK(hipStreamWaitEvent(s, c.e_join[1], 0));
+  // --- Miller loops of all pairs (pairs of invalid sets contribute 1) ---------
+  const uint32_t np = pp.n_pairs, nf = pp.n_f();
   TB_EV(10, s);
-  if (nthr) {
-    const dim3 gm((nthr + TB_BLOCK - 1) / TB_BLOCK);
-    if (n <= miller_wave_max())
-      hipLaunchKernelGGL(k_miller_wave, dim3(n), dim3(64), 0, s, (const g1a*)(w + L.P), (const g2a*)(w + L.Q), w + L.skip,
-                         w + L.set_code, w + L.sig_code, n, (fp12*)(w + L.f));
-    else if (one_pair)
-      hipLaunchKernelGGL(k_miller1, gm, blk, 0, s, (const g1a*)(w + L.P), (const g2a*)(w + L.Q), w + L.skip, w + L.set_code,
-                         w + L.sig_code, n, (fp12*)(w + L.f));
-    else
-      hipLaunchKernelGGL(k_miller2, gm, blk, 0, s, (const g1a*)(w + L.P), (const g2a*)(w + L.Q), w + L.skip, w + L.set_code,
-                         w + L.sig_code, n, (fp12*)(w + L.f));
+  if (np) {
+    const uint8_t* ca = w + L.set_code;
+    const uint8_t* cb = w + L.sig_code;
+    fp12* f = (fp12*)(w + L.f);
+    if (pp.wave)
+      hipLaunchKernelGGL(k_miller_wave, dim3(np), dim3(64), 0, s, (const g1a*)P, (const g2a*)Q, (const uint8_t*)skip, ca, cb, np, f);
+    else if (pp.split) {
+      uint4* lines = (uint4*)(w + L.lines);
+      for (uint32_t lo = 0; lo < np; lo += TB_LINE_CHUNK) {
+        const uint32_t m = std::min(TB_LINE_CHUNK, np - lo), mt = (m + pp.per - 1) / pp.per;
+        hipLaunchKernelGGL(k_miller_lines, dim3((m + TB_BLOCK - 1) / TB_BLOCK), blk, 0, s, (const g1a*)P + lo, (const g2a*)Q + lo,
+                           (const uint8_t*)skip + lo, ca + lo, cb + lo, m, lines);
+        hipLaunchKernelGGL(pp.per == 2 ? k_miller_acc2 : k_miller_acc1, dim3((mt + TB_BLOCK - 1) / TB_BLOCK), blk, 0, s,
+                           (const uint4*)lines, (const uint8_t*)skip + lo, ca + lo, cb + lo, m, f + lo / pp.per);
+      }
+    } else
+      hipLaunchKernelGGL(pp.per == 1 ? k_miller1 : k_miller2, dim3((nf + TB_BLOCK - 1) / TB_BLOCK), blk, 0, s, (const g1a*)P,
+                         (const g2a*)Q, (const uint8_t*)skip, ca, cb, np, f);
   }
   TB_EV(11, s);
-  HIPCHK(hipStreamWaitEvent(s, c.e_join[1], 0));
   TB_EV(12, s);
+  if (nf == 0) {  // no pairs at all: the partial product is 1
+    HIPCHK(hipMemsetAsync(w + L.f, 0, sizeof(fp12), s));
+    hipLaunchKernelGGL(k_fp12_one, dim3(1), dim3(64), 0, s, (fp12*)(w + L.f));
+  }
   {
     // levels of chunked wave products: f -> fpart -> fpart2 -> fpart ... -> partial_out
     const fp12* src = (const fp12*)(w + L.f);
-    uint32_t cnt = nthr + 1;
+    uint32_t cnt = nf ? nf : 1;
     int lvl = 0;
     for (;;) {
       const uint32_t nout = (cnt + TB_PROD_CHUNK - 1) / TB_PROD_CHUNK;
@@ -473,9 +486,9 @@ int run_shard(int d, const SET* sets, size_t lo, size_t hi, const uint64_t* rand
   b.rand = (const uint64_t*)(di + p.off_rand);
   b.n = p.n;
   uint8_t* dpart = di + align_up(p.total);
-  ws_layout L(0, 0);
+  ws_layout L;
   HIPCHK(hipEventRecord(e0, s));
-  int rc = launch_partial(*c, b, s, dpart, L, di + p.off_dst, dlen, codes_host != nullptr, nullptr, false,
+  int rc = launch_partial(*c, b, s, dpart, L, di + p.off_dst, dlen, nullptr, false,
                           idx_mode ? (const uint32_t*)(di + p.off_pks) : nullptr);
   if (rc) return rc;
   HIPCHK(hipEventRecord(e1, s));
@@ -609,7 +622,12 @@ extern "C" int tbls_init(int n_devices, uint32_t flags) {
         hipEventCreateWithFlags(&c->e_join[1], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->e_sig, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->e_ws, hipEventDisableTiming) != hipSuccess || hipEventCreate(&c->e_t0) != hipSuccess ||
-        hipEventCreate(&c->e_t1) != hipSuccess) {
+        hipEventCreate(&c->e_t1) != hipSuccess || c->comb.ensure(TB_MSM_BUCKETS * sizeof(g1a))) {
+      delete c;
+      break;
+    }
+    hipLaunchKernelGGL(k_g1_comb_init, dim3(TB_MSM_BUCKETS / TB_BLOCK), dim3(TB_BLOCK), 0, c->stream, c->comb.as<g1a>());
+    if (hipGetLastError() != hipSuccess || hipStreamSynchronize(c->stream) != hipSuccess) {
       delete c;
       break;
     }
@@ -628,6 +646,7 @@ extern "C" void tbls_shutdown(void) {
     if (c->fin.p) (void)hipFree(c->fin.p);
     if (c->dstb.p) (void)hipFree(c->dstb.p);
     if (c->recs.p) (void)hipFree(c->recs.p);
+    if (c->comb.p) (void)hipFree(c->comb.p);
     if (c->tab_aff.p) (void)hipFree(c->tab_aff.p);
     if (c->tab_code.p) (void)hipFree(c->tab_code.p);
     if (c->hin.p) (void)hipHostFree(c->hin.p);
@@ -773,14 +792,6 @@ extern "C" int tbls_verify(const uint8_t pk[48], const uint8_t* msg, size_t len,
   return TBLS_SUCCESS;
 }
 
-// k_each.hip (declared here rather than in tb_kdecl.h)
-extern "C" __global__ void k_each_miller(const g1a* __restrict__ P, const g2a* __restrict__ Q, const uint8_t* __restrict__ skip, const uint8_t* __restrict__ set_code, const g2a* __restrict__ sig_aff, const uint8_t* __restrict__ sig_use, const uint8_t* __restrict__ sig_code, uint32_t n, fp12* __restrict__ f, uint8_t* __restrict__ use);
-extern "C" __global__ void k_each_final_wave(const fp12* __restrict__ f, const uint8_t* __restrict__ use, uint8_t* __restrict__ ok);
-extern "C" __global__ void k_each_miller_r(const g1a* __restrict__ P, const g2a* __restrict__ Q, const uint8_t* __restrict__ skip, const uint8_t* __restrict__ set_code, const g2j* __restrict__ rsig, const uint8_t* __restrict__ sig_code, uint32_t n, fp12* __restrict__ f, uint8_t* __restrict__ use);
-extern "C" __global__ void k_each_group_wave(const fp12* __restrict__ f, uint32_t n, uint32_t gsz, uint8_t* __restrict__ gok);
-extern "C" __global__ void k_each_member_wave(const fp12* __restrict__ f, const uint8_t* __restrict__ use, const uint32_t* __restrict__ idx, uint8_t* __restrict__ ok);
-#define TB_EACH_GROUP 64u  // sets per group-tested final exponentiation
-
 // Per-set fastAggregateVerify verdicts for sets[lo, hi) on device d in one
 // pass (k_each.hip): shared per-set stages with r = 1, then one thread per set
 // for its two-pair Miller loop and final exponentiation.
@@ -791,13 +802,7 @@ static int run_each(int d, const tbls_set* sets, size_t lo, size_t hi, uint8_t* 
   HIPCHK(hipSetDevice(c->dev));
   packed p = pack_layout(sets, lo, hi, 43);
   if (c->hin.ensure(p.total + 256) || c->in.ensure(p.total + 256)) return TBLS_DEVICE_ERROR;
-  static const bool group = getenv("TBLS_EACH_GROUP") && getenv("TBLS_EACH_GROUP")[0] == '1';
-  std::vector<uint64_t> rnd;
-  if (group) {  // per-call randomizers in [1, 2^64) from the OS entropy source
-    rnd.resize(hi);
-    if (fill_random(rnd.data() + lo, hi - lo)) return TBLS_DEVICE_ERROR;
-  }
-  pack_fill(c->hin.b(), p, sets, lo, group ? rnd.data() : nullptr, ETH2_DST, 43);  // else r = 1 for every set
+  pack_fill(c->hin.b(), p, sets, lo, nullptr, ETH2_DST, 43);  // r = 1 for every set
   hipStream_t s = c->stream;
   HIPCHK(ws_acquire(*c, s));
   HIPCHK(hipStreamSynchronize(s));  // ws may be reallocated below
@@ -816,12 +821,6 @@ static int run_each(int d, const tbls_set* sets, size_t lo, size_t hi, uint8_t* 
   const size_t sig_use = o;  o = align_up(o + n);
   const size_t okd = o;      o = align_up(o + n);
   const size_t n_bad = o;    o = align_up(o + 4);
-  const size_t fv = o;       o = align_up(o + (size_t)n * sizeof(fp12));
-  const size_t use = o;      o = align_up(o + n);
-  const size_t rsig = o;     o = align_up(o + (group ? (size_t)n * sizeof(g2j) : 0));
-  const uint32_t ngrp = (n + TB_EACH_GROUP - 1) / TB_EACH_GROUP;
-  const size_t gok = o;      o = align_up(o + ngrp);
-  const size_t midx = o;     o = align_up(o + (group ? (size_t)n * 4 : 0));
   const size_t mlist = o;    o = align_up(o + (size_t)n * 4 + 4);
   if (c->ws.ensure(o)) return TBLS_DEVICE_ERROR;
   uint8_t* w = c->ws.as<uint8_t>();
@@ -833,60 +832,13 @@ static int run_each(int d, const tbls_set* sets, size_t lo, size_t hi, uint8_t* 
                        w + pk_code);
   launch_set_pk(s, n, K, (const uint32_t*)(di + p.off_pkoff), (const g1a*)(w + pk_aff), (const uint8_t*)(w + pk_code),
                 (const uint64_t*)(di + p.off_rand), (g1a*)(w + P), w + set_code, (uint32_t*)(w + n_bad), nullptr, 0u,
-                (uint32_t*)(w + mlist), (uint32_t*)(w + mlist) + n);
-  if (group)
-    hipLaunchKernelGGL(k_set_sig, g, blk, 0, s, di + p.off_sigs, (const uint64_t*)(di + p.off_rand), n, (g2j*)(w + rsig), w + sig_code,
-                       (uint32_t*)(w + n_bad));
-  else
-    hipLaunchKernelGGL(k_sig_check, g, blk, 0, s, di + p.off_sigs, n, (g2a*)(w + sig_aff), w + sig_use, w + sig_code, (uint32_t*)(w + n_bad));
+                (uint32_t*)(w + mlist), (uint32_t*)(w + mlist) + n, nullptr, nullptr);
+  hipLaunchKernelGGL(k_sig_check, g, blk, 0, s, di + p.off_sigs, n, (g2a*)(w + sig_aff), w + sig_use, w + sig_code, (uint32_t*)(w + n_bad), 0u);
   hipLaunchKernelGGL(k_set_hash, g, blk, 0, s, di + p.off_msgs, (const uint32_t*)(di + p.off_msgoff), di + p.off_dst, 43u, n, (g2a*)(w + Q),
                      w + skip);
-  if (group) {
-    // randomized Miller values; one final exponentiation per group of sets, then
-    // one per member of each failing group (k_each.hip)
-    hipLaunchKernelGGL(k_each_miller_r, g, blk, 0, s, (const g1a*)(w + P), (const g2a*)(w + Q), (const uint8_t*)(w + skip),
-                       (const uint8_t*)(w + set_code), (const g2j*)(w + rsig), (const uint8_t*)(w + sig_code), n, (fp12*)(w + fv), w + use);
-    hipLaunchKernelGGL(k_each_group_wave, dim3(ngrp), dim3(64), 0, s, (const fp12*)(w + fv), n, TB_EACH_GROUP, w + gok);
-    HIPCHK(hipGetLastError());
-    if (c->hout.ensure(2 * (size_t)n + ngrp)) return TBLS_DEVICE_ERROR;
-    uint8_t* hu = c->hout.b();
-    HIPCHK(hipMemcpyAsync(hu, w + use, n, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(hu + n, w + gok, ngrp, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
-    std::vector<uint32_t> members;
-    for (uint32_t i = 0; i < n; i++) {
-      if (hu[n + i / TB_EACH_GROUP])
-        ok_host[i] = hu[i];  // group passed: every finite member is valid
-      else
-        members.push_back(i);
-    }
-    if (!members.empty()) {
-      const uint32_t m = (uint32_t)members.size();
-      HIPCHK(hipMemcpyAsync(w + midx, members.data(), 4 * (size_t)m, hipMemcpyHostToDevice, s));
-      hipLaunchKernelGGL(k_each_member_wave, dim3(m), dim3(64), 0, s, (const fp12*)(w + fv), (const uint8_t*)(w + use),
-                         (const uint32_t*)(w + midx), w + okd);
-      HIPCHK(hipGetLastError());
-      HIPCHK(hipMemcpyAsync(hu + n + ngrp, w + okd, n, hipMemcpyDeviceToHost, s));
-      HIPCHK(hipStreamSynchronize(s));
-      for (uint32_t i : members) ok_host[i] = hu[n + ngrp + i];
-    }
-    HIPCHK(ws_release(*c, s));
-    return TBLS_SUCCESS;
-  }
-  // A/B (profiles/r01_bench_each_*): the wave final exponentiation runs its
-  // Fp12 inversion serially on lane 0, which at one wave per set costs more
-  // than it saves; TBLS_EACH_WAVE=1 selects it.
-  static const bool wave = getenv("TBLS_EACH_WAVE") && getenv("TBLS_EACH_WAVE")[0] == '1';
-  if (!wave) {
-    hipLaunchKernelGGL(k_verify_each, g, blk, 0, s, (const g1a*)(w + P), (const g2a*)(w + Q), (const uint8_t*)(w + skip),
-                       (const uint8_t*)(w + set_code), (const g2a*)(w + sig_aff), (const uint8_t*)(w + sig_use),
-                       (const uint8_t*)(w + sig_code), n, w + okd);
-  } else {
-    hipLaunchKernelGGL(k_each_miller, g, blk, 0, s, (const g1a*)(w + P), (const g2a*)(w + Q), (const uint8_t*)(w + skip),
-                       (const uint8_t*)(w + set_code), (const g2a*)(w + sig_aff), (const uint8_t*)(w + sig_use),
-                       (const uint8_t*)(w + sig_code), n, (fp12*)(w + fv), w + use);
-    hipLaunchKernelGGL(k_each_final_wave, dim3(n), dim3(64), 0, s, (const fp12*)(w + fv), (const uint8_t*)(w + use), w + okd);
-  }
+  hipLaunchKernelGGL(k_verify_each, g, blk, 0, s, (const g1a*)(w + P), (const g2a*)(w + Q), (const uint8_t*)(w + skip),
+                     (const uint8_t*)(w + set_code), (const g2a*)(w + sig_aff), (const uint8_t*)(w + sig_use),
+                     (const uint8_t*)(w + sig_code), n, w + okd);
   HIPCHK(hipGetLastError());
   if (c->hout.ensure(n)) return TBLS_DEVICE_ERROR;
   HIPCHK(hipMemcpyAsync(c->hout.p, w + okd, n, hipMemcpyDeviceToHost, s));
@@ -1173,8 +1125,8 @@ extern "C" int tbls_dev_batch_partial(int device, const tbls_dev_batch* b, void*
     if (c->dstb.ensure(256)) return TBLS_DEVICE_ERROR;
     HIPCHK(hipMemcpy(c->dstb.p, ETH2_DST, 43, hipMemcpyHostToDevice));
   }
-  ws_layout L(0, 0);
-  return launch_partial(*c, *b, s, partial_out, L, c->dstb.as<uint8_t>(), 43, false);
+  ws_layout L;
+  return launch_partial(*c, *b, s, partial_out, L, c->dstb.as<uint8_t>(), 43);
 }
 
 extern "C" int tbls_dev_batch_partial_idx(int device, const tbls_dev_batch* b, const uint32_t* key_idx, void* stream, void* partial_out) {
@@ -1189,8 +1141,8 @@ extern "C" int tbls_dev_batch_partial_idx(int device, const tbls_dev_batch* b, c
     if (c->dstb.ensure(256)) return TBLS_DEVICE_ERROR;
     HIPCHK(hipMemcpy(c->dstb.p, ETH2_DST, 43, hipMemcpyHostToDevice));
   }
-  ws_layout L(0, 0);
-  return launch_partial(*c, *b, s, partial_out, L, c->dstb.as<uint8_t>(), 43, false, nullptr, false, key_idx);
+  ws_layout L;
+  return launch_partial(*c, *b, s, partial_out, L, c->dstb.as<uint8_t>(), 43, nullptr, false, key_idx);
 }
 
 static int partial_timed(int device, const tbls_dev_batch* b, void* stream, void* partial_out, float* stage_ms, bool serial) {
@@ -1206,8 +1158,8 @@ static int partial_timed(int device, const tbls_dev_batch* b, void* stream, void
   }
   hipEvent_t ev[TB_NSTAGE_EV];
   for (int i = 0; i < TB_NSTAGE_EV; i++) HIPCHK(hipEventCreate(&ev[i]));
-  ws_layout L(0, 0);
-  int rc = launch_partial(*c, *b, s, partial_out, L, c->dstb.as<uint8_t>(), 43, false, ev, serial);
+  ws_layout L;
+  int rc = launch_partial(*c, *b, s, partial_out, L, c->dstb.as<uint8_t>(), 43, ev, serial);
   if (!rc) {
     HIPCHK(hipEventSynchronize(ev[TB_NSTAGE_EV - 1]));
     static const int order[TB_NSTAGE] = {0, 1, 2, 3, 4, 5, 6};  // pk, set_pk, set_sig, set_hash, g2_sum, miller, prod

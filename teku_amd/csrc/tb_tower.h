@@ -39,16 +39,86 @@ TB_HD TB_INLINE fp2 fp2_mul_fp(const fp2& a, const fp& b) { return {fp_mul(a.c0,
 TB_HD TB_INLINE fp2 fp2_mul3(const fp2& a) { return {fp_mul3(a.c0), fp_mul3(a.c1)}; }
 TB_HD TB_INLINE fp2 fp2_half(const fp2& a) { return {fp_half(a.c0), fp_half(a.c1)}; }
 
+// Karatsuba Fp2 product with lazy reduction.  The three half products a0 b0,
+// a1 b1 and (a0 + a1)(b0 + b1) are scanned column by column on 14 x 29-bit
+// limbs and only the two results are Montgomery-reduced:
+//   re = a0 b0 - a1 b1 + p 2^388      (the offset keeps it non-negative)
+//   im = (a0 + a1)(b0 + b1) - a0 b0 - a1 b1
+// so a product costs 3 x 196 + 2 x 196 = 980 v_mad_u64_u32 instead of the
+// 3 x 392 of three Montgomery products.  Per column five independent
+// accumulator chains (the two pure products, the Karatsuba product plus im's
+// reduction, re's reduction plus offset) give the multiplier its ILP.
+// Bounds: coordinates < 2p (weakly reduced; the sums a0 + a1 < 4p < 2^383 are
+// operands too, so every operand is < 2^384); re < 2^769.4,
+// im < 2^769, so both outputs are < 2p; mid-scan column values stay inside
+// +-2^63 (signed, arithmetic carries).
+TB_HD TB_INLINE fp2 fp2_mul_lazy(const fp2& a, const fp2& b) {
+  uint32_t A0[14], A1[14], AS[14], B0[14], B1[14], BS[14];
+  to29(A0, a.c0);
+  to29(A1, a.c1);
+  to29(AS, fp_add_nr(a.c0, a.c1));
+  to29(B0, b.c0);
+  to29(B1, b.c1);
+  to29(BS, fp_add_nr(b.c0, b.c1));
+  uint32_t m0[14], m1[14], r0[14], r1[14];
+  int64_t k0 = 0, k1 = 0;  // carries into the column (signed)
+  TB_UNROLL for (int k = 0; k < 27; k++) {
+    const int lo = k < 14 ? 0 : k - 13;
+    const int hi = k < 14 ? k : 13;
+    uint64_t c0 = 0, c1 = 0, x0 = (uint64_t)k0 + (k >= 13 ? OFF29[k - 13] : 0u), x2 = (uint64_t)k1;
+    TB_UNROLL for (int i = lo; i <= hi; i++) {
+      mad29(c0, A0[i], B0[k - i]);
+      mad29(c1, A1[i], B1[k - i]);
+      mad29(x2, AS[i], BS[k - i]);
+    }
+    const int mhi = k < 14 ? k - 1 : 13;  // m_k is formed at the end of column k
+    TB_UNROLL for (int i = lo; i <= mhi; i++) {
+      mad29(x0, m0[i], P29[k - i]);
+      mad29(x2, m1[i], P29[k - i]);
+    }
+    uint64_t t0 = x0 + c0 - c1, t1 = x2 - c0 - c1;
+    if (k < 14) {
+      m0[k] = ((uint32_t)t0 * N0_29) & M29;
+      m1[k] = ((uint32_t)t1 * N0_29) & M29;
+      mad29(t0, m0[k], P29[0]);
+      mad29(t1, m1[k], P29[0]);
+    } else {
+      r0[k - 14] = (uint32_t)t0 & M29;
+      r1[k - 14] = (uint32_t)t1 & M29;
+    }
+    k0 = (int64_t)t0 >> 29;
+    k1 = (int64_t)t1 >> 29;
+  }
+  r0[13] = (uint32_t)k0;
+  r1[13] = (uint32_t)k1;
+  fp2 r;
+  from29(r.c0, r0);
+  from29(r.c1, r1);
+  return r;
+}
+
 // Karatsuba: the three Fp products are independent and run interleaved in one call
-TB_HD TB_INLINE fp2 fp2_mul(fp2 a, fp2 b) {
-#if !TB_DEVICE_PASS && defined(TB_COUNT_MULS)
-  tb_mul_count += 3;
-#endif
+TB_HD TB_INLINE fp2 fp2_mul_full(fp2 a, fp2 b) {
   fp t[3];
   const fp x[3] = {a.c0, a.c1, fp_add_nr(a.c0, a.c1)};
   const fp y[3] = {b.c0, b.c1, fp_add_nr(b.c0, b.c1)};
   fp_mul_n<3>(t, x, y);
   return {fp_sub(t[0], t[1]), fp_sub(fp_sub(t[2], t[0]), t[1])};
+}
+
+#ifndef TB_FP2_LAZY
+#define TB_FP2_LAZY 1
+#endif
+TB_HD TB_INLINE fp2 fp2_mul(fp2 a, fp2 b) {
+#if !TB_DEVICE_PASS && defined(TB_COUNT_MULS)
+  tb_mul_count += 3;
+  tb_fp2mul_count += TB_FP2_LAZY ? 1 : 0;
+#endif
+#if TB_FP2_LAZY
+  return fp2_mul_lazy(a, b);
+#else
+  return fp2_mul_full(a, b);
+#endif
 }
 
 TB_HD TB_INLINE fp2 fp2_sqr(fp2 a) {

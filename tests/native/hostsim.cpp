@@ -8,6 +8,7 @@
 extern "C" {
 unsigned long long tb_mul_count = 0;
 unsigned long long tb_sqr_count = 0;
+unsigned long long tb_fp2mul_count = 0;  // lazy-reduction Fp2 products among them (3 M each, 980 v_mad_u64_u32)
 }
 #endif
 #include "tb_testops.h"
@@ -32,6 +33,17 @@ extern "C" unsigned long long tbls_hostsim_mul_count(int reset) {
 #if defined(TB_COUNT_MULS)
   unsigned long long v = tb_mul_count;
   if (reset) tb_mul_count = 0;
+  return v;
+#else
+  (void)reset;
+  return 0;
+#endif
+}
+
+extern "C" unsigned long long tbls_hostsim_fp2mul_count(int reset) {
+#if defined(TB_COUNT_MULS)
+  unsigned long long v = tb_fp2mul_count;
+  if (reset) tb_fp2mul_count = 0;
   return v;
 #else
   (void)reset;

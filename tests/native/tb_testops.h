@@ -41,6 +41,12 @@ enum {
   TOP_STAGE_SET_HASH = 27,
   TOP_G2_JADD = 28,
   TOP_MILLER2 = 30,
+  // raw-limb operands (any 384-bit value, no Montgomery conversion): out =
+  // canonical result || the raw weakly reduced result (checks the < 2p bound)
+  TOP_FP_MUL_RAW = 32,
+  TOP_FP_SQR_RAW = 33,
+  TOP_FP2_MUL_RAW = 34,
+  TOP_FP2_SQR_RAW = 35,
 };
 
 #define TB_TEST_IN 1536
@@ -90,8 +96,32 @@ TB_HD TB_INLINE void tio_put_g2j_aff(uint8_t* b, const g2j& p) {
   }
 }
 
+TB_HD TB_INLINE void tio_put_raw(uint8_t* b, const fp& r) {
+  fp_plain_to_be(fp_canon(r), b);
+  fp_plain_to_be(r, b + 48);
+}
+
 TB_HD TB_NOINLINE void test_op(int op, const uint8_t* in, uint8_t* out) {
   switch (op) {
+    case TOP_FP_MUL_RAW:
+      tio_put_raw(out, fp_mul(fp_plain_from_be(in), fp_plain_from_be(in + 48)));
+      break;
+    case TOP_FP_SQR_RAW:
+      tio_put_raw(out, fp_sqr(fp_plain_from_be(in)));
+      break;
+    case TOP_FP2_MUL_RAW: {
+      const fp2 a = {fp_plain_from_be(in), fp_plain_from_be(in + 48)}, b = {fp_plain_from_be(in + 96), fp_plain_from_be(in + 144)};
+      const fp2 r = fp2_mul(a, b);
+      tio_put_raw(out, r.c0);
+      tio_put_raw(out + 96, r.c1);
+      break;
+    }
+    case TOP_FP2_SQR_RAW: {
+      const fp2 r = fp2_sqr({fp_plain_from_be(in), fp_plain_from_be(in + 48)});
+      tio_put_raw(out, r.c0);
+      tio_put_raw(out + 96, r.c1);
+      break;
+    }
     case TOP_FP_MUL:
       tio_put_fp(out, fp_mul(tio_fp(in), tio_fp(in + 48)));
       break;

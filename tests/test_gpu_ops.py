@@ -145,3 +145,8 @@ def test_miller_wave_matches_single_lane(run):
     wave = [dec_fp12(x) for x in run("MILLER_WAVE", recs)]
     assert wave == single
     assert O.final_exponentiation(wave[1]) == O.pairing(*pairs[1])
+
+
+def test_fp_bounds_of_weak_reduction(run):
+    """The same bound checks on the GPU build (tests/opcodec.check_raw_ops)."""
+    check_raw_ops(run, random.Random(12))

@@ -72,3 +72,9 @@ def test_miller2_shared_accumulator(run):
     rec = enc_fp(P0[0]) + enc_fp(P0[1]) + enc_fp2(Q0[0]) + enc_fp2(Q0[1]) + enc_fp(P1[0]) + enc_fp(P1[1]) + enc_fp2(Q1[0]) + enc_fp2(Q1[1])
     f = dec_fp12(run("MILLER2", [rec])[0])
     assert O.final_exponentiation(f) == O.f12_mul(O.pairing(P0, Q0), O.pairing(P1, Q1))
+
+
+def test_fp_bounds_of_weak_reduction(run):
+    """tb_fp.h / tb_tower.h contract at its bounds (host build of the kernel
+    code): products of operands in [p, 2^384), incl. the lazy Fp2 product."""
+    check_raw_ops(run, random.Random(11))

@@ -16,7 +16,7 @@ from oracle.keys import interop_sk  # noqa: E402
 from tests.opcodec import OPS, enc_fp, enc_fp2, enc_fp12, enc_h2c, run_ops  # noqa: E402
 
 OPS.update(STAGE_PK=24, STAGE_SET_PK=25, STAGE_SET_SIG=26, STAGE_SET_HASH=27, G2_JADD=28)
-MADS_MUL, MADS_SQR = 392, 301  # v_mad_u64_u32 per 14 x 29-bit Montgomery product / squaring (tb_fp.h)
+MADS_MUL, MADS_SQR, MADS_F2 = 392, 301, 980  # v_mad_u64_u32 per 14 x 29-bit Montgomery product / squaring (tb_fp.h), lazy Fp2 product (tb_tower.h)
 
 
 def main():
@@ -29,6 +29,9 @@ def main():
     sqc = lib.tbls_hostsim_sqr_count
     sqc.restype = ctypes.c_ulonglong
     sqc.argtypes = [ctypes.c_int]
+    f2c = lib.tbls_hostsim_fp2mul_count
+    f2c.restype = ctypes.c_ulonglong
+    f2c.argtypes = [ctypes.c_int]
     N = 8
     sks = [interop_sk(i) for i in range(N)]
     pks = [O.sk_to_pk(s) for s in sks]
@@ -36,39 +39,44 @@ def main():
     sigs = [O.sign(s, m) for s, m in zip(sks, msgs)]
     r = 0xF123456789ABCDEF
 
-    sq = {}
+    sq, f2 = {}, {}
 
     def per_unit(op, recs, units_per_rec=1, name=None):
         cnt(1)
         sqc(1)
+        f2c(1)
         run_ops(fn, op, recs)
-        m, s_ = cnt(1) / (len(recs) * units_per_rec), sqc(1) / (len(recs) * units_per_rec)
+        u = len(recs) * units_per_rec
+        m, s_, f_ = cnt(1) / u, sqc(1) / u, f2c(1) / u
         if name:
             sq[name] = s_
+            f2[name] = f_
         return m
 
     res = {}
     res["pk_decompress"] = per_unit("STAGE_PK", pks, name="pk_decompress")
     aff = [O.g1_decompress(p)[1] for p in pks]
     res["set_pk"] = per_unit("STAGE_SET_PK", [enc_fp(a[0]) + enc_fp(a[1]) + r.to_bytes(8, "little") for a in aff], name="set_pk")
-    # small batches (k_set_sig): decode + G2 check + [r] sig per set
-    res["set_sig_rsig"] = per_unit("STAGE_SET_SIG", [s + r.to_bytes(8, "little") for s in sigs], name="set_sig_rsig")
-    # large batches (k_sig_check, the bench config): decode + G2 check only (r = 1: no scalar loop)
+    # k_sig_check: decode + G2 check (r = 1: no scalar loop)
     res["set_sig"] = per_unit("STAGE_SET_SIG", [s + (1).to_bytes(8, "little") for s in sigs], name="set_sig")
     res["set_hash"] = per_unit("STAGE_SET_HASH", [enc_h2c(m) for m in msgs], name="set_hash")
     q = [O.g2_decompress(s)[1] for s in sigs]
-    res["g2_sum_tree"] = per_unit("G2_JADD", [enc_fp2(a[0]) + enc_fp2(a[1]) + enc_fp2(b[0]) + enc_fp2(b[1]) for a, b in zip(q, q[1:] + q[:1])], name="g2_sum_tree")
-    # Large batches: sum r_i sig_i as the bucket MSM of k_sigs.hip (k_msm_*), per set at
-    # n = MSM_N.  Point-operation costs in Fp products from the tb_curve.h formulas
+    # Large batches: the signature side as bucket sums by randomizer byte
+    # (k_msm_bucket: one mixed addition per nonzero byte, 8 windows) and one
+    # extra Miller pair per bucket (k_msm_bucket_pairs: 64-lane tree of 63
+    # additions + affine conversion per bucket), k_sigs.hip, per set at n =
+    # MSM_N.  Point-operation costs in Fp products from the tb_curve.h formulas
     # (Fp2 mul = 3 products, Fp2 sqr = 2): madd-2007-bl 7M+4S = 29, add-2007-bl
-    # 11M+5S = 43, dbl-2009-l 2M+5S = 16.
-    MADD, ADD, DBL, MSM_N = 29, 43, 16, 131072
-    per_set = 8 * 255 / 256 * MADD  # one mixed add per nonzero 8-bit digit
-    reduce_ = 2048 * 15 * ADD  # k_msm_bsum: 16 chunk partials per bucket
-    reduce_ += 512 * (2 * 4 * ADD + 7 * DBL + 4 * ADD)  # k_msm_window: running sums + [lo-1] (8-bit)
-    reduce_ += (64 * 7 + 8 * 7 + 7) * ADD + 56 * DBL  # k_msm_final: segment sums, Horner
-    res["g2_sum"] = per_set + reduce_ / MSM_N
-    sq["g2_sum"] = (8 * 255 / 256 * 4 * 2 + (2048 * 15 + 512 * 12 + 511) * 5 * 2 / MSM_N + (512 * 7 + 56) * 5 * 2 / MSM_N)
+    # 11M+5S = 43; the Fp2 affine conversion (binary-GCD inversion ~65 +
+    # norm/products) ~81.
+    MADD, ADD, AFF2, MSM_N, BPAIRS = 29, 43, 81, 131072, 2040
+    res["g2_sum"] = 8 * 255 / 256 * MADD + BPAIRS * (63 * ADD + AFF2) / MSM_N
+    sq["g2_sum"] = 8 * 255 / 256 * 4 * 2 + BPAIRS * 63 * 5 * 2 / MSM_N
+    f2["g2_sum"] = 8 * 255 / 256 * 7 + BPAIRS * 63 * 11 / MSM_N
+    res["pairs_per_set"] = (MSM_N + BPAIRS) / MSM_N
+    # small batches: the signature pair's G1 point -[r] g1 = sum of <= 8
+    # precomputed multiples (k_set_pk: G1 madd 7M+4S = 11) + affine (~70)
+    res["set_pk_sigpair"] = 8 * 255 / 256 * 11 + 70
     # k_set_pk_wave (configs 2/3): one wave per set of k keys -- (k - 64) mixed
     # additions (a lane's first key costs nothing), a 63-addition LDS tree, then
     # [r] apk on the Jacobian sum and the affine conversion.  G1 costs from the
@@ -86,12 +94,17 @@ def main():
     res["fp12_prod"] = per_unit("FP12_MUL", [enc_fp12(f[0]) + enc_fp12(f[1])], units_per_rec=2, name="fp12_prod")
     res["final_exp"] = per_unit("FINAL_EXP", [enc_fp12(f[0])])
     # per single-signer set (the unit of the headline metric), excluding the once-per-batch final exp
-    res["per_set_total"] = sum(res[k] for k in ["pk_decompress", "set_pk", "set_sig", "set_hash", "g2_sum", "miller", "fp12_prod"])
-    res["note"] = ("set_sig / g2_sum: large-batch path (k_sig_check + bucket MSM, n >= 32768, the bench config); "
-                   "set_sig_rsig / g2_sum_tree: small-batch path (k_set_sig with [r] sig + tree sum)")
+    res["per_set_total"] = sum(res[k] for k in ["pk_decompress", "set_pk", "set_sig", "set_hash", "g2_sum"]) + res["pairs_per_set"] * (
+        res["miller"] + res["fp12_prod"])
+    res["note"] = ("per set of the large-batch path (n = 131072, the bench config): set_sig = decode + G2 check (k_sig_check), "
+                   "g2_sum = bucket sums + bucket pairs' trees/affine; miller per pair (pairs_per_set pairs per set). "
+                   "Small batches add set_pk_sigpair per set and one signature pair per set instead of the bucket pairs.")
     res["sqr_per_unit"] = {k: round(v, 1) for k, v in sq.items()}
-    res["mads_per_unit"] = {k: round((res[k] - sq[k]) * MADS_MUL + sq[k] * MADS_SQR) for k in sq}
-    res["mads_per_mul"], res["mads_per_sqr"] = MADS_MUL, MADS_SQR
+    res["mads_per_unit"] = {
+        k: round((res[k] - sq[k] - 3 * f2.get(k, 0)) * MADS_MUL + sq[k] * MADS_SQR + f2.get(k, 0) * MADS_F2) for k in sq if k in res
+    }
+    res["fp2_products_per_unit"] = {k: round(v, 1) for k, v in f2.items()}
+    res["mads_per_mul"], res["mads_per_sqr"], res["mads_per_fp2_mul"] = MADS_MUL, MADS_SQR, MADS_F2
     out = os.path.join(ROOT, "tools", "mul_counts.json")
     json.dump({k: (round(v, 1) if isinstance(v, float) else v) for k, v in res.items() if k != "note"} | {"note": res["note"]}, open(out, "w"), indent=1)
     print(json.dumps(res, indent=1))
