@@ -25,7 +25,7 @@
 using namespace tb;
 
 // One thread per set: Miller loop and final exponentiation.
-extern "C" __global__ void __launch_bounds__(TB_BLOCK)
+extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_MIN_WAVES)
     k_verify_each(const g1a* __restrict__ P, const g2a* __restrict__ Q, const uint8_t* __restrict__ skip,
                   const uint8_t* __restrict__ set_code, const g2a* __restrict__ sig_aff, const uint8_t* __restrict__ sig_use,
                   const uint8_t* __restrict__ sig_code, uint32_t n, uint8_t* __restrict__ ok) {

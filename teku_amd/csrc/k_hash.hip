@@ -4,7 +4,7 @@
 using namespace tb;
 
 // per set: Q_i = hash_to_G2(m_i) (affine)
-extern "C" __global__ void __launch_bounds__(TB_BLOCK)
+extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_MIN_WAVES)
     k_set_hash(const uint8_t* __restrict__ msgs, const uint32_t* __restrict__ msg_off, const uint8_t* __restrict__ dst,
                uint32_t dlen, uint32_t n, g2a* __restrict__ Q, uint8_t* __restrict__ skip) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -21,7 +21,7 @@ extern "C" __global__ void __launch_bounds__(TB_BLOCK)
 }
 
 // per item: compressed hash_to_G2 of message i
-extern "C" __global__ void __launch_bounds__(TB_BLOCK)
+extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_MIN_WAVES)
     k_hash_to_g2(const uint8_t* __restrict__ msgs, const uint32_t* __restrict__ msg_off, const uint8_t* __restrict__ dst,
                  uint32_t dlen, uint32_t n, uint8_t* __restrict__ out) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -35,7 +35,7 @@ extern "C" __global__ void __launch_bounds__(TB_BLOCK)
 }
 
 // per item: sig_i = sk_i * H(m_i) (BlstBLS12381.sign) ; sk as 4 LE u64 words
-extern "C" __global__ void __launch_bounds__(TB_BLOCK)
+extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_MIN_WAVES)
     k_sign(const uint64_t* __restrict__ sks, const uint8_t* __restrict__ msgs, const uint32_t* __restrict__ msg_off,
            const uint8_t* __restrict__ dst, uint32_t dlen, uint32_t n, uint8_t* __restrict__ out) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;

@@ -7,7 +7,7 @@ using namespace tb;
 // ---------------------------------------------------------------------------
 // public keys
 // ---------------------------------------------------------------------------
-extern "C" __global__ void __launch_bounds__(TB_BLOCK)
+extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_MIN_WAVES)
     k_pk_decompress(const uint8_t* __restrict__ pks, uint32_t K, g1a* __restrict__ pk_aff, uint8_t* __restrict__ pk_code) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= K) return;
@@ -41,7 +41,7 @@ __device__ TB_INLINE g1a neg_r_g1(const g1a* __restrict__ comb, uint64_t r) {
 // the table, tab_n entries).  multi_wave: sets with more than one key are left
 // to k_set_pk_wave (one 64-lane wave per set) and skipped here.  P2 (nullable):
 // the set's signature pair's G1 point, P2[i] = -[r_i] g1 (k_sigs.hip).
-extern "C" __global__ void __launch_bounds__(TB_BLOCK)
+extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_MIN_WAVES)
     k_set_pk(const uint32_t* __restrict__ pk_off, const g1a* __restrict__ pk_aff, const uint8_t* __restrict__ pk_code,
              const uint64_t* __restrict__ rand, uint32_t n, g1a* __restrict__ P, uint8_t* __restrict__ set_code,
              uint32_t* __restrict__ n_bad, const uint32_t* __restrict__ key_idx, uint32_t tab_n, uint32_t multi_wave,
@@ -62,7 +62,7 @@ extern "C" __global__ void __launch_bounds__(TB_BLOCK)
 
 // Compaction of the multi-key sets (pk_off[i+1] - pk_off[i] > 1) into list[],
 // count in cnt[0] (zeroed by the host): the work list of k_set_pk_wave.
-extern "C" __global__ void __launch_bounds__(TB_BLOCK)
+extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_MIN_WAVES)
     k_multi_list(const uint32_t* __restrict__ pk_off, uint32_t n, uint32_t* __restrict__ list, uint32_t* __restrict__ cnt) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -124,7 +124,7 @@ extern "C" __global__ void __launch_bounds__(64)
 // Non-batch API kernels (aggregation, hashing, signing)
 // ---------------------------------------------------------------------------
 // out: 48-byte compressed aggregate, or code via status. BlstPublicKey.aggregate.
-extern "C" __global__ void __launch_bounds__(TB_BLOCK)
+extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_MIN_WAVES)
     k_aggregate_pks(const g1a* __restrict__ pk_aff, const uint8_t* __restrict__ pk_code, uint32_t K, uint8_t* __restrict__ out) {
   __shared__ g1j sh[TB_BLOCK];
   __shared__ int any_bad;
@@ -151,7 +151,7 @@ extern "C" __global__ void __launch_bounds__(TB_BLOCK)
 }
 
 // per item: pk_i = sk_i * g1
-extern "C" __global__ void __launch_bounds__(TB_BLOCK)
+extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_MIN_WAVES)
     k_sk_to_pk(const uint64_t* __restrict__ sks, uint32_t n, uint8_t* __restrict__ out) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;

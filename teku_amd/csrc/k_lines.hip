@@ -78,7 +78,7 @@ __device__ TB_INLINE line3 line_load(const uint4* __restrict__ lines, uint32_t n
 __device__ TB_NOINLINE line3 add_step_leaf(g2p& T, const g2a& Q, const g1a& P) { return miller_add_step(T, Q, P); }
 }  // namespace
 
-extern "C" __global__ void __launch_bounds__(TB_BLOCK)
+extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_MIN_WAVES)
     k_miller_lines(const g1a* __restrict__ P, const g2a* __restrict__ Q, const uint8_t* __restrict__ skip,
                    const uint8_t* __restrict__ code_a, const uint8_t* __restrict__ code_b, uint32_t n, uint4* __restrict__ lines) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -93,13 +93,24 @@ extern "C" __global__ void __launch_bounds__(TB_BLOCK)
   }
 }
 
+// Thread t accumulates the main pairs PER t .. PER t + PER - 1 (< n; their
+// lines in `lines`, stride n) and, at each step s, at most one line of the
+// n_extra pairs in `xlines` (stride n_extra; the signature side's bit-sum
+// pairs, whose lines k_miller_lines writes on the signature stream): extra
+// pair e goes to thread (s * n_extra + e) mod T at step s.  The product of all threads' f is the
+// same, since every thread applies the same squaring schedule after step s;
+// spreading the extra pairs one line at a time keeps every thread's work
+// within one line product (+0.5 %) instead of adding whole Miller loops to a
+// few threads (a tail as long as the kernel).
 template <int PER>
 __device__ TB_INLINE void miller_acc_body(const uint4* __restrict__ lines, const uint8_t* __restrict__ skip,
                                           const uint8_t* __restrict__ code_a, const uint8_t* __restrict__ code_b, uint32_t n,
+                                          const uint4* __restrict__ xlines, const uint8_t* __restrict__ xskip, uint32_t n_extra,
                                           fp12* __restrict__ f_out) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t T = (n + PER - 1) / PER;
   const uint32_t i0 = PER * t;
-  if (i0 >= n) return;
+  if (t >= T) return;
   bool use[PER];
   TB_UNROLL for (int j = 0; j < PER; j++) {
     const uint32_t i = i0 + j;
@@ -107,6 +118,14 @@ __device__ TB_INLINE void miller_acc_body(const uint4* __restrict__ lines, const
   }
   fp12 f = fp12_one();
   int s = 0;
+  auto extra = [&](int step) {
+    if (!n_extra) return;
+    const uint32_t e = (t + T - (uint32_t)(step * n_extra) % T) % T;
+    if (e < n_extra && xskip[e] == 0) {
+      const line3 l = line_load(xlines, n_extra, e, step);
+      f = fp12_mul_by_line_i(f, l.a, l.b, l.c);
+    }
+  };
   TB_NOUNROLL for (int b = 62; b >= 0; --b) {
     if (b != 62) f = fp12_sqr_i(f);
     TB_UNROLL for (int j = 0; j < PER; j++) {
@@ -115,6 +134,7 @@ __device__ TB_INLINE void miller_acc_body(const uint4* __restrict__ lines, const
         f = fp12_mul_by_line_i(f, l.a, l.b, l.c);
       }
     }
+    extra(s);
     s++;
     if ((X_ABS >> b) & 1) {
       TB_UNROLL for (int j = 0; j < PER; j++) {
@@ -123,20 +143,23 @@ __device__ TB_INLINE void miller_acc_body(const uint4* __restrict__ lines, const
           f = fp12_mul_by_line_i(f, l.a, l.b, l.c);
         }
       }
+      extra(s);
       s++;
     }
   }
   f_out[t] = fp12_conj(f);
 }
 
-extern "C" __global__ void __launch_bounds__(TB_BLOCK)
+extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_MIN_WAVES)
     k_miller_acc1(const uint4* __restrict__ lines, const uint8_t* __restrict__ skip, const uint8_t* __restrict__ code_a,
-                  const uint8_t* __restrict__ code_b, uint32_t n, fp12* __restrict__ f) {
-  miller_acc_body<1>(lines, skip, code_a, code_b, n, f);
+                  const uint8_t* __restrict__ code_b, uint32_t n, const uint4* __restrict__ xlines, const uint8_t* __restrict__ xskip,
+                  uint32_t n_extra, fp12* __restrict__ f) {
+  miller_acc_body<1>(lines, skip, code_a, code_b, n, xlines, xskip, n_extra, f);
 }
 
-extern "C" __global__ void __launch_bounds__(TB_BLOCK)
+extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_MIN_WAVES)
     k_miller_acc2(const uint4* __restrict__ lines, const uint8_t* __restrict__ skip, const uint8_t* __restrict__ code_a,
-                  const uint8_t* __restrict__ code_b, uint32_t n, fp12* __restrict__ f) {
-  miller_acc_body<2>(lines, skip, code_a, code_b, n, f);
+                  const uint8_t* __restrict__ code_b, uint32_t n, const uint4* __restrict__ xlines, const uint8_t* __restrict__ xskip,
+                  uint32_t n_extra, fp12* __restrict__ f) {
+  miller_acc_body<2>(lines, skip, code_a, code_b, n, xlines, xskip, n_extra, f);
 }

@@ -83,7 +83,7 @@ __device__ TB_INLINE fp12 miller_loop2_inl(const g1a& P0, const g2a& Q0, bool s0
 // 2t+1 of the n set pairs (the f^2 of a step is paid once for both).  Invalid
 // sets (any code) and skipped pairs contribute 1; the batch already fails
 // through n_bad.
-extern "C" __global__ void __launch_bounds__(TB_BLOCK)
+extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_MIN_WAVES)
     k_miller2(const g1a* __restrict__ P, const g2a* __restrict__ Q, const uint8_t* __restrict__ skip,
               const uint8_t* __restrict__ code_a, const uint8_t* __restrict__ code_b, uint32_t n, fp12* __restrict__ f) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -97,7 +97,7 @@ extern "C" __global__ void __launch_bounds__(TB_BLOCK)
 
 // One pair per thread (mid-size batches: half the per-thread latency of the
 // two-pair accumulator when the GPU is not full).
-extern "C" __global__ void __launch_bounds__(TB_BLOCK)
+extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_MIN_WAVES)
     k_miller1(const g1a* __restrict__ P, const g2a* __restrict__ Q, const uint8_t* __restrict__ skip,
               const uint8_t* __restrict__ code_a, const uint8_t* __restrict__ code_b, uint32_t n, fp12* __restrict__ f) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;

@@ -6,7 +6,7 @@ using namespace tb;
 
 // BlstSignature.aggregate: every input must decode and be in G2.
 // out[0..95] = compressed sum; status[0] = first failing code (0 = ok)
-extern "C" __global__ void __launch_bounds__(TB_BLOCK)
+extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_MIN_WAVES)
     k_aggregate_sigs(const uint8_t* __restrict__ sigs, uint32_t K, uint8_t* __restrict__ out, int* __restrict__ status) {
   __shared__ g2j sh[TB_BLOCK];
   __shared__ int bad;
@@ -40,7 +40,7 @@ extern "C" __global__ void __launch_bounds__(TB_BLOCK)
 // sums group g = sigs[off[g], off[g+1]) with the same rules as
 // k_aggregate_sigs (every input decodes and is in G2; infinity adds nothing;
 // an empty group is the infinity signature, AbstractSignatureTest.java:49-52).
-extern "C" __global__ void __launch_bounds__(TB_BLOCK)
+extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_MIN_WAVES)
     k_aggregate_sigs_many(const uint8_t* __restrict__ sigs, const uint32_t* __restrict__ off, uint8_t* __restrict__ out,
                           int* __restrict__ status) {
   __shared__ g2j sh[TB_BLOCK];
@@ -73,7 +73,7 @@ extern "C" __global__ void __launch_bounds__(TB_BLOCK)
 }
 
 // per item: signature validity (decode + G2 check); out code | (inf << 8)
-extern "C" __global__ void __launch_bounds__(TB_BLOCK)
+extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_MIN_WAVES)
     k_sig_validate(const uint8_t* __restrict__ sigs, uint32_t n, uint32_t* __restrict__ out) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -99,19 +99,22 @@ extern "C" __global__ void __launch_bounds__(TB_BLOCK)
 //  * large batches: a bucket sum by the randomizers' bytes,
 //      sum_i r_i sig_i = sum_w sum_d (d 2^(8w)) B[w][d],  B[w][d] = sum of the
 //      sig_i whose byte w is d,
-//    and each bucket sum becomes one extra pair e(-C[w][d], B[w][d]): 8 x 255
-//    = 2040 pairs for the whole batch.  The bucket sums cost 8 mixed
-//    additions per signature; the weighting by d 2^(8w) -- the latency chain
-//    of a Pippenger reduction (running sums, 56 doublings of Horner) -- is
-//    replaced by the precomputed G1 multiples, and the 2040 pairs ride in the
-//    batch's Miller kernel.
+//    then split by digit bit, sum_d d B[w][d] = sum_k 2^k V[w][k] with
+//    V[w][k] = sum of the B[w][d] whose d has bit k set, and each V becomes
+//    one extra pair e(-C[w][2^k], V[w][k]): 64 pairs for the whole batch.
+//    The bucket sums cost 8 mixed additions per signature; the weighting by
+//    d 2^(8w) -- the latency chain of a Pippenger reduction (running sums, 56
+//    doublings of Horner) -- is replaced by the precomputed G1 multiples, and
+//    the 64 pairs' lines are spread over the batch's Miller accumulators
+//    (k_lines.hip), one line per thread at most.
 //
 //   k_msm_hist     per set: bucket counts (window w, digit d = byte w of r);
 //   k_msm_scan     exclusive scan -> bucket offsets          (randomizers only:
 //   k_msm_scatter  per set: set index into its 8 bucket lists  run beside k_sig_check)
 //   k_msm_bucket   per (bucket, chunk): sum of the chunk's affine signatures
-//   k_msm_bucket_pairs  per bucket: 64-lane LDS tree over its chunk sums,
-//                  affine B[w][d] and the pair (-C[w][d], B[w][d])
+//   k_msm_bucket_sum    per bucket: 64-lane LDS tree over its chunk sums
+//   k_msm_bitsum_pairs  per (window, bit): 128-bucket sum, affine, the pair
+//                  (-C[w][2^k], V[w][k])
 // Any invalid signature fails the whole batch (n_bad), so only valid, finite
 // signatures enter the buckets; infinity contributes nothing (blst skips it).
 // ---------------------------------------------------------------------------
@@ -120,7 +123,7 @@ extern "C" __global__ void __launch_bounds__(TB_BLOCK)
 #define TB_MSM_CHUNKS 64    // chunks per bucket list (131072 threads at 2048 buckets)
 
 // thread (w, d): comb[w * 256 + d] = (d 2^(8w)) g1, affine (d = 0: unused)
-extern "C" __global__ void __launch_bounds__(TB_BLOCK) k_g1_comb_init(g1a* __restrict__ comb) {
+extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_MIN_WAVES) k_g1_comb_init(g1a* __restrict__ comb) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= TB_MSM_W * TB_MSM_NB) return;
   const uint32_t w = t / TB_MSM_NB, d = t % TB_MSM_NB;
@@ -138,7 +141,7 @@ extern "C" __global__ void __launch_bounds__(TB_BLOCK) k_g1_comb_init(g1a* __res
 // per set: decode + G2 check.  skip_mode = 0: sig_aff + sig_use (1 = valid and
 // finite: the bucket input); skip_mode = 1: sig_aff = Q of the set's signature
 // pair and sig_use = its skip flag (1 = no pair: infinite or invalid).
-extern "C" __global__ void __launch_bounds__(TB_BLOCK)
+extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_MIN_WAVES)
     k_sig_check(const uint8_t* __restrict__ sigs, uint32_t n, g2a* __restrict__ sig_aff, uint8_t* __restrict__ sig_use,
                 uint8_t* __restrict__ sig_code, uint32_t* __restrict__ n_bad, uint32_t skip_mode) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -158,7 +161,7 @@ extern "C" __global__ void __launch_bounds__(TB_BLOCK)
   if (code != TB_SUCCESS) atomicAdd(n_bad, 1u);
 }
 
-extern "C" __global__ void __launch_bounds__(TB_BLOCK)
+extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_MIN_WAVES)
     k_msm_hist(const uint64_t* __restrict__ rand, uint32_t n, uint32_t* __restrict__ cnt) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -197,7 +200,7 @@ extern "C" __global__ void __launch_bounds__(256)
   if (t == 255) off[TB_MSM_W * TB_MSM_NB] = sh[t];
 }
 
-extern "C" __global__ void __launch_bounds__(TB_BLOCK)
+extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_MIN_WAVES)
     k_msm_scatter(const uint64_t* __restrict__ rand, uint32_t n, uint32_t* __restrict__ cur, uint32_t* __restrict__ idx) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -209,7 +212,7 @@ extern "C" __global__ void __launch_bounds__(TB_BLOCK)
 }
 
 // thread (bucket b, chunk c): sum of the affine signatures of chunk c of list b
-extern "C" __global__ void __launch_bounds__(TB_BLOCK)
+extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_MIN_WAVES)
     k_msm_bucket(const g2a* __restrict__ sig_aff, const uint8_t* __restrict__ use, const uint32_t* __restrict__ off,
                  const uint32_t* __restrict__ idx, g2j* __restrict__ part) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -227,15 +230,36 @@ extern "C" __global__ void __launch_bounds__(TB_BLOCK)
   part[t] = acc;
 }
 
-// block (w, d != 0): B = sum of the bucket's 64 chunk sums (LDS tree); pair
-// slot w * 255 + d - 1 = (-C[w][d], B), skipped when B is infinity
-extern "C" __global__ void __launch_bounds__(64)
-    k_msm_bucket_pairs(const g2j* __restrict__ part, const g1a* __restrict__ comb, g1a* __restrict__ P, g2a* __restrict__ Q,
-                       uint8_t* __restrict__ skip) {
+// block (w, d != 0): B[w][d] = sum of the bucket's 64 chunk sums (LDS tree)
+extern "C" __global__ void __launch_bounds__(64) k_msm_bucket_sum(const g2j* __restrict__ part, g2j* __restrict__ bucket) {
   __shared__ g2j sh[64];
   const uint32_t t = threadIdx.x;
   const uint32_t w = blockIdx.x / (TB_MSM_NB - 1), d = blockIdx.x % (TB_MSM_NB - 1) + 1, b = w * TB_MSM_NB + d;
   sh[t] = part[b * TB_MSM_CHUNKS + t];
+  __syncthreads();
+  for (uint32_t s = 32; s > 0; s >>= 1) {
+    if (t < s) sh[t] = jac_add(sh[t], sh[t + s]);
+    __syncthreads();
+  }
+  if (t == 0) bucket[b] = sh[0];
+}
+
+// block j = 8w + k: V = sum of the 128 bucket sums B[w][d] whose digit d has
+// bit k set, so that sum_d d B[w][d] = sum_k 2^k V[w][k]; pair slot j =
+// (-(2^(8w+k)) g1, V) with the G1 point from the comb table (d = 2^k), skipped
+// when V is infinity.  Lane l sums the digits of rank l and l + 64 among the
+// 128 with bit k set, then a 64-lane LDS tree.
+extern "C" __global__ void __launch_bounds__(64)
+    k_msm_bitsum_pairs(const g2j* __restrict__ bucket, const g1a* __restrict__ comb, g1a* __restrict__ P, g2a* __restrict__ Q,
+                       uint8_t* __restrict__ skip) {
+  __shared__ g2j sh[64];
+  const uint32_t t = threadIdx.x, w = blockIdx.x / 8, k = blockIdx.x % 8;
+  g2j acc = jac_inf<fp2>();
+  for (uint32_t r = t; r < 128; r += 64) {
+    const uint32_t d = ((r >> k) << (k + 1)) | (1u << k) | (r & ((1u << k) - 1u));  // r-th digit with bit k set
+    acc = jac_add(acc, bucket[w * TB_MSM_NB + d]);
+  }
+  sh[t] = acc;
   __syncthreads();
   for (uint32_t s = 32; s > 0; s >>= 1) {
     if (t < s) sh[t] = jac_add(sh[t], sh[t + s]);
@@ -248,7 +272,7 @@ extern "C" __global__ void __launch_bounds__(64)
       a.x = fp2_zero();
       a.y = fp2_zero();
     }
-    g1a c = comb[b];
+    g1a c = comb[w * TB_MSM_NB + (1u << k)];
     c.y = fp_neg(c.y);
     P[blockIdx.x] = c;
     Q[blockIdx.x] = a;

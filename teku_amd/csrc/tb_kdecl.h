@@ -28,6 +28,14 @@
 using namespace tb;
 
 #define TB_BLOCK 64
+// Minimum waves per SIMD the heavy one-thread-per-item kernels are compiled
+// for (__launch_bounds__ second argument): 1 lets a kernel use all 512
+// registers per lane; 2 caps it at 256 (the compiler spills the rest) so two
+// waves share each SIMD and hide each other's latency.  Build variants for
+// A/B: tools/build_variant.py.
+#ifndef TB_MIN_WAVES
+#define TB_MIN_WAVES 1
+#endif
 
 // Latency-bound kernels (G2 sum, the single Miller loop, Fp12 products, the
 // final exponentiation) run underneath throughput kernels that fill every
@@ -58,7 +66,8 @@ extern "C" __global__ void k_aggregate_pks(const g1a* __restrict__ pk_aff, const
 extern "C" __global__ void k_sk_to_pk(const uint64_t* __restrict__ sks, uint32_t n, uint8_t* __restrict__ out);
 extern "C" __global__ void k_g1_comb_init(g1a* __restrict__ comb);
 extern "C" __global__ void k_sig_check(const uint8_t* __restrict__ sigs, uint32_t n, g2a* __restrict__ sig_aff, uint8_t* __restrict__ sig_use, uint8_t* __restrict__ sig_code, uint32_t* __restrict__ n_bad, uint32_t skip_mode);
-extern "C" __global__ void k_msm_bucket_pairs(const g2j* __restrict__ part, const g1a* __restrict__ comb, g1a* __restrict__ P, g2a* __restrict__ Q, uint8_t* __restrict__ skip);
+extern "C" __global__ void k_msm_bucket_sum(const g2j* __restrict__ part, g2j* __restrict__ bucket);
+extern "C" __global__ void k_msm_bitsum_pairs(const g2j* __restrict__ bucket, const g1a* __restrict__ comb, g1a* __restrict__ P, g2a* __restrict__ Q, uint8_t* __restrict__ skip);
 extern "C" __global__ void k_msm_hist(const uint64_t* __restrict__ rand, uint32_t n, uint32_t* __restrict__ cnt);
 extern "C" __global__ void k_msm_scan(const uint32_t* __restrict__ cnt, uint32_t* __restrict__ off, uint32_t* __restrict__ cur);
 extern "C" __global__ void k_msm_scatter(const uint64_t* __restrict__ rand, uint32_t n, uint32_t* __restrict__ cur, uint32_t* __restrict__ idx);
@@ -73,8 +82,8 @@ extern "C" __global__ void k_sign(const uint64_t* __restrict__ sks, const uint8_
 extern "C" __global__ void k_miller2(const g1a* __restrict__ P, const g2a* __restrict__ Q, const uint8_t* __restrict__ skip, const uint8_t* __restrict__ code_a, const uint8_t* __restrict__ code_b, uint32_t n, fp12* __restrict__ f);
 extern "C" __global__ void k_miller1(const g1a* __restrict__ P, const g2a* __restrict__ Q, const uint8_t* __restrict__ skip, const uint8_t* __restrict__ code_a, const uint8_t* __restrict__ code_b, uint32_t n, fp12* __restrict__ f);
 extern "C" __global__ void k_miller_lines(const g1a* __restrict__ P, const g2a* __restrict__ Q, const uint8_t* __restrict__ skip, const uint8_t* __restrict__ code_a, const uint8_t* __restrict__ code_b, uint32_t n, uint4* __restrict__ lines);
-extern "C" __global__ void k_miller_acc1(const uint4* __restrict__ lines, const uint8_t* __restrict__ skip, const uint8_t* __restrict__ code_a, const uint8_t* __restrict__ code_b, uint32_t n, fp12* __restrict__ f);
-extern "C" __global__ void k_miller_acc2(const uint4* __restrict__ lines, const uint8_t* __restrict__ skip, const uint8_t* __restrict__ code_a, const uint8_t* __restrict__ code_b, uint32_t n, fp12* __restrict__ f);
+extern "C" __global__ void k_miller_acc1(const uint4* __restrict__ lines, const uint8_t* __restrict__ skip, const uint8_t* __restrict__ code_a, const uint8_t* __restrict__ code_b, uint32_t n, const uint4* __restrict__ xlines, const uint8_t* __restrict__ xskip, uint32_t n_extra, fp12* __restrict__ f);
+extern "C" __global__ void k_miller_acc2(const uint4* __restrict__ lines, const uint8_t* __restrict__ skip, const uint8_t* __restrict__ code_a, const uint8_t* __restrict__ code_b, uint32_t n, const uint4* __restrict__ xlines, const uint8_t* __restrict__ xskip, uint32_t n_extra, fp12* __restrict__ f);
 #define TB_LINE_BYTES_PER_PAIR (68u * 288u)  // k_miller_lines output per pair
 extern "C" __global__ void k_miller_wave(const g1a* __restrict__ P, const g2a* __restrict__ Q, const uint8_t* __restrict__ skip, const uint8_t* __restrict__ code_a, const uint8_t* __restrict__ code_b, uint32_t n, fp12* __restrict__ f);
 extern "C" __global__ void k_fp12_one(fp12* __restrict__ f);

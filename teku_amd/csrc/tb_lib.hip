@@ -11,7 +11,9 @@
 #include <cstring>
 #include <mutex>
 #include <algorithm>
+#include <dlfcn.h>
 #include <sys/random.h>
+#include <rccl/rccl.h>  // types and prototypes only: RCCL is resolved with dlopen (gather_partials)
 #include <thread>
 #include <type_traits>
 #include <vector>
@@ -81,12 +83,12 @@ struct dev_ctx {
   dbuf tab_aff, tab_code;                    // device-resident public-key table (tbls_pk_table_load)
   uint32_t tab_n = 0;
   hipEvent_t e_fork = nullptr, e_join[2] = {nullptr, nullptr}, e_sig = nullptr;
-  hipEvent_t e_t0 = nullptr, e_t1 = nullptr;  // per-call device timing (run_shard), created once
+  hipEvent_t e_t0 = nullptr, e_t1 = nullptr;  // per-call device timing (shard_launch), created once
   // Last use of `ws` on any stream.  The device-resident API queues work on the
   // caller's stream and returns; every later user of `ws` (on whatever stream)
   // first waits for this event, then records it after its own work.
   hipEvent_t e_ws = nullptr;
-  dbuf recs;  // partial records gathered for the final exponentiation (final_on_device0)
+  dbuf recs;  // partial records gathered for the final exponentiation (gather_partials, device 0)
   dbuf comb;  // (d 2^(8w)) g1 for w < 8, d < 256 (k_g1_comb_init): the signature pairs' G1 side
   hbuf hin, hout;
 };
@@ -112,13 +114,14 @@ size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
 // below it, one signature pair (-[r_i] g1, sig_i) per set.
 #define TB_MSM_MIN 32768u
 #define TB_MSM_BUCKETS 2048u  // 8 windows x 256 digits (digit 0 unused)
-#define TB_MSM_BPAIRS 2040u   // 8 x 255 bucket pairs
+#define TB_MSM_NSUM 2040u     // 8 x 255 bucket sums (k_msm_bucket_sum)
+#define TB_MSM_XPAIRS 64u     // 8 windows x 8 digit bits: the signature side's pairs
 #define TB_MSM_PARTS (TB_MSM_BUCKETS * 64u)  // buckets x 64 chunks (k_msm_bucket)
 // Split Miller loop (k_miller_lines + k_miller_acc*, k_lines.hip): pairs per
-// line-buffer chunk (19,584 B of lines per pair: 2.6 GB per chunk), and the
+// line-buffer chunk (19,584 B of lines per pair: 5.1 GB per chunk), and the
 // pair count from which two pairs share an accumulator (the GPU is full at one
 // accumulator wave per SIMD: 1024 waves x 64 lanes x 2 pairs).
-#define TB_LINE_CHUNK 131072u
+#define TB_LINE_CHUNK 262144u
 #define TB_MILLER_PER2_MIN 131072u
 #define TB_MILLER1_MAX 4096u
 static bool miller_split() {
@@ -133,26 +136,29 @@ static uint32_t miller_wave_max() {
 }
 
 // Pairs of a batch of n sets: [0, n) the sets' (r_i apk_i, H(m_i)), then the
-// signature side -- n pairs (-[r_i] g1, sig_i) below TB_MSM_MIN sets, else
-// TB_MSM_BPAIRS bucket pairs.
+// signature side -- n pairs (-[r_i] g1, sig_i) below TB_MSM_MIN sets (ordinary
+// pairs of the Miller kernels), else TB_MSM_XPAIRS bit-sum pairs whose lines
+// the split Miller loop spreads over its accumulators (k_lines.hip).
 struct pair_plan {
-  uint32_t n, n_extra, n_pairs, per;
+  uint32_t n, n_extra, n_pairs, n_main, n_spread, per;
   bool msm, wave, split;
   explicit pair_plan(uint32_t n_) : n(n_) {
     msm = n >= TB_MSM_MIN;
-    n_extra = msm ? TB_MSM_BPAIRS : n;
+    n_extra = msm ? TB_MSM_XPAIRS : n;
     n_pairs = n + n_extra;
     wave = n_pairs <= miller_wave_max();
     split = !wave && miller_split();
-    per = wave ? 1u : split ? (n_pairs >= TB_MILLER_PER2_MIN ? 2u : 1u) : (n_pairs <= TB_MILLER1_MAX ? 1u : 2u);
+    n_spread = split && msm ? n_extra : 0u;  // pairs spread line by line
+    n_main = n_pairs - n_spread;             // pairs owned by accumulator threads
+    per = wave ? 1u : split ? (n_main >= TB_MILLER_PER2_MIN ? 2u : 1u) : (n_pairs <= TB_MILLER1_MAX ? 1u : 2u);
   }
-  uint32_t n_f() const { return (n_pairs + per - 1) / per; }  // Miller values
-  uint32_t line_pairs() const { return split ? std::min(n_pairs, TB_LINE_CHUNK) : 0u; }
+  uint32_t n_f() const { return (n_main + per - 1) / per; }  // Miller values
+  uint32_t line_pairs() const { return split ? std::min(n_main, TB_LINE_CHUNK) : 0u; }
 };
 
 struct ws_layout {
   size_t pk_aff, pk_code, P, Q, skip, set_code, sig_code, f, fpart, fpart2, n_bad, result;
-  size_t sig_aff, sig_use, msm_cnt, msm_off, msm_cur, msm_idx, msm_part, mlist, mcnt, lines, total;
+  size_t sig_aff, sig_use, msm_cnt, msm_off, msm_cur, msm_idx, msm_part, msm_sum, mlist, mcnt, lines, xlines, total;
   uint32_t nb_f;
   ws_layout() : total(0) {}
   ws_layout(const pair_plan& pp, uint32_t K) {
@@ -175,9 +181,11 @@ struct ws_layout {
     msm_cur = o;  o = align_up(o + (msm ? TB_MSM_BUCKETS * 4 : 0));
     msm_idx = o;  o = align_up(o + nm * 8 * 4);
     msm_part = o; o = align_up(o + (msm ? (size_t)TB_MSM_PARTS * sizeof(g2j) : 0));
+    msm_sum = o;  o = align_up(o + (msm ? (size_t)TB_MSM_BUCKETS * sizeof(g2j) : 0));
     mlist = o;    o = align_up(o + (size_t)n * 4);
     mcnt = o;     o = align_up(o + 4);
     lines = o;    o = align_up(o + (size_t)pp.line_pairs() * TB_LINE_BYTES_PER_PAIR);
+    xlines = o;   o = align_up(o + (size_t)pp.n_spread * TB_LINE_BYTES_PER_PAIR);
     f = o;        o = align_up(o + (size_t)(nf ? nf : 1) * sizeof(fp12));
     fpart = o;    o = align_up(o + (size_t)nb_f * sizeof(fp12));
     fpart2 = o;   o = align_up(o + (size_t)((nb_f + TB_PROD_CHUNK - 1) / TB_PROD_CHUNK) * sizeof(fp12));
@@ -276,8 +284,12 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
   if (pp.msm) {
     hipLaunchKernelGGL(k_msm_bucket, dim3(TB_MSM_PARTS / TB_BLOCK), blk, 0, sb, (const g2a*)(w + L.sig_aff), (const uint8_t*)(w + L.sig_use),
                        (const uint32_t*)msm_off, (const uint32_t*)msm_idx, (g2j*)(w + L.msm_part));
-    hipLaunchKernelGGL(k_msm_bucket_pairs, dim3(TB_MSM_BPAIRS), dim3(64), 0, sb, (const g2j*)(w + L.msm_part), c.comb.as<const g1a>(),
+    hipLaunchKernelGGL(k_msm_bucket_sum, dim3(TB_MSM_NSUM), dim3(64), 0, sb, (const g2j*)(w + L.msm_part), (g2j*)(w + L.msm_sum));
+    hipLaunchKernelGGL(k_msm_bitsum_pairs, dim3(TB_MSM_XPAIRS), dim3(64), 0, sb, (const g2j*)(w + L.msm_sum), c.comb.as<const g1a>(),
                        P + n, Q + n, skip + n);
+    if (pp.n_spread)  // their lines now, on this stream (the main pairs' kernel would take a whole extra wave round)
+      hipLaunchKernelGGL(k_miller_lines, dim3(1), dim3(TB_MSM_XPAIRS), 0, sb, (const g1a*)P + n, (const g2a*)Q + n, (const uint8_t*)skip + n,
+                         w + L.set_code + n, w + L.sig_code + n, TB_MSM_XPAIRS, (uint4*)(w + L.xlines));
   }
   TB_EV(9, sb);
   HIPCHK(hipEventRecord(c.e_join[1], sb));
@@ -308,13 +320,16 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
     if (pp.wave)
       hipLaunchKernelGGL(k_miller_wave, dim3(np), dim3(64), 0, s, (const g1a*)P, (const g2a*)Q, (const uint8_t*)skip, ca, cb, np, f);
     else if (pp.split) {
+      // chunks of the main pairs; the spread pairs' lines (xlines) are absorbed by the last chunk
       uint4* lines = (uint4*)(w + L.lines);
-      for (uint32_t lo = 0; lo < np; lo += TB_LINE_CHUNK) {
-        const uint32_t m = std::min(TB_LINE_CHUNK, np - lo), mt = (m + pp.per - 1) / pp.per;
+      for (uint32_t lo = 0; lo < pp.n_main; lo += TB_LINE_CHUNK) {
+        const uint32_t m = std::min(TB_LINE_CHUNK, pp.n_main - lo), mt = (m + pp.per - 1) / pp.per;
+        const uint32_t ex = lo + m == pp.n_main ? pp.n_spread : 0u;
         hipLaunchKernelGGL(k_miller_lines, dim3((m + TB_BLOCK - 1) / TB_BLOCK), blk, 0, s, (const g1a*)P + lo, (const g2a*)Q + lo,
                            (const uint8_t*)skip + lo, ca + lo, cb + lo, m, lines);
         hipLaunchKernelGGL(pp.per == 2 ? k_miller_acc2 : k_miller_acc1, dim3((mt + TB_BLOCK - 1) / TB_BLOCK), blk, 0, s,
-                           (const uint4*)lines, (const uint8_t*)skip + lo, ca + lo, cb + lo, m, f + lo / pp.per);
+                           (const uint4*)lines, (const uint8_t*)skip + lo, ca + lo, cb + lo, m, (const uint4*)(w + L.xlines),
+                           (const uint8_t*)skip + pp.n_main, ex, f + lo / pp.per);
       }
     } else
       hipLaunchKernelGGL(pp.per == 1 ? k_miller1 : k_miller2, dim3((nf + TB_BLOCK - 1) / TB_BLOCK), blk, 0, s, (const g1a*)P,
@@ -452,15 +467,13 @@ void pack_fill(uint8_t* h, const packed& p, const SET* sets, size_t lo, const ui
 
 const uint8_t ETH2_DST[] = "BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_POP_";
 
-// Runs sets[lo, hi) on device d; produces the 580-byte partial record on the host.
-// Optionally returns per-set verdict codes (set_code | sig_code) on the host.
+// Stage sets[lo, hi) on device c (its lock held) and queue the partial
+// pipeline on c->stream: the 580-byte partial record lands at *dpart (device
+// memory, c->in) -- nothing is synchronized.  e_t0/e_t1 bracket the kernels.
 template <class SET>
-int run_shard(int d, const SET* sets, size_t lo, size_t hi, const uint64_t* rand, const uint8_t* dst, uint32_t dlen,
-              uint8_t* partial_host, uint8_t* codes_host, double* dev_ms) {
+int shard_launch(dev_ctx* c, const SET* sets, size_t lo, size_t hi, const uint64_t* rand, const uint8_t* dst, uint32_t dlen,
+                 uint8_t** dpart, ws_layout& L, uint32_t* n_out) {
   constexpr bool idx_mode = !std::is_same<SET, tbls_set>::value;
-  dev_ctx* c = ctx_for(d);
-  if (!c) return TBLS_DEVICE_ERROR;
-  std::lock_guard<std::mutex> lk(c->mu);
   HIPCHK(hipSetDevice(c->dev));
   if (idx_mode) {  // key indices against this device's table, under its lock (a reload cannot interleave)
     if (!c->tab_n) return TBLS_BAD_ARGUMENT;
@@ -470,10 +483,10 @@ int run_shard(int d, const SET* sets, size_t lo, size_t hi, const uint64_t* rand
   }
   packed p = pack_layout(sets, lo, hi, dlen);
   const size_t in_total = p.total + TBLS_PARTIAL_BYTES + 256;
+  hipStream_t s = c->stream;
+  if (in_total > c->in.cap || in_total > c->hin.cap) HIPCHK(hipStreamSynchronize(s));  // buffers may still be read
   if (c->hin.ensure(in_total) || c->in.ensure(in_total)) return TBLS_DEVICE_ERROR;
   pack_fill(c->hin.b(), p, sets, lo, rand, dst, dlen);
-  hipStream_t s = c->stream;
-  hipEvent_t e0 = c->e_t0, e1 = c->e_t1;
   HIPCHK(hipMemcpyAsync(c->in.p, c->hin.p, p.total, hipMemcpyHostToDevice, s));
   uint8_t* di = c->in.as<uint8_t>();
   tbls_dev_batch b;
@@ -485,44 +498,167 @@ int run_shard(int d, const SET* sets, size_t lo, size_t hi, const uint64_t* rand
   b.sigs = di + p.off_sigs;
   b.rand = (const uint64_t*)(di + p.off_rand);
   b.n = p.n;
-  uint8_t* dpart = di + align_up(p.total);
-  ws_layout L;
-  HIPCHK(hipEventRecord(e0, s));
-  int rc = launch_partial(*c, b, s, dpart, L, di + p.off_dst, dlen, nullptr, false,
-                          idx_mode ? (const uint32_t*)(di + p.off_pks) : nullptr);
+  *dpart = di + align_up(p.total);
+  *n_out = p.n;
+  HIPCHK(hipEventRecord(c->e_t0, s));
+  int rc = launch_partial(*c, b, s, *dpart, L, di + p.off_dst, dlen, nullptr, false, idx_mode ? (const uint32_t*)(di + p.off_pks) : nullptr);
   if (rc) return rc;
-  HIPCHK(hipEventRecord(e1, s));
-  const size_t outb = TBLS_PARTIAL_BYTES + (codes_host ? 2 * (size_t)p.n : 0);
-  if (c->hout.ensure(outb)) return TBLS_DEVICE_ERROR;
-  HIPCHK(hipMemcpyAsync(c->hout.p, dpart, TBLS_PARTIAL_BYTES, hipMemcpyDeviceToHost, s));
-  if (codes_host && p.n) {
-    HIPCHK(hipMemcpyAsync(c->hout.b() + TBLS_PARTIAL_BYTES, c->ws.as<uint8_t>(L.set_code), p.n, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(c->hout.b() + TBLS_PARTIAL_BYTES + p.n, c->ws.as<uint8_t>(L.sig_code), p.n, hipMemcpyDeviceToHost, s));
-  }
-  HIPCHK(hipStreamSynchronize(s));
-  float ms = 0;
-  (void)hipEventElapsedTime(&ms, e0, e1);
-  if (dev_ms) *dev_ms = ms;
-  memcpy(partial_host, c->hout.p, TBLS_PARTIAL_BYTES);
-  if (codes_host) {
-    for (uint32_t i = 0; i < p.n; i++) {
-      uint8_t a = c->hout.b()[TBLS_PARTIAL_BYTES + i], bb = c->hout.b()[TBLS_PARTIAL_BYTES + p.n + i];
-      codes_host[i] = bb ? bb : a;  // signature errors first (decode failures surface as BlsException)
-    }
+  HIPCHK(hipEventRecord(c->e_t1, s));
+  return TBLS_SUCCESS;
+}
+
+// Per-set verdict codes of the last shard_launch (set_code | sig_code; signature
+// errors first: decode failures surface as BlsException), after the stream is idle.
+int shard_codes(dev_ctx* c, const ws_layout& L, uint32_t n, uint8_t* codes_host) {
+  if (!n) return TBLS_SUCCESS;
+  if (c->hout.ensure(2 * (size_t)n)) return TBLS_DEVICE_ERROR;
+  HIPCHK(hipMemcpyAsync(c->hout.p, c->ws.as<uint8_t>(L.set_code), n, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipMemcpyAsync(c->hout.b() + n, c->ws.as<uint8_t>(L.sig_code), n, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  for (uint32_t i = 0; i < n; i++) {
+    const uint8_t a = c->hout.b()[i], bb = c->hout.b()[n + i];
+    codes_host[i] = bb ? bb : a;
   }
   return TBLS_SUCCESS;
 }
 
-int final_on_device0(const uint8_t* recs_host, uint32_t g, int* ok) {
-  dev_ctx* c = ctx_for(0);
+// One device: shard -> final exponentiation straight from the device-resident
+// partial record (no host round trip).  codes_host (nullable): per-set codes.
+template <class SET>
+int verify_on_device(int d, const SET* sets, size_t n, const uint64_t* rand, const uint8_t* dst, uint32_t dlen, int* ok,
+                     uint8_t* codes_host, double* dev_ms) {
+  dev_ctx* c = ctx_for(d);
   if (!c) return TBLS_DEVICE_ERROR;
   std::lock_guard<std::mutex> lk(c->mu);
-  HIPCHK(hipSetDevice(c->dev));
-  // partial records go to a persistent region (no per-call allocation); the
-  // stream is idle here (every user of c->recs synchronizes before returning)
-  if (c->recs.ensure((size_t)g * TBLS_PARTIAL_BYTES)) return TBLS_DEVICE_ERROR;
-  HIPCHK(hipMemcpyAsync(c->recs.p, recs_host, (size_t)g * TBLS_PARTIAL_BYTES, hipMemcpyHostToDevice, c->stream));
-  return launch_final(*c, c->recs.p, g, c->stream, ok);
+  uint8_t* dpart = nullptr;
+  ws_layout L;
+  uint32_t nn = 0;
+  int rc = shard_launch(c, sets, 0, n, rand, dst, dlen, &dpart, L, &nn);
+  if (rc) return rc;
+  rc = launch_final(*c, dpart, 1, c->stream, ok);  // synchronizes c->stream
+  if (rc) return rc;
+  if (dev_ms) {
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, c->e_t0, c->e_t1);
+    *dev_ms = ms;
+  }
+  return codes_host ? shard_codes(c, L, nn, codes_host) : TBLS_SUCCESS;
+}
+
+// ---------------------------------------------------------------------------
+// Multi-GPU gather of the partial records: one 580-byte record
+// per device to device 0, then one final exponentiation there.
+//  * rccl (default): ncclGather over a single-process communicator
+//    (ncclCommInitAll over the library's devices, created on first use),
+//    every device's call inside one ncclGroupStart/End, on its own stream --
+//    the records move over xGMI;
+//  * peer: hipMemcpyPeerAsync of each record into device 0's buffer;
+//  * host: each record through pinned host memory (no peer access needed).
+// All three give the same bytes in device 0's buffer (TBLS_GATHER selects).
+// ---------------------------------------------------------------------------
+enum gather_mode { GATHER_RCCL, GATHER_PEER, GATHER_HOST };
+gather_mode gather_sel() {
+  const char* v = getenv("TBLS_GATHER");
+  if (v && !strcmp(v, "peer")) return GATHER_PEER;
+  if (v && !strcmp(v, "host")) return GATHER_HOST;
+  return GATHER_RCCL;
+}
+bool gather_forced() { return getenv("TBLS_GATHER") != nullptr; }  // also for one device (tests)
+
+struct rccl_api {
+  bool tried = false, ok = false;
+  decltype(&ncclCommInitAll) CommInitAll = nullptr;
+  decltype(&ncclCommDestroy) CommDestroy = nullptr;
+  decltype(&ncclGather) Gather = nullptr;
+  decltype(&ncclGroupStart) GroupStart = nullptr;
+  decltype(&ncclGroupEnd) GroupEnd = nullptr;
+  std::vector<ncclComm_t> comms;
+};
+rccl_api g_rccl;
+
+// RCCL resolved at run time (an already-loaded librccl.so.1 -- e.g. torch's --
+// is reused by its soname), one communicator per device; g_mu held.
+bool rccl_ready_locked() {
+  if (g_rccl.tried) return g_rccl.ok;
+  g_rccl.tried = true;
+  void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+  if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
+  if (!h) return false;
+  g_rccl.CommInitAll = (decltype(g_rccl.CommInitAll))dlsym(h, "ncclCommInitAll");
+  g_rccl.CommDestroy = (decltype(g_rccl.CommDestroy))dlsym(h, "ncclCommDestroy");
+  g_rccl.Gather = (decltype(g_rccl.Gather))dlsym(h, "ncclGather");
+  g_rccl.GroupStart = (decltype(g_rccl.GroupStart))dlsym(h, "ncclGroupStart");
+  g_rccl.GroupEnd = (decltype(g_rccl.GroupEnd))dlsym(h, "ncclGroupEnd");
+  if (!g_rccl.CommInitAll || !g_rccl.CommDestroy || !g_rccl.Gather || !g_rccl.GroupStart || !g_rccl.GroupEnd) return false;
+  std::vector<int> devs;
+  for (dev_ctx* c : g_ctx) devs.push_back(c->dev);
+  g_rccl.comms.assign(devs.size(), nullptr);
+  if (g_rccl.CommInitAll(g_rccl.comms.data(), (int)devs.size(), devs.data()) != ncclSuccess) {
+    g_rccl.comms.clear();
+    return false;
+  }
+  g_rccl.ok = true;
+  return true;
+}
+
+// Device records dpart[g] (on each device's stream) -> c0->recs (device 0)
+int gather_partials(gather_mode mode, int G, const std::vector<uint8_t*>& dpart) {
+  dev_ctx* c0 = ctx_for(0);
+  HIPCHK(hipSetDevice(c0->dev));
+  if (c0->recs.ensure((size_t)G * TBLS_PARTIAL_BYTES)) return TBLS_DEVICE_ERROR;
+  uint8_t* recv = c0->recs.as<uint8_t>();
+  if (mode == GATHER_RCCL) {
+    {
+      std::lock_guard<std::mutex> lk(g_mu);
+      if (!rccl_ready_locked()) return TBLS_DEVICE_ERROR;
+    }
+    if (g_rccl.GroupStart() != ncclSuccess) return TBLS_DEVICE_ERROR;
+    int bad = 0;
+    for (int g = 0; g < G; g++) {
+      dev_ctx* c = ctx_for(g);
+      bad |= hipSetDevice(c->dev) != hipSuccess;
+      bad |= g_rccl.Gather(dpart[g], g == 0 ? recv : nullptr, TBLS_PARTIAL_BYTES, ncclUint8, 0, g_rccl.comms[g], c->stream) != ncclSuccess;
+    }
+    bad |= g_rccl.GroupEnd() != ncclSuccess;
+    if (bad) return TBLS_DEVICE_ERROR;
+    // device 0's stream holds the gather; the others' sends complete on theirs
+    for (int g = 1; g < G; g++) {
+      dev_ctx* c = ctx_for(g);
+      HIPCHK(hipSetDevice(c->dev));
+      HIPCHK(hipEventRecord(c->e_join[0], c->stream));
+      HIPCHK(hipSetDevice(c0->dev));
+      HIPCHK(hipStreamWaitEvent(c0->stream, c->e_join[0], 0));
+    }
+    HIPCHK(hipSetDevice(c0->dev));
+    return TBLS_SUCCESS;
+  }
+  if (mode == GATHER_PEER) {
+    for (int g = 0; g < G; g++) {
+      dev_ctx* c = ctx_for(g);
+      HIPCHK(hipSetDevice(c->dev));
+      HIPCHK(hipMemcpyPeerAsync(recv + (size_t)g * TBLS_PARTIAL_BYTES, c0->dev, dpart[g], c->dev, TBLS_PARTIAL_BYTES, c->stream));
+      if (g) {
+        HIPCHK(hipEventRecord(c->e_join[0], c->stream));
+        HIPCHK(hipSetDevice(c0->dev));
+        HIPCHK(hipStreamWaitEvent(c0->stream, c->e_join[0], 0));
+      }
+    }
+    HIPCHK(hipSetDevice(c0->dev));
+    return TBLS_SUCCESS;
+  }
+  std::vector<uint8_t> host((size_t)G * TBLS_PARTIAL_BYTES);
+  for (int g = 0; g < G; g++) {
+    dev_ctx* c = ctx_for(g);
+    HIPCHK(hipSetDevice(c->dev));
+    if (c->hout.ensure(TBLS_PARTIAL_BYTES)) return TBLS_DEVICE_ERROR;
+    HIPCHK(hipMemcpyAsync(c->hout.p, dpart[g], TBLS_PARTIAL_BYTES, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    memcpy(host.data() + (size_t)g * TBLS_PARTIAL_BYTES, c->hout.p, TBLS_PARTIAL_BYTES);
+  }
+  HIPCHK(hipSetDevice(c0->dev));
+  HIPCHK(hipMemcpyAsync(recv, host.data(), host.size(), hipMemcpyHostToDevice, c0->stream));
+  HIPCHK(hipStreamSynchronize(c0->stream));
+  return TBLS_SUCCESS;
 }
 
 // generic single-kernel helpers: upload bytes, run, download
@@ -639,6 +775,10 @@ extern "C" int tbls_init(int n_devices, uint32_t flags) {
 
 extern "C" void tbls_shutdown(void) {
   std::lock_guard<std::mutex> lk(g_mu);
+  if (g_rccl.ok)
+    for (ncclComm_t cm : g_rccl.comms) (void)g_rccl.CommDestroy(cm);
+  g_rccl.comms.clear();
+  g_rccl.ok = g_rccl.tried = false;
   for (dev_ctx* c : g_ctx) {
     (void)hipSetDevice(c->dev);
     if (c->in.p) (void)hipFree(c->in.p);
@@ -682,35 +822,54 @@ int batch_verify_impl(const SET* sets, size_t n, const uint64_t* rand, int n_gpu
   int G = (int)g_ctx.size();
   if (n_gpus > 0 && n_gpus < G) G = n_gpus;
   if ((size_t)G > n) G = (int)n;
-  // contiguous shards balanced by key count
-  uint64_t totalK = 0;
-  for (size_t i = 0; i < n; i++) totalK += sets[i].n_pks + 1;
-  std::vector<size_t> cut(G + 1, n);
-  cut[0] = 0;
-  {
-    uint64_t acc = 0;
-    int g = 1;
-    for (size_t i = 0; i < n && g < G; i++) {
-      acc += sets[i].n_pks + 1;
-      while (g < G && acc * G >= totalK * (uint64_t)g) cut[g++] = i + 1;  // as dist.shard_bounds
+  std::vector<double> dms(G, 0);
+  int rc = TBLS_SUCCESS;
+  if (G == 1 && !gather_forced()) {
+    rc = verify_on_device(0, sets, n, rand, ETH2_DST, 43, ok, nullptr, &dms[0]);
+  } else {
+    // contiguous shards balanced by key count
+    uint64_t totalK = 0;
+    for (size_t i = 0; i < n; i++) totalK += sets[i].n_pks + 1;
+    std::vector<size_t> cut(G + 1, n);
+    cut[0] = 0;
+    {
+      uint64_t acc = 0;
+      int g = 1;
+      for (size_t i = 0; i < n && g < G; i++) {
+        acc += sets[i].n_pks + 1;
+        while (g < G && acc * G >= totalK * (uint64_t)g) cut[g++] = i + 1;  // as dist.shard_bounds
+      }
+    }
+    // every device's lock for the whole batch, in device order (no deadlock)
+    std::vector<std::unique_lock<std::mutex>> locks;
+    for (int g = 0; g < G; g++) locks.emplace_back(ctx_for(g)->mu);
+    std::vector<uint8_t*> dpart(G, nullptr);
+    std::vector<int> rcs(G, 0);
+    auto stage = [&](int g) {
+      ws_layout L;
+      uint32_t nn;
+      rcs[g] = shard_launch(ctx_for(g), sets, cut[g], cut[g + 1], rand, ETH2_DST, 43, &dpart[g], L, &nn);
+    };
+    if (G == 1) {
+      stage(0);
+    } else {  // host-side packing and launch queueing in parallel, one thread per device
+      std::vector<std::thread> th;
+      for (int g = 0; g < G; g++) th.emplace_back(stage, g);
+      for (auto& x : th) x.join();
+    }
+    for (int g = 0; g < G; g++)
+      if (rcs[g]) return rcs[g];
+    rc = gather_partials(gather_sel(), G, dpart);
+    if (!rc) rc = launch_final(*ctx_for(0), ctx_for(0)->recs.p, (uint32_t)G, ctx_for(0)->stream, ok);
+    for (int g = 0; g < G && !rc; g++) {
+      dev_ctx* c = ctx_for(g);
+      (void)hipSetDevice(c->dev);
+      (void)hipStreamSynchronize(c->stream);
+      float ms = 0;
+      (void)hipEventElapsedTime(&ms, c->e_t0, c->e_t1);
+      dms[g] = ms;
     }
   }
-  std::vector<uint8_t> recs((size_t)G * TBLS_PARTIAL_BYTES);
-  std::vector<int> rcs(G, 0);
-  std::vector<double> dms(G, 0);
-  if (G == 1) {
-    rcs[0] = run_shard(0, sets, 0, n, rand, ETH2_DST, 43, recs.data(), nullptr, &dms[0]);
-  } else {
-    std::vector<std::thread> th;
-    for (int g = 0; g < G; g++)
-      th.emplace_back([&, g] {
-        rcs[g] = run_shard(g, sets, cut[g], cut[g + 1], rand, ETH2_DST, 43, recs.data() + (size_t)g * TBLS_PARTIAL_BYTES, nullptr, &dms[g]);
-      });
-    for (auto& x : th) x.join();
-  }
-  for (int g = 0; g < G; g++)
-    if (rcs[g]) return rcs[g];
-  int rc = final_on_device0(recs.data(), (uint32_t)G, ok);
   if (t) {
     t->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     t->device_ms = 0;
@@ -763,7 +922,7 @@ extern "C" size_t tbls_pk_table_size(void) {
 }
 
 extern "C" int tbls_batch_verify_idx(const tbls_set_idx* sets, size_t n, const uint64_t* rand, int n_gpus, int* ok, tbls_timing* t) {
-  // indices are checked against each device's table under that device's lock (run_shard)
+  // indices are checked against each device's table under that device's lock (shard_launch)
   return batch_verify_impl(sets, n, rand, n_gpus, ok, t);
 }
 
@@ -774,13 +933,11 @@ static int verify_one(const uint8_t* pks, uint32_t n_pks, const uint8_t* msg, si
   if (ensure_init()) return TBLS_DEVICE_ERROR;
   if (dlen > 255) return TBLS_BAD_ARGUMENT;
   tbls_set s = {pks, n_pks, msg, (uint32_t)len, sig};
-  uint8_t rec[TBLS_PARTIAL_BYTES];
   uint8_t code = 0;
   uint64_t one = 1;
-  int rc = run_shard(0, &s, 0, 1, &one, dst, (uint32_t)dlen, rec, &code, nullptr);
-  if (rc) return rc;
+  int rc = verify_on_device(0, &s, 1, &one, dst, (uint32_t)dlen, ok, &code, nullptr);
   if (code_out) *code_out = code;
-  return final_on_device0(rec, 1, ok);
+  return rc;
 }
 
 extern "C" int tbls_verify(const uint8_t pk[48], const uint8_t* msg, size_t len, const uint8_t sig[96], const uint8_t* dst, size_t dlen,
@@ -919,11 +1076,7 @@ extern "C" int tbls_aggregate_verify(const uint8_t* pks, const uint8_t* const* m
   std::vector<tbls_set> sets(n);
   std::vector<uint64_t> ones(n, 1);
   for (size_t i = 0; i < n; i++) sets[i] = {pks + 48 * i, 1, msgs[i], msg_lens[i], i == 0 ? sig : INF_SIG};
-  uint8_t rec[TBLS_PARTIAL_BYTES];
-  std::vector<uint8_t> codes(n);
-  int rc = run_shard(0, sets.data(), 0, n, ones.data(), ETH2_DST, 43, rec, codes.data(), nullptr);
-  if (rc) return rc;
-  return final_on_device0(rec, 1, ok);
+  return verify_on_device(0, sets.data(), n, ones.data(), ETH2_DST, 43, ok, nullptr, nullptr);
 }
 
 extern "C" int tbls_pk_validate(const uint8_t pk[48]) {

@@ -14,6 +14,7 @@ gloo test (tests/test_dist.py).
 
 from __future__ import annotations
 
+import struct
 from typing import Optional, Sequence, Tuple
 
 import torch
@@ -53,3 +54,32 @@ def all_gather_partials(partial: torch.Tensor) -> torch.Tensor:
     parts = [torch.empty_like(partial) for _ in range(world)]
     dist.all_gather(parts, partial)
     return torch.cat(parts)
+
+
+# ---- partial record codec (the bytes tbls_dev_batch_partial writes) ----------
+# 576-byte Fp12 then a little-endian uint32 invalid-set count.  The Fp12 is the
+# kernels' struct fp12 {fp6 c0, c1} / fp6 {fp2 c0, c1, c2} / fp2 {fp c0, c1}:
+# 12 Fp coordinates in that nesting order, each 12 little-endian 32-bit limbs
+# of the Montgomery form x * 2^406 mod p, weakly reduced (< 2p).
+P_MOD = 0x1A0111EA397FE69A4B1BA7B6434BACD764774B84F38512BF6730D2A0F6B0F6241EABFFFEB153FFFFB9FEFFFFFFFFAAAB
+R_MONT = 1 << 406
+PARTIAL_BYTES = 580
+
+
+def decode_partial(rec: bytes):
+    """-> (Fp12 as ((a0, a1, a2), (b0, b1, b2)) with a_i = (x, y) canonical ints, n_bad)."""
+    assert len(rec) == PARTIAL_BYTES
+    rinv = pow(R_MONT, -1, P_MOD)
+    limbs = struct.unpack("<144I", rec[:576])
+    v = [sum(limbs[12 * k + j] << (32 * j) for j in range(12)) * rinv % P_MOD for k in range(12)]
+    c = [(v[2 * i], v[2 * i + 1]) for i in range(6)]
+    return ((c[0], c[1], c[2]), (c[3], c[4], c[5])), struct.unpack("<I", rec[576:])[0]
+
+
+def encode_partial(f, n_bad: int) -> bytes:
+    (a0, a1, a2), (b0, b1, b2) = f
+    out = []
+    for x in (v for fp2 in (a0, a1, a2, b0, b1, b2) for v in fp2):
+        m = x * R_MONT % P_MOD
+        out += [(m >> (32 * j)) & 0xFFFFFFFF for j in range(12)]
+    return struct.pack("<144I", *out) + struct.pack("<I", n_bad)

@@ -1,9 +1,11 @@
 """World-size-2 (gloo, CPU) test of the multi-GPU path's sharding and its one
 collective (teku_amd/dist.py): each rank builds the partial record of its
 shard -- partial Miller product including its own (-g1, S_g) pair, plus an
-invalid-set count -- ranks all_gather the records, rank 0 multiplies them and
-runs the single final exponentiation.  The partials are computed with the
-oracle here (no GPU); on GPUs they come from tbls_dev_batch_partial."""
+invalid-set count -- in the HIP record format (12 x 32-bit Montgomery limbs per
+coordinate, teku_amd.dist.encode_partial; tests/test_gpu_dist.py decodes real
+tbls_dev_batch_partial records with the same codec), ranks all_gather the
+records, rank 0 multiplies them and runs the single final exponentiation.  The
+partials are computed with the oracle here (no GPU)."""
 
 import os
 import random
@@ -26,17 +28,6 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _enc12(f):
-    (a0, a1, a2), (b0, b1, b2) = f
-    return b"".join(x.to_bytes(48, "big") for c in (a0, a1, a2, b0, b1, b2) for x in c)
-
-
-def _dec12(b):
-    v = [int.from_bytes(b[48 * i : 48 * i + 48], "big") for i in range(12)]
-    c = [(v[2 * i], v[2 * i + 1]) for i in range(6)]
-    return ((c[0], c[1], c[2]), (c[3], c[4], c[5]))
-
-
 def _partial(pks, msgs, sigs, rands):
     f, s, bad = O.F12_ONE, O.jac_inf(O.FP2), 0
     for pk, m, sg, r in zip(pks, msgs, sigs, rands):
@@ -51,7 +42,9 @@ def _partial(pks, msgs, sigs, rands):
     s_aff = O.jac_to_affine(O.FP2, s)
     if s_aff is not None:
         f = O.f12_mul(f, O.miller_loop(O.NEG_G1, s_aff))
-    return _enc12(f) + bad.to_bytes(4, "little")
+    from teku_amd.dist import encode_partial
+
+    return encode_partial(f, bad)  # the HIP record format: Montgomery limbs
 
 
 def _worker(rank, world, port, case, out_q):
@@ -65,11 +58,13 @@ def _worker(rank, world, port, case, out_q):
     assert rec.numel() == PARTIAL_BYTES
     allp = bytes(all_gather_partials(rec).numpy())
     if rank == 0:
+        from teku_amd.dist import decode_partial
+
         f, bad = O.F12_ONE, 0
         for g in range(world):
-            r = allp[g * PARTIAL_BYTES : (g + 1) * PARTIAL_BYTES]
-            f = O.f12_mul(f, _dec12(r[:576]))
-            bad += int.from_bytes(r[576:], "little")
+            fg, bg = decode_partial(allp[g * PARTIAL_BYTES : (g + 1) * PARTIAL_BYTES])
+            f = O.f12_mul(f, fg)
+            bad += bg
         out_q.put(bad == 0 and O.f12_is_one(O.final_exponentiation(f)))
     dist.barrier()
     dist.destroy_process_group()
@@ -119,3 +114,20 @@ def test_two_ranks_tampered_batch(sets4):
     bad = list(sigs)
     bad[3] = sigs[0]  # rank 1's shard carries a wrong signature
     assert _run((pks, msgs, bad, rands)) is False
+
+
+def test_partial_record_codec_roundtrip():
+    """encode_partial / decode_partial: canonical and weakly reduced (x + p) limbs."""
+    import struct
+
+    from teku_amd.dist import P_MOD, R_MONT, decode_partial, encode_partial
+
+    rng = random.Random(9)
+    f = tuple(tuple((rng.randrange(O.P), rng.randrange(O.P)) for _ in range(3)) for _ in range(2))
+    rec = encode_partial(f, 3)
+    assert decode_partial(rec) == (f, 3)
+    limbs = list(struct.unpack("<144I", rec[:576]))
+    m = sum(limbs[j] << (32 * j) for j in range(12)) + P_MOD  # first coordinate in [p, 2p)
+    limbs[:12] = [(m >> (32 * j)) & 0xFFFFFFFF for j in range(12)]
+    assert decode_partial(struct.pack("<144I", *limbs) + rec[576:])[0] == f
+    assert R_MONT == 1 << 406

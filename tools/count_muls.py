@@ -62,18 +62,20 @@ def main():
     res["set_hash"] = per_unit("STAGE_SET_HASH", [enc_h2c(m) for m in msgs], name="set_hash")
     q = [O.g2_decompress(s)[1] for s in sigs]
     # Large batches: the signature side as bucket sums by randomizer byte
-    # (k_msm_bucket: one mixed addition per nonzero byte, 8 windows) and one
-    # extra Miller pair per bucket (k_msm_bucket_pairs: 64-lane tree of 63
-    # additions + affine conversion per bucket), k_sigs.hip, per set at n =
-    # MSM_N.  Point-operation costs in Fp products from the tb_curve.h formulas
-    # (Fp2 mul = 3 products, Fp2 sqr = 2): madd-2007-bl 7M+4S = 29, add-2007-bl
-    # 11M+5S = 43; the Fp2 affine conversion (binary-GCD inversion ~65 +
-    # norm/products) ~81.
-    MADD, ADD, AFF2, MSM_N, BPAIRS = 29, 43, 81, 131072, 2040
-    res["g2_sum"] = 8 * 255 / 256 * MADD + BPAIRS * (63 * ADD + AFF2) / MSM_N
-    sq["g2_sum"] = 8 * 255 / 256 * 4 * 2 + BPAIRS * 63 * 5 * 2 / MSM_N
-    f2["g2_sum"] = 8 * 255 / 256 * 7 + BPAIRS * 63 * 11 / MSM_N
-    res["pairs_per_set"] = (MSM_N + BPAIRS) / MSM_N
+    # (k_msm_bucket: one mixed addition per nonzero byte, 8 windows), a
+    # 64-lane tree per bucket (k_msm_bucket_sum: 63 additions), then 64 bit
+    # sums of 128 buckets each (k_msm_bitsum_pairs: 2 + 63 additions, affine)
+    # whose 64 extra Miller pairs are spread over the accumulators
+    # (k_sigs.hip, k_lines.hip), per set at n = MSM_N.  Point-operation costs in
+    # Fp products from the tb_curve.h formulas (Fp2 mul = 3 products, Fp2 sqr =
+    # 2): madd-2007-bl 7M+4S = 29, add-2007-bl 11M+5S = 43; the Fp2 affine
+    # conversion (binary-GCD inversion ~65 + norm/products) ~81.
+    MADD, ADD, AFF2, MSM_N, NSUM, XP = 29, 43, 81, 131072, 2040, 64
+    adds = NSUM * 63 + XP * 65
+    res["g2_sum"] = 8 * 255 / 256 * MADD + (adds * ADD + XP * AFF2) / MSM_N
+    sq["g2_sum"] = 8 * 255 / 256 * 4 * 2 + adds * 5 * 2 / MSM_N
+    f2["g2_sum"] = 8 * 255 / 256 * 7 + adds * 11 / MSM_N
+    res["pairs_per_set"] = (MSM_N + XP) / MSM_N
     # small batches: the signature pair's G1 point -[r] g1 = sum of <= 8
     # precomputed multiples (k_set_pk: G1 madd 7M+4S = 11) + affine (~70)
     res["set_pk_sigpair"] = 8 * 255 / 256 * 11 + 70
