@@ -5,19 +5,70 @@
 using namespace tb;
 
 namespace {
+// Fp12 squaring and sparse line product for the accumulator kernel, written as
+// an explicit sequence of Fp2 products with scheduling fences between them
+// (TB_ACC_FENCE): the compiler's scheduler otherwise interleaves neighbouring
+// products for latency and keeps all their operands and temporaries live at
+// once -- past the 512-register file, into scratch.  With the fences at most
+// one Fp2 product's temporaries are live beside the values the formulas
+// need; the product itself keeps five independent accumulator chains
+// (tb_tower.h fp2_mul_lazy).
+#ifndef TB_ACC_FENCE
+#define TB_ACC_FENCE 1
+#endif
+#if TB_ACC_FENCE && defined(__HIP_DEVICE_COMPILE__)
+#define TB_FENCE() __builtin_amdgcn_sched_barrier(0)
+#else
+#define TB_FENCE() ((void)0)
+#endif
+
+__device__ TB_INLINE fp2 m2(const fp2& a, const fp2& b) {
+  const fp2 r = fp2_mul(a, b);
+  TB_FENCE();
+  return r;
+}
+
+__device__ TB_INLINE fp6 fp6_mul_f(const fp6& a, const fp6& b) {
+  const fp2 t0 = m2(a.c0, b.c0);
+  const fp2 t1 = m2(a.c1, b.c1);
+  const fp2 t2 = m2(a.c2, b.c2);
+  const fp2 c0 = fp2_add(t0, fp2_mul_xi(fp2_sub(m2(fp2_add(a.c1, a.c2), fp2_add(b.c1, b.c2)), fp2_add(t1, t2))));
+  const fp2 c1 = fp2_add(fp2_sub(m2(fp2_add(a.c0, a.c1), fp2_add(b.c0, b.c1)), fp2_add(t0, t1)), fp2_mul_xi(t2));
+  const fp2 c2 = fp2_add(fp2_sub(m2(fp2_add(a.c0, a.c2), fp2_add(b.c0, b.c2)), fp2_add(t0, t2)), t1);
+  return {c0, c1, c2};
+}
+
+// a * (b0 + b1 v)
+__device__ TB_INLINE fp6 fp6_mul_by_01_f(const fp6& a, const fp2& b0, const fp2& b1) {
+  const fp2 t0 = m2(a.c0, b0);
+  const fp2 t1 = m2(a.c1, b1);
+  const fp2 c0 = fp2_add(t0, fp2_mul_xi(m2(a.c2, b1)));
+  const fp2 c1 = fp2_sub(fp2_sub(m2(fp2_add(a.c0, a.c1), fp2_add(b0, b1)), t0), t1);
+  const fp2 c2 = fp2_add(t1, m2(a.c2, b0));
+  return {c0, c1, c2};
+}
+
 TB_HD TB_INLINE fp12 fp12_sqr_i(const fp12& a) {
-  fp6 ab = fp6_mul(a.c0, a.c1);
-  fp6 t = fp6_mul(fp6_add(a.c0, a.c1), fp6_add(a.c0, fp6_mul_v(a.c1)));
-  fp6 c0 = fp6_sub(fp6_sub(t, ab), fp6_mul_v(ab));
-  fp6 c1 = fp6_add(ab, ab);
+  const fp6 ab = fp6_mul_f(a.c0, a.c1);
+  const fp6 s1 = fp6_add(a.c0, a.c1), s2 = fp6_add(a.c0, fp6_mul_v(a.c1));
+  TB_FENCE();
+  const fp6 t = fp6_mul_f(s1, s2);
+  const fp6 c0 = fp6_sub(fp6_sub(t, ab), fp6_mul_v(ab));
+  const fp6 c1 = fp6_add(ab, ab);
   return {c0, c1};
 }
 
+// f * line, line = (A + B v) + (C v) w: f1 * C v first, then f0 + f1 (f1
+// dies), (f0 + f1) * (A + (B + C) v), then f0 * (A + B v) (f0 dies)
 TB_HD TB_INLINE fp12 fp12_mul_by_line_i(const fp12& f, const fp2& A, const fp2& B, const fp2& C) {
-  fp6 t0 = fp6_mul_by_01(f.c0, A, B);
-  fp6 t1 = fp6_mul_by_1(f.c1, C);
-  fp6 c1 = fp6_sub(fp6_sub(fp6_mul_by_01(fp6_add(f.c0, f.c1), A, fp2_add(B, C)), t0), t1);
-  fp6 c0 = fp6_add(t0, fp6_mul_v(t1));
+  const fp6 t1 = {fp2_mul_xi(m2(f.c1.c2, C)), m2(f.c1.c0, C), m2(f.c1.c1, C)};
+  const fp6 s = fp6_add(f.c0, f.c1);
+  const fp2 BC = fp2_add(B, C);
+  TB_FENCE();
+  const fp6 u = fp6_mul_by_01_f(s, A, BC);
+  const fp6 t0 = fp6_mul_by_01_f(f.c0, A, B);
+  const fp6 c1 = fp6_sub(fp6_sub(u, t0), t1);
+  const fp6 c0 = fp6_add(t0, fp6_mul_v(t1));
   return {c0, c1};
 }
 
@@ -75,7 +126,60 @@ __device__ TB_INLINE line3 line_load(const uint4* __restrict__ lines, uint32_t n
   return l;
 }
 
-__device__ TB_NOINLINE line3 add_step_leaf(g2p& T, const g2a& Q, const g1a& P) { return miller_add_step(T, Q, P); }
+
+__device__ TB_INLINE fp2 s2(const fp2& a) {
+  const fp2 r = fp2_sqr(a);
+  TB_FENCE();
+  return r;
+}
+
+__device__ TB_INLINE fp2 mf(const fp2& a, const fp& b) {
+  const fp2 r = fp2_mul_fp(a, b);
+  TB_FENCE();
+  return r;
+}
+
+// tb_pairing.h miller_add_step (T + Q, Q affine, chord line at P), fenced
+__device__ TB_INLINE line3 add_step_f(g2p& T, const g2a& Q, const g1a& P) {
+  const fp2 theta = fp2_sub(T.y, m2(Q.y, T.z));
+  const fp2 lambda = fp2_sub(T.x, m2(Q.x, T.z));
+  const fp2 c = s2(theta);
+  const fp2 d = s2(lambda);
+  const fp2 e = m2(lambda, d);
+  const fp2 f = m2(T.z, c);
+  const fp2 g = m2(T.x, d);
+  const fp2 h = fp2_sub(fp2_add(e, f), fp2_dbl(g));
+  line3 l;
+  l.a = fp2_sub(m2(theta, Q.x), m2(lambda, Q.y));
+  l.b = fp2_neg(mf(theta, P.x));
+  l.c = mf(lambda, P.y);
+  T.y = fp2_sub(m2(theta, fp2_sub(g, h)), m2(e, T.y));
+  T.x = m2(lambda, h);
+  T.z = m2(T.z, e);
+  return l;
+}
+
+// tb_pairing.h miller_dbl_step as a fenced sequence ordered so that Y, Z and
+// X die as early as the formulas allow
+__device__ TB_INLINE line3 dbl_step_f(g2p& T, const g1a& P) {
+  const fp2 B = s2(T.y);
+  const fp2 C = s2(T.z);
+  const fp2 H = fp2_sub(s2(fp2_add(T.y, T.z)), fp2_add(B, C));
+  const fp2 A = fp2_half(m2(T.x, T.y));
+  const fp2 J = s2(T.x);
+  const fp2 E = fp2_mul_3b(C);
+  const fp2 F = fp2_add(fp2_dbl(E), E);
+  const fp2 G = fp2_half(fp2_add(B, F));
+  const fp2 EE = s2(E);
+  line3 l;
+  l.a = fp2_sub(E, B);
+  l.b = mf(fp2_add(fp2_dbl(J), J), P.x);
+  l.c = fp2_neg(mf(H, P.y));
+  T.x = m2(A, fp2_sub(B, F));
+  T.z = m2(B, H);
+  T.y = fp2_sub(s2(G), fp2_add(fp2_dbl(EE), EE));
+  return l;
+}
 }  // namespace
 
 extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_MIN_WAVES)
@@ -88,8 +192,8 @@ extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_MIN_WAVES)
   g2p T = {Q[i].x, Q[i].y, fp2_one()};
   int s = 0;
   TB_NOUNROLL for (int b = 62; b >= 0; --b) {
-    line_store(lines, n, i, s++, miller_dbl_step(T, p));
-    if ((X_ABS >> b) & 1) line_store(lines, n, i, s++, add_step_leaf(T, Q[i], p));
+    line_store(lines, n, i, s++, dbl_step_f(T, p));
+    if ((X_ABS >> b) & 1) line_store(lines, n, i, s++, add_step_f(T, Q[i], p));
   }
 }
 
