@@ -59,7 +59,7 @@ STAGE_KERNEL = {
     "set_pk": "k_set_pk",
     "set_sig": "k_sig_check",
     "set_hash": "k_set_hash",
-    "g2_sum": "k_msm_bucket + k_msm_bucket_pairs",
+    "g2_sum": "k_msm_bucket + k_msm_bucket_sum + k_msm_bitsum_pairs",
     "miller": "k_miller_lines + k_miller_acc2",
     "fp12_prod": "k_fp12_prod_wave",
 }
@@ -298,6 +298,75 @@ def extra_configs(device, stream, reps):
     return out
 
 
+def kzg_leg(device, reps, cpu_sample):
+    """EIP-4844 KZG: verifyBlobKzgProofBatch on the
+    reference's trusted setup (tests/golden/kzg/trusted_setup.txt), seeded
+    random blobs, commitments and proofs made by the GPU prover.  Reports the
+    host-API latency at 1 and 6 blobs (Deneb's per-block maximum, PCIe
+    included), device-resident throughput at 64 and 512 blobs with per-stage
+    kernel times, and the C oracle's per-blob time (1 thread) on a sample."""
+    from teku_amd import kzg
+
+    setup = os.path.join(ROOT, "tests", "golden", "kzg", "trusted_setup.txt")
+    ck = kzg.CKZG4844.get_instance()
+    ck.load_trusted_setup(setup)
+    import random
+
+    def blob(seed):
+        rnd = random.Random(seed)
+        return b"".join(rnd.randrange(kzg.BLS_MODULUS).to_bytes(32, "big") for _ in range(4096))
+
+    base = [blob(9000 + i) for i in range(64)]
+    cs = ck.blobs_to_kzg_commitments(base)
+    t0 = time.perf_counter()
+    ps = [ck.compute_blob_kzg_proof(b, c) for b, c in zip(base[:8], cs[:8])]
+    prove_ms = (time.perf_counter() - t0) * 1e3 / 8
+    ps += [ck.compute_blob_kzg_proof(b, c) for b, c in zip(base[8:], cs[8:])]
+    t0 = time.perf_counter()
+    ck.blobs_to_kzg_commitments(base)
+    commit_ms = (time.perf_counter() - t0) * 1e3 / 64
+    out = {"what": "verify_blob_kzg_proof_batch (CKZG4844.verifyBlobKzgProofBatch) on the reference trusted setup, seeded blobs",
+           "commit_ms_per_blob_64": commit_ms, "prove_ms_per_blob": prove_ms}
+    for n in (1, 6):
+        assert ck.verify_blob_kzg_proof_batch(base[:n], cs[:n], ps[:n])
+        lat = timed(lambda: ck.verify_blob_kzg_proof_batch(base[:n], cs[:n], ps[:n]), reps)
+        out[f"p50_ms_{n}"] = statistics.median(lat)
+        out[f"p99_ms_{n}"] = pct(lat, 0.99)
+    L = kzg.lib()
+    ok = ctypes.c_int(0)
+    st = (ctypes.c_float * 6)()
+    for n in (64, 512):
+        reps_n = [i % 64 for i in range(n)]
+        db = torch.tensor(bytearray(b"".join(base[i] for i in reps_n)), dtype=torch.uint8, device=device)
+        dc = torch.tensor(bytearray(b"".join(cs[i] for i in reps_n)), dtype=torch.uint8, device=device)
+        dp = torch.tensor(bytearray(b"".join(ps[i] for i in reps_n)), dtype=torch.uint8, device=device)
+        torch.cuda.synchronize()
+
+        def run():
+            kzg._check(L.tkzg_dev_verify_blob_kzg_proof_batch(ctypes.byref(ok), db.data_ptr(), dc.data_ptr(), dp.data_ptr(), n, None))
+            assert ok.value == 1
+
+        run()
+        lat = timed(run, max(3, reps // 4))
+        med = statistics.median(lat)
+        stage = dict(zip(kzg.STAGES, list(st) if L.tkzg_last_stage_ms(st) == 0 else []))
+        out[f"dev_{n}"] = {"ms": med, "blobs_per_s": n / (med * 1e-3), "stage_ms": stage,
+                           # the challenge kernel streams the blobs once: 131,152 B of transcript per blob
+                           "challenge_hbm_GBps": n * 131152 / (stage.get("challenge", 0) * 1e-3) / 1e9 if stage.get("challenge") else None}
+    if cpu_sample:
+        from oracle import kzg_oracle as K
+
+        s = K.Setup.from_file(setup)
+        t0 = time.perf_counter()
+        assert s.verify_blob_kzg_proof_batch(base[:2], cs[:2], ps[:2]) is True
+        cpu_s = time.perf_counter() - t0
+        s.close()
+        out["cpu_baseline"] = {"value": 2 / cpu_s, "unit": "blobs/s", "cores": 1, "kind": "port",
+                               "sample": "2-blob verify_blob_kzg_proof_batch through the C oracle (spec restatement: one Fermat "
+                                         "inversion per barycentric term, 8-bit-window Pippenger), one thread"}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -309,6 +378,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip configs 2/3/4")
     ap.add_argument("--serial", action="store_true", help="timed steps with every stage alone on the stream (profiling)")
+    ap.add_argument("--no-kzg", action="store_true", help="skip the KZG leg (SURVEY.md 8(f) rank 4)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -424,6 +494,7 @@ def main():
             assert arr128.batch_verify(synth.random_multipliers(128), n_gpus=1)
         lat = timed(lambda: arr128.batch_verify(synth.random_multipliers(128), n_gpus=1), args.lat_reps)
     extra = {} if args.no_extra else extra_configs(device, stream, args.extra_reps)
+    kzg_out = None if args.no_kzg else kzg_leg(device, args.extra_reps, not args.no_cpu_baseline)
 
     cpu = None if args.no_cpu_baseline else cpu_baseline_oracle(pks, msgs, sigs, min(4096, S), min(512, S))
     line = {
@@ -456,6 +527,7 @@ def main():
         "stage_ms_exclusive": dict(zip(STAGES, excl)),
         "roofline": roofline,
         "configs": extra,
+        "kzg": kzg_out,
         "cpu_baseline": cpu,
         "workload_gen_s": gen_s,
     }

@@ -14,7 +14,9 @@ namespace tb {
 // ---------------------------------------------------------------------------
 TB_HD TB_INLINE uint32_t rotr32(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
 
-TB_HD TB_NOINLINE void sha256_compress(uint32_t st[8], const uint32_t blk[16]) {
+// The compression body, force-inlined where a caller keeps its next block's
+// loads in flight across it (k_kzg_challenge); sha256_compress is the call.
+TB_HD TB_INLINE void sha256_compress_i(uint32_t st[8], const uint32_t blk[16]) {
   uint32_t w[16];
   TB_UNROLL for (int i = 0; i < 16; i++) w[i] = blk[i];
   uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
@@ -53,6 +55,8 @@ TB_HD TB_NOINLINE void sha256_compress(uint32_t st[8], const uint32_t blk[16]) {
   st[6] += g;
   st[7] += h;
 }
+
+TB_HD TB_NOINLINE void sha256_compress(uint32_t st[8], const uint32_t blk[16]) { sha256_compress_i(st, blk); }
 
 // SHA-256 over a virtual byte string of length L (get(i) for i < L), starting
 // from state `st` that already absorbed `prefix_bytes` (a multiple of 64).
