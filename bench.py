@@ -87,8 +87,10 @@ def roofline_entry(stage_ms, S, device, ms_per_step):
     kernel = STAGE_KERNEL[name]
     traffic = None
     tpath = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(tpath):
-        traffic = json.load(open(tpath)).get(kernel, {}).get("bytes_per_launch")
+    if os.path.exists(tpath):  # HBM bytes per launch from the PMC passes, summed over the stage's kernels
+        tj = json.load(open(tpath))
+        parts = [tj.get(k.strip(), {}).get("bytes_per_launch") for k in kernel.split("+")]
+        traffic = sum(parts) if all(p is not None for p in parts) else None
     per_set = M_PER_UNIT.get("per_set_total")
     return {
         "bound": "valu-int (v_mad_u64_u32 issue)",
@@ -349,6 +351,7 @@ def kzg_leg(device, reps, cpu_sample):
         run()
         lat = timed(run, max(3, reps // 4))
         med = statistics.median(lat)
+        kzg._check(L.tkzg_dev_verify_blob_kzg_proof_batch_profiled(ctypes.byref(ok), db.data_ptr(), dc.data_ptr(), dp.data_ptr(), n, None))
         stage = dict(zip(kzg.STAGES, list(st) if L.tkzg_last_stage_ms(st) == 0 else []))
         out[f"dev_{n}"] = {"ms": med, "blobs_per_s": n / (med * 1e-3), "stage_ms": stage,
                            # the challenge kernel streams the blobs once: 131,152 B of transcript per blob
@@ -379,6 +382,7 @@ def main():
     ap.add_argument("--no-extra", action="store_true", help="skip configs 2/3/4")
     ap.add_argument("--serial", action="store_true", help="timed steps with every stage alone on the stream (profiling)")
     ap.add_argument("--no-kzg", action="store_true", help="skip the KZG leg (SURVEY.md 8(f) rank 4)")
+    ap.add_argument("--kzg-only", action="store_true", help="profiling: run only the KZG leg and print its JSON")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -386,6 +390,9 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
+    if args.kzg_only:
+        print(json.dumps(kzg_leg(device, args.extra_reps, False)), flush=True)
+        return
     if world > 1:
         dist.init_process_group("nccl", device_id=device)
     L = native.lib()

@@ -78,8 +78,13 @@ int tkzg_verify_kzg_proof(int* ok, const uint8_t commitment[48], const uint8_t z
 int tkzg_dev_verify_blob_kzg_proof_batch(int* ok, const uint8_t* d_blobs, const uint8_t* d_commitments, const uint8_t* d_proofs, size_t count,
                                          void* stream);
 
-/* Per-stage device timings of the last tkzg_dev_verify_blob_kzg_proof_batch
- * (ms): challenge, eval, points, transcript r, terms, pairing. */
+/* The same with every stage alone on the stream, bracketed by events (the
+ * overlapped call decodes the points on a second stream). */
+int tkzg_dev_verify_blob_kzg_proof_batch_profiled(int* ok, const uint8_t* d_blobs, const uint8_t* d_commitments, const uint8_t* d_proofs,
+                                                  size_t count, void* stream);
+
+/* Per-stage device timings of the last profiled call (ms): challenge, eval,
+ * points, transcript r, terms, pairing. */
 int tkzg_last_stage_ms(float ms[6]);
 
 /* Test hook: the batch's per-blob challenges z_i and evaluations y_i (32 bytes

@@ -23,7 +23,9 @@
 //                     - [sum r^i y_i] G1   (B is the spec's C_minus_y_lincomb +
 //                     proof_z_lincomb, with the y-terms merged into one
 //                     generator multiple)
-//   k_kzg_pairing     tree sums of A and B, then e(A, [tau]_2) e(-B, [1]_2) == 1
+//   k_kzg_pair_sums   tree sums of A and B; then the BLS path's k_miller_wave
+//                     (one wave per pair) and k_final_verify_wave check
+//                     e(A, [tau]_2) e(-B, [1]_2) == 1
 // Prover side (blob_to_kzg_commitment, compute_kzg_proof_impl):
 //   k_kzg_quotient (+ k_kzg_quotient_domain), k_kzg_lincomb_terms,
 //   k_kzg_lincomb_reduce: g1_lincomb over the bit-reversed Lagrange points.
@@ -279,13 +281,83 @@ extern "C" __global__ void __launch_bounds__(TB_BLOCK) k_kzg_batch_r(const uint8
   r[0] = fr_from_digest(fr_plain_from_bewords(st));
 }
 
-// [k]P, k in Montgomery form, P affine finite: MSB-first double-and-add over 255 bits
+// GLV split of a scalar k < r (plain limbs): k = a + b mu with a, b < 2^128,
+// mu = z^2 the eigenvalue of phi(-P) = (beta x, -y) on G1.
+// b = floor(k GLV_M / 2^384) (GLV_M = floor(2^384 / mu)) underestimates
+// floor(k / mu) by at most 2; a = k - b mu is then corrected into [0, mu).
+__device__ __forceinline__ void glv_split(const fr& k, uint32_t (&a)[4], uint32_t (&b)[4]) {
+  uint32_t prod[17];
+  TB_UNROLL for (int i = 0; i < 17; i++) prod[i] = 0;
+  TB_UNROLL for (int i = 0; i < 8; i++) {
+    uint64_t c = 0;
+    TB_UNROLL for (int j = 0; j < 9; j++) {
+      c = (uint64_t)k.l[i] * GLV_M[j] + prod[i + j] + (c >> 32);
+      prod[i + j] = (uint32_t)c;
+    }
+    prod[i + 9] = (uint32_t)(c >> 32);
+  }
+  uint32_t q[5];
+  TB_UNROLL for (int i = 0; i < 5; i++) q[i] = prod[12 + i];
+  // rem = k - q mu (8 limbs; q mu <= k)
+  uint32_t qm[9];
+  TB_UNROLL for (int i = 0; i < 9; i++) qm[i] = 0;
+  TB_UNROLL for (int i = 0; i < 5; i++) {
+    uint64_t c = 0;
+    TB_UNROLL for (int j = 0; j < 4; j++) {
+      if (i + j < 9) {
+        c = (uint64_t)q[i] * GLV_MU[j] + qm[i + j] + (c >> 32);
+        qm[i + j] = (uint32_t)c;
+      }
+    }
+    if (i + 4 < 9) qm[i + 4] = (uint32_t)(c >> 32);
+  }
+  uint32_t rem[8], br = 0;
+  TB_UNROLL for (int i = 0; i < 8; i++) {
+    const uint64_t d = (uint64_t)k.l[i] - qm[i] - br;
+    rem[i] = (uint32_t)d;
+    br = (uint32_t)(d >> 63);
+  }
+  TB_UNROLL for (int it = 0; it < 2; it++) {  // rem >= mu ? rem -= mu, q += 1
+    uint32_t t[8], bw = 0;
+    TB_UNROLL for (int i = 0; i < 8; i++) {
+      const uint64_t d = (uint64_t)rem[i] - (i < 4 ? GLV_MU[i] : 0u) - bw;
+      t[i] = (uint32_t)d;
+      bw = (uint32_t)(d >> 63);
+    }
+    const bool ge = bw == 0;
+    uint32_t cq = ge ? 1u : 0u;
+    TB_UNROLL for (int i = 0; i < 8; i++) rem[i] = ge ? t[i] : rem[i];
+    TB_UNROLL for (int i = 0; i < 5; i++) {
+      const uint64_t s = (uint64_t)q[i] + cq;
+      q[i] = (uint32_t)s;
+      cq = (uint32_t)(s >> 32);
+    }
+  }
+  TB_UNROLL for (int i = 0; i < 4; i++) {
+    a[i] = rem[i];
+    b[i] = q[i];
+  }
+}
+
+// [k]P, k in Montgomery form, P affine finite: [a]P + [b]phi(-P) by a joint
+// MSB-first double-and-add over 128 bits (addends P, phi(-P), P + phi(-P),
+// all affine) -- 128 doublings instead of 255.
 __device__ __forceinline__ g1j g1_mul_fr(const g1a& P, const fr& k_mont) {
-  const fr k = fr_from_mont(k_mont);
+  uint32_t a[4], b[4];
+  glv_split(fr_from_mont(k_mont), a, b);
+  g1a Q;
+  Q.x = fp_mul(P.x, fp_from_const(BETA));
+  Q.y = fp_neg(P.y);
+  g1a S;
+  (void)jac_to_aff(S, jac_add_aff(jac_from_aff(P), Q));  // P + [mu]P: never infinity (1 + mu != 0 mod r)
   g1j acc = jac_inf<fp>();
-  TB_NOUNROLL for (int i = 254; i >= 0; --i) {
+  TB_NOUNROLL for (int i = 127; i >= 0; --i) {
     acc = jac_dbl_i(acc);
-    if ((k.l[i >> 5] >> (i & 31)) & 1u) acc = jac_add_aff_i(acc, P);
+    const bool ba = (a[i >> 5] >> (i & 31)) & 1u, bb = (b[i >> 5] >> (i & 31)) & 1u;
+    if (ba || bb) {
+      const g1a T = ba ? (bb ? S : P) : Q;
+      acc = jac_add_aff_i(acc, T);
+    }
   }
   return acc;
 }
@@ -321,12 +393,15 @@ extern "C" __global__ void __launch_bounds__(TB_BLOCK) k_kzg_terms(const g1a* __
   T[k] = inf[pi] ? jac_inf<fp>() : g1_mul_fr(pts[pi], s);
 }
 
-// A = sum T[0, n), B = sum T[n, 3n]; ok = e(A, [tau]_2) e(-B, [1]_2) == 1
-extern "C" __global__ void __launch_bounds__(256) k_kzg_pairing(const g1j* __restrict__ T, uint32_t n, const g2a* __restrict__ tau2,
-                                                                 int* __restrict__ ok) {
+// A = sum T[0, n), B = sum T[n, 3n], as the two pairs of the check
+// e(A, [tau]_2) e(-B, [1]_2) == 1 in the layout of the BLS path's wave kernels
+// (k_miller_wave over P/Q/skip, then k_final_verify_wave on the product):
+// P = {A, -B}, Q = {[tau]_2, [1]_2}, skip = infinity, zero = 4 zero bytes
+// (the pair codes and the invalid count those kernels also read).
+extern "C" __global__ void __launch_bounds__(256) k_kzg_pair_sums(const g1j* __restrict__ T, uint32_t n, const g2a* __restrict__ tau2,
+                                                                   g1a* __restrict__ P, g2a* __restrict__ Q, uint8_t* __restrict__ skip,
+                                                                   uint32_t* __restrict__ zero) {
   __shared__ g1j s_p[256];
-  __shared__ g1a s_aff[2];
-  __shared__ int s_inf[2];
   const uint32_t t = threadIdx.x;
   TB_NOUNROLL for (int side = 0; side < 2; side++) {
     const uint32_t lo = side == 0 ? 0u : n, hi = side == 0 ? n : 3u * n + 1u;
@@ -341,17 +416,17 @@ extern "C" __global__ void __launch_bounds__(256) k_kzg_pairing(const g1j* __res
     if (t == 0) {
       g1a a;
       const bool fin = jac_to_aff(a, side == 0 ? s_p[0] : jac_neg(s_p[0]));
-      s_aff[side] = a;
-      s_inf[side] = fin ? 0 : 1;
+      P[side] = a;
+      skip[side] = fin ? 0 : 1;
     }
     __syncthreads();
   }
-  if (t != 0) return;
-  g2a g2;
-  g2.x = fp2_from_const(G2_X);
-  g2.y = fp2_from_const(G2_Y);
-  const fp12 f = miller_loop2(s_aff[0], tau2[0], s_inf[0] != 0, s_aff[1], g2, s_inf[1] != 0);
-  ok[0] = fp12_is_one(final_exp(f)) ? 1 : 0;
+  if (t == 0) {
+    Q[0] = tau2[0];
+    Q[1].x = fp2_from_const(G2_X);
+    Q[1].y = fp2_from_const(G2_Y);
+    zero[0] = 0;
+  }
 }
 
 // ---------------------------------------------------------------------------

@@ -86,8 +86,8 @@ struct carve {
 struct kzg_state {
   std::mutex mu;
   bool loaded = false;
-  hipStream_t s = nullptr;
-  hipEvent_t ev[7] = {};
+  hipStream_t s = nullptr, s2 = nullptr;  // s2: the point decoding, overlapped with the challenges
+  hipEvent_t ev[7] = {}, fork = nullptr, join = nullptr;
   g1a* lag = nullptr;
   uint8_t* lag_inf = nullptr;
   fr* roots = nullptr;
@@ -106,10 +106,38 @@ kzg_state& st() {
 
 uint32_t blocks(size_t n, uint32_t b) { return (uint32_t)((n + b - 1) / b); }
 
+constexpr size_t PAIR_WS_BYTES = 2 * sizeof(g1a) + 2 * sizeof(g2a) + 16 + 16 + 2 * sizeof(fp12) + 5 * 16;
+
 // worst-case workspace for a verify of n blobs (besides the inputs)
 size_t verify_ws_bytes(size_t n) {
   return align16(2 * n * sizeof(g1a)) + align16(2 * n) + align16(2 * n) + 2 * align16(n * sizeof(fr)) + align16(n) +
-         align16(32 + 160 * n) + align16(sizeof(fr)) + align16((3 * n + 1) * sizeof(g1j)) + align16(sizeof(int)) + 64;
+         align16(32 + 160 * n) + align16(sizeof(fr)) + align16((3 * n + 1) * sizeof(g1j)) + align16(sizeof(int)) + 64 + PAIR_WS_BYTES;
+}
+
+// e(A, [tau]_2) e(-B, [1]_2) == 1 from the term buffer T (n blobs): pair sums,
+// one wave per Miller loop, one wave for the product + final exponentiation
+struct pair_ws {
+  g1a* P;
+  g2a* Q;
+  uint8_t* skip;
+  uint32_t* zero;
+  fp12* f;
+};
+pair_ws take_pair_ws(carve& c) {
+  pair_ws p;
+  p.P = c.take<g1a>(2);
+  p.Q = c.take<g2a>(2);
+  p.skip = c.take<uint8_t>(16);
+  p.zero = c.take<uint32_t>(4);
+  p.f = c.take<fp12>(2);
+  return p;
+}
+
+void launch_pairing(kzg_state& g, const g1j* T, uint32_t n, const pair_ws& p, int* ok, hipStream_t s) {
+  hipLaunchKernelGGL(k_kzg_pair_sums, dim3(1), dim3(256), 0, s, T, n, (const g2a*)(g.g2 + 1), p.P, p.Q, p.skip, p.zero);
+  const uint8_t* z8 = reinterpret_cast<const uint8_t*>(p.zero);
+  hipLaunchKernelGGL(k_miller_wave, dim3(2), dim3(64), 0, s, (const g1a*)p.P, (const g2a*)p.Q, (const uint8_t*)p.skip, z8, z8, 2u, p.f);
+  hipLaunchKernelGGL(k_final_verify_wave, dim3(1), dim3(64), 0, s, (const fp12*)p.f, 2u, (const uint32_t*)p.zero, ok);
 }
 
 // The verification on device-resident inputs: ok_host <- verdict, or BADARGS
@@ -126,15 +154,27 @@ int verify_dev(kzg_state& g, const uint8_t* d_blobs, const uint8_t* d_com, const
   fr* r = c.take<fr>(1);
   g1j* T = c.take<g1j>(3 * n + 1);
   int* ok = c.take<int>(1);
+  const pair_ws pw = take_pair_ws(c);
   const uint32_t un = (uint32_t)n;
   if (timed) KCHK(hipEventRecord(g.ev[0], s));
+  // the point decoding (independent of the challenges) on s2 unless timing the stages one by one
+  hipStream_t sp = timed ? s : g.s2;
+  if (!timed) {
+    KCHK(hipEventRecord(g.fork, s));
+    KCHK(hipStreamWaitEvent(sp, g.fork, 0));
+    hipLaunchKernelGGL(k_kzg_points, dim3(blocks(n, TB_BLOCK)), dim3(TB_BLOCK), 0, sp, d_com, un, pts, pinf, codes);
+    hipLaunchKernelGGL(k_kzg_points, dim3(blocks(n, TB_BLOCK)), dim3(TB_BLOCK), 0, sp, d_proof, un, pts + n, pinf + n, codes + n);
+    KCHK(hipEventRecord(g.join, sp));
+  }
   hipLaunchKernelGGL(k_kzg_challenge, dim3(blocks(n, TB_BLOCK)), dim3(TB_BLOCK), 0, s, d_blobs, d_com, un, z);
   if (timed) KCHK(hipEventRecord(g.ev[1], s));
   hipLaunchKernelGGL(k_kzg_eval, dim3(un), dim3(256), 0, s, d_blobs, un, z, g.roots, (fr*)nullptr, y, codes + 2 * n);
-  if (timed) KCHK(hipEventRecord(g.ev[2], s));
-  hipLaunchKernelGGL(k_kzg_points, dim3(blocks(n, TB_BLOCK)), dim3(TB_BLOCK), 0, s, d_com, un, pts, pinf, codes);
-  hipLaunchKernelGGL(k_kzg_points, dim3(blocks(n, TB_BLOCK)), dim3(TB_BLOCK), 0, s, d_proof, un, pts + n, pinf + n, codes + n);
-  if (timed) KCHK(hipEventRecord(g.ev[3], s));
+  if (timed) {
+    KCHK(hipEventRecord(g.ev[2], s));
+    hipLaunchKernelGGL(k_kzg_points, dim3(blocks(n, TB_BLOCK)), dim3(TB_BLOCK), 0, s, d_com, un, pts, pinf, codes);
+    hipLaunchKernelGGL(k_kzg_points, dim3(blocks(n, TB_BLOCK)), dim3(TB_BLOCK), 0, s, d_proof, un, pts + n, pinf + n, codes + n);
+    KCHK(hipEventRecord(g.ev[3], s));
+  }
   if (n > 1) {
     hipLaunchKernelGGL(k_kzg_records, dim3(blocks(n, TB_BLOCK)), dim3(TB_BLOCK), 0, s, d_com, d_proof, z, y, un, rec);
     hipLaunchKernelGGL(k_kzg_batch_r, dim3(1), dim3(TB_BLOCK), 0, s, rec, (uint32_t)(32 + 160 * n), r);
@@ -142,9 +182,10 @@ int verify_dev(kzg_state& g, const uint8_t* d_blobs, const uint8_t* d_com, const
     KCHK(hipMemsetAsync(r, 0, sizeof(fr), s));
   }
   if (timed) KCHK(hipEventRecord(g.ev[4], s));
+  if (!timed) KCHK(hipStreamWaitEvent(s, g.join, 0));
   hipLaunchKernelGGL(k_kzg_terms, dim3(blocks(3 * n + 1, TB_BLOCK)), dim3(TB_BLOCK), 0, s, pts, pinf, z, y, r, un, T);
   if (timed) KCHK(hipEventRecord(g.ev[5], s));
-  hipLaunchKernelGGL(k_kzg_pairing, dim3(1), dim3(256), 0, s, T, un, g.g2 + 1, ok);
+  launch_pairing(g, T, un, pw, ok, s);
   if (timed) KCHK(hipEventRecord(g.ev[6], s));
   KCHK(hipGetLastError());
   // verdict + codes back through the pinned stage
@@ -285,7 +326,10 @@ extern "C" int tkzg_load_trusted_setup(const uint8_t* g1_monomial, size_t g1_mon
   if (g.loaded) free_setup(g);  // CKZG4844.loadTrustedSetup frees the previous one first (CKZG4844.java:64-72)
   if (!g.s) {
     KCHK(hipStreamCreateWithFlags(&g.s, hipStreamNonBlocking));
+    KCHK(hipStreamCreateWithFlags(&g.s2, hipStreamNonBlocking));
     for (auto& e : g.ev) KCHK(hipEventCreate(&e));
+    KCHK(hipEventCreateWithFlags(&g.fork, hipEventDisableTiming));
+    KCHK(hipEventCreateWithFlags(&g.join, hipEventDisableTiming));
   }
   // device: [lag | lag_inf | roots | g2 | g2_inf]  scratch: [bytes in | codes]
   const size_t persist = align16(N * sizeof(g1a)) + align16(N) + align16(N * sizeof(fr)) + align16(NG2 * sizeof(g2a)) + align16(NG2);
@@ -358,16 +402,26 @@ extern "C" int tkzg_verify_blob_kzg_proof(int* ok, const uint8_t* blob, size_t b
   });
 }
 
-extern "C" int tkzg_dev_verify_blob_kzg_proof_batch(int* ok, const uint8_t* d_blobs, const uint8_t* d_commitments, const uint8_t* d_proofs,
-                                                    size_t count, void* stream) {
+static int dev_verify(int* ok, const uint8_t* d_blobs, const uint8_t* d_commitments, const uint8_t* d_proofs, size_t count, void* stream,
+                      bool timed) {
   return with_setup([&](kzg_state& g) {
     if (count == 0) {
       *ok = 1;
       return (int)TKZG_OK;
     }
     if (g.ws.ensure(verify_ws_bytes(count))) return fail(TKZG_MALLOC, "workspace allocation failed");
-    return verify_dev(g, d_blobs, d_commitments, d_proofs, count, stream ? (hipStream_t)stream : g.s, g.ws.b(), ok, true);
+    return verify_dev(g, d_blobs, d_commitments, d_proofs, count, stream ? (hipStream_t)stream : g.s, g.ws.b(), ok, timed);
   });
+}
+
+extern "C" int tkzg_dev_verify_blob_kzg_proof_batch(int* ok, const uint8_t* d_blobs, const uint8_t* d_commitments, const uint8_t* d_proofs,
+                                                    size_t count, void* stream) {
+  return dev_verify(ok, d_blobs, d_commitments, d_proofs, count, stream, false);
+}
+
+extern "C" int tkzg_dev_verify_blob_kzg_proof_batch_profiled(int* ok, const uint8_t* d_blobs, const uint8_t* d_commitments,
+                                                             const uint8_t* d_proofs, size_t count, void* stream) {
+  return dev_verify(ok, d_blobs, d_commitments, d_proofs, count, stream, true);
 }
 
 extern "C" int tkzg_blobs_to_kzg_commitments(uint8_t* out, const uint8_t* blobs, size_t blobs_len, size_t n) {
@@ -430,7 +484,7 @@ extern "C" int tkzg_compute_kzg_proof(uint8_t proof_out[48], uint8_t y_out[32], 
 
 extern "C" int tkzg_verify_kzg_proof(int* ok, const uint8_t commitment[48], const uint8_t z_b[32], const uint8_t y_b[32], const uint8_t proof[48]) {
   return with_setup([&](kzg_state& g) {
-    if (g.ws.ensure(512 + verify_ws_bytes(1)) || g.stage.ensure(256)) return fail(TKZG_MALLOC, "workspace allocation failed");
+    if (g.ws.ensure(1024 + verify_ws_bytes(1)) || g.stage.ensure(256)) return fail(TKZG_MALLOC, "workspace allocation failed");
     carve c{g.ws.b()};
     uint8_t* d_in = c.take<uint8_t>(256);  // commitment | proof | z | y
     uint8_t* codes = c.take<uint8_t>(8);
@@ -439,6 +493,7 @@ extern "C" int tkzg_verify_kzg_proof(int* ok, const uint8_t commitment[48], cons
     uint8_t* pinf = c.take<uint8_t>(2);
     g1j* T = c.take<g1j>(4);
     int* d_ok = c.take<int>(1);
+    const pair_ws pw = take_pair_ws(c);
     uint8_t* h = g.stage.b();
     memcpy(h, commitment, 48);
     memcpy(h + 48, proof, 48);
@@ -448,7 +503,7 @@ extern "C" int tkzg_verify_kzg_proof(int* ok, const uint8_t commitment[48], cons
     hipLaunchKernelGGL(k_kzg_points, dim3(1), dim3(TB_BLOCK), 0, g.s, d_in, 2u, pts, pinf, codes);
     hipLaunchKernelGGL(k_kzg_scalars_in, dim3(1), dim3(TB_BLOCK), 0, g.s, d_in + 96, 2u, zy, codes + 2);
     hipLaunchKernelGGL(k_kzg_terms, dim3(1), dim3(TB_BLOCK), 0, g.s, pts, pinf, zy, zy + 1, zy, 1u, T);
-    hipLaunchKernelGGL(k_kzg_pairing, dim3(1), dim3(256), 0, g.s, T, 1u, g.g2 + 1, d_ok);
+    launch_pairing(g, T, 1u, pw, d_ok, g.s);
     KCHK(hipGetLastError());
     KCHK(hipStreamSynchronize(g.s));
     KCHK(hipMemcpyAsync(h, d_ok, sizeof(int), hipMemcpyDeviceToHost, g.s));

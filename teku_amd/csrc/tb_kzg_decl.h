@@ -15,7 +15,7 @@ __global__ void k_kzg_scalars_out(const tb::fr* in, uint32_t n, uint8_t* be);
 __global__ void k_kzg_records(const uint8_t* commitments, const uint8_t* proofs, const tb::fr* z, const tb::fr* y, uint32_t n, uint8_t* rec);
 __global__ void k_kzg_batch_r(const uint8_t* rec, uint32_t len, tb::fr* r);
 __global__ void k_kzg_terms(const tb::g1a* pts, const uint8_t* inf, const tb::fr* z, const tb::fr* y, const tb::fr* r, uint32_t n, tb::g1j* T);
-__global__ void k_kzg_pairing(const tb::g1j* T, uint32_t n, const tb::g2a* tau2, int* ok);
+__global__ void k_kzg_pair_sums(const tb::g1j* T, uint32_t n, const tb::g2a* tau2, tb::g1a* P, tb::g2a* Q, uint8_t* skip, uint32_t* zero);
 __global__ void k_kzg_quotient(const tb::fr* poly, const tb::fr* z, const tb::fr* y, const tb::fr* roots, uint32_t n_blobs, tb::fr* q);
 __global__ void k_kzg_quotient_domain(const tb::fr* poly, const tb::fr* z, const tb::fr* y, const tb::fr* roots, tb::fr* q);
 __global__ void k_kzg_lincomb_terms(const tb::fr* sc, const tb::g1a* lag, const uint8_t* lag_inf, uint32_t n_blobs, tb::g1j* T);

@@ -48,6 +48,7 @@ _SIGS = {
     "tkzg_compute_kzg_proof": (ctypes.c_int, [_u8p, _u8p, _u8p, _sz, _u8p]),
     "tkzg_verify_kzg_proof": (ctypes.c_int, [_ip, _u8p, _u8p, _u8p, _u8p]),
     "tkzg_dev_verify_blob_kzg_proof_batch": (ctypes.c_int, [_ip, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, _sz, ctypes.c_void_p]),
+    "tkzg_dev_verify_blob_kzg_proof_batch_profiled": (ctypes.c_int, [_ip, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, _sz, ctypes.c_void_p]),
     "tkzg_last_stage_ms": (ctypes.c_int, [ctypes.POINTER(ctypes.c_float)]),
     "tkzg_last_transcript": (ctypes.c_int, [_u8p, _u8p, _sz, _u8p]),
     "tkzg_last_error": (ctypes.c_char_p, []),
