@@ -222,7 +222,9 @@ __device__ TB_INLINE void miller_acc_body(const uint4* __restrict__ lines, const
   }
   fp12 f = fp12_one();
   int s = 0;
-  auto extra = [&](int step) {
+  // always_inline: an outlined call here (one per step) made the caller save
+  // and restore its live accumulator registers through scratch every step
+  auto extra = [&](int step) __attribute__((always_inline)) {
     if (!n_extra) return;
     const uint32_t e = (t + T - (uint32_t)(step * n_extra) % T) % T;
     if (e < n_extra && xskip[e] == 0) {

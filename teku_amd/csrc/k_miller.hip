@@ -1,29 +1,8 @@
-// Miller loops: two pairs per Fp12 accumulator (k_miller2), one pair per
-// thread (k_miller1) and one pair per 64-lane wave (k_miller_wave).
+// Fused Miller loops: two pairs per Fp12 accumulator (k_miller2) and one pair
+// per thread (k_miller1); the wave-parallel loop is in k_mwave.hip.
 #include "tb_kdecl.h"
 
 using namespace tb;
-
-// Wave-parallel Miller loop (tb_fp12_wave.h miller_loop_wave): one pair per
-// 64-lane workgroup -- the small-batch path, where one pair per thread leaves
-// the GPU idle and the per-pair serial chain is the latency.
-extern "C" __global__ void __launch_bounds__(64)
-    k_miller_wave(const g1a* __restrict__ P, const g2a* __restrict__ Q, const uint8_t* __restrict__ skip,
-                  const uint8_t* __restrict__ code_a, const uint8_t* __restrict__ code_b, uint32_t n, fp12* __restrict__ f) {
-  __shared__ miller_lds L;
-  const uint32_t i = blockIdx.x;
-  if (i >= n) return;
-  tb_latency_prio();
-  const bool s0 = skip[i] != 0 || code_a[i] != 0 || code_b[i] != 0;
-  fp* out = reinterpret_cast<fp*>(f + i);
-  if (s0) {
-    if (threadIdx.x < 12) out[threadIdx.x] = threadIdx.x == 0 ? fp_one() : fp_zero();
-    return;
-  }
-  w12_tabs_load(L.s);
-  miller_loop_wave(L, P[i], Q[i]);
-  if (threadIdx.x < 12) out[threadIdx.x] = L.F[threadIdx.x];
-}
 
 // ---------------------------------------------------------------------------
 // One-pair-per-thread and two-pairs-per-thread Miller loops with every step

@@ -18,9 +18,12 @@ namespace tb {
 // coefficient tables (staged from W12_ALL once per kernel by w12_tabs_load, so
 // the lane-varying table reads are LDS reads, not global loads).
 #define W12_QP 5  // lanes per output coordinate in the post-combination
+struct u13 {
+  uint32_t l[13];
+};
 struct wave12_scratch {
   fp prod[64];
-  fp part[12 * W12_QP];
+  u13 part[12 * W12_QP];
   uint16_t tab[W12_ALL_N];
 };
 
@@ -29,22 +32,87 @@ __device__ TB_INLINE void w12_tabs_load(wave12_scratch& s) {
   __syncthreads();
 }
 
-// sum_{t in [b, e)} +-src[idx_t]; entries (idx << 1) | negative; at most
-// MAXLEN terms (unrolled and predicated so the LDS reads issue early)
+// Lazy sums.  The pre- and post-combinations add up to 8 signed terms, each a
+// weakly reduced value in [0, 2p).  Instead of a reduced fp_add per term
+// (add, trial subtraction, select, and a negation for the signed ones) they
+// accumulate on 13 x 32-bit limbs: acc = K * 2p + sum(+-v), with -v added as
+// ~v + 1 (two's complement, exact mod 2^416), K = the term count bound, so
+// the true value is in [0, 4Kp) < 2^386.  Such a value is a valid Montgomery
+// operand as is (mont29 takes any 14 x 29-bit input; the output is < 2p), and
+// the post-combination reduces it once per output coordinate (reduce13).
+template <int K>
+__device__ TB_INLINE u13 u13_kp2() {  // K * 2p, constant-folded
+  u13 r;
+  uint64_t c = 0;
+  TB_UNROLL for (int i = 0; i < 12; i++) {
+    c += (uint64_t)P2_MOD[i] * K;
+    r.l[i] = (uint32_t)c;
+    c >>= 32;
+  }
+  r.l[12] = (uint32_t)c;
+  return r;
+}
+
+__device__ TB_INLINE void u13_add(u13& acc, const u13& v) {
+  uint32_t c = 0;
+  TB_UNROLL for (int i = 0; i < 13; i++) acc.l[i] = addc32(acc.l[i], v.l[i], c, &c);
+}
+
+// acc += (x & 1 ? -src[x >> 1] : src[x >> 1]) over the entries [b, e) (at most
+// MAXLEN; unrolled and predicated so the LDS reads issue early)
 template <int MAXLEN>
-__device__ TB_INLINE fp w_sparse_sum(const fp* src, const uint16_t* ent, int b, int e) {
-  fp acc = fp_zero();
+__device__ TB_INLINE void w_lazy_sum(u13& acc, const fp* src, const uint16_t* ent, int b, int e) {
   TB_UNROLL for (int t = 0; t < MAXLEN; t++) {
     if (b + t < e) {
       const uint32_t x = ent[b + t];
       const fp v = src[x >> 1];
-      fp nv;
-      uint32_t br = 0;
-      TB_UNROLL for (int i = 0; i < 12; i++) nv.l[i] = subc32(P2_MOD[i], v.l[i], br, &br);  // 2p - v in (0, 2p]
-      acc = fp_add(acc, fp_sel((x & 1u) != 0, nv, v));
+      const uint32_t neg = x & 1u, m = 0u - neg;
+      uint32_t c = neg;
+      TB_UNROLL for (int i = 0; i < 12; i++) acc.l[i] = addc32(acc.l[i], v.l[i] ^ m, c, &c);
+      acc.l[12] = acc.l[12] + m + c;
     }
   }
-  return acc;
+}
+
+// Montgomery product of two 13-limb values < 2^406 (output < 2p)
+__device__ TB_INLINE fp fp_mul13(const u13& a, const u13& b) {
+  uint32_t x[1][14], y[1][14], z[1][14];
+  TB_UNROLL for (int i = 0; i < 14; i++) {
+    const int o = 29 * i, w = o >> 5, sh = o & 31;
+    uint32_t va = a.l[w] >> sh, vb = b.l[w] >> sh;
+    if (sh + 29 > 32 && w + 1 < 13) {
+      va |= a.l[w + 1] << (32 - sh);
+      vb |= b.l[w + 1] << (32 - sh);
+    }
+    x[0][i] = va & M29;
+    y[0][i] = vb & M29;
+  }
+  mont29<1, false>(z, x, y);
+  fp r;
+  from29(r, z[0]);
+  return r;
+}
+
+// v in [0, 2^390) -> v mod p in [0, 2p): q = floor(t C / 2^50) with t = v >> 352
+// and C = floor(2^50 / (p_352 + 1)) underestimates v / p by at most 2, so
+// v - q p is in [0, 3p); one conditional subtraction of p lands in [0, 2p).
+__device__ TB_INLINE fp reduce13(const u13& v) {
+  constexpr uint64_t PT = (uint64_t)P_MOD[11] + 1;  // p >> 352, plus one
+  constexpr uint64_t C = (1ull << 50) / PT;
+  const uint64_t t = (uint64_t)v.l[11] | ((uint64_t)v.l[12] << 32);
+  const uint32_t q = (uint32_t)((t * C) >> 50);
+  fp r;
+  uint64_t c = 0;
+  uint32_t br = 0;
+  TB_UNROLL for (int i = 0; i < 12; i++) {
+    c += (uint64_t)q * P_MOD[i];
+    r.l[i] = subc32(v.l[i], (uint32_t)c, br, &br);
+    c >>= 32;
+  }
+  fp d;
+  uint32_t b2 = 0;
+  TB_UNROLL for (int i = 0; i < 12; i++) d.l[i] = subc32(r.l[i], P_MOD[i], b2, &b2);
+  return fp_sel(b2 != 0, r, d);
 }
 
 // generic bilinear op: dst = POST(prod(A x, B y)) + LIN x, tables at offsets
@@ -52,14 +120,17 @@ __device__ TB_INLINE fp w_sparse_sum(const fp* src, const uint16_t* ent, int b, 
 template <int NPROD, int AOFF, int AENT, int AMAX, int BOFF, int BENT, int BMAX, int POFF, int PENT, int PMAX, int LOFF,
           int LENT, int LMAX>
 __device__ TB_INLINE void w_bilinear(fp* dst, const fp* x, const fp* y, wave12_scratch& s) {
+  static_assert(AMAX <= 8 && BMAX <= 8 && (PMAX + W12_QP - 1) / W12_QP <= 8 && LMAX <= 8, "lazy-sum bound (< 2^386)");
   const int l = threadIdx.x;
   const uint16_t* T = s.tab;
   if (l < NPROD) {
-    const fp a = w_sparse_sum<AMAX>(x, T + AENT, T[AOFF + l], T[AOFF + l + 1]);
-    const fp b = w_sparse_sum<BMAX>(y, T + BENT, T[BOFF + l], T[BOFF + l + 1]);
-    s.prod[l] = fp_mul(a, b);
+    u13 a = u13_kp2<AMAX>(), b = u13_kp2<BMAX>();
+    w_lazy_sum<AMAX>(a, x, T + AENT, T[AOFF + l], T[AOFF + l + 1]);
+    w_lazy_sum<BMAX>(b, y, T + BENT, T[BOFF + l], T[BOFF + l + 1]);
+    s.prod[l] = fp_mul13(a, b);
   }
   __syncthreads();
+  constexpr int QMAX = (PMAX + W12_QP - 1) / W12_QP;
   if (l < 12 * W12_QP) {
     const int i = l / W12_QP, q = l - i * W12_QP;
     const int b0 = T[POFF + i], e0 = T[POFF + i + 1];
@@ -67,14 +138,22 @@ __device__ TB_INLINE void w_bilinear(fp* dst, const fp* x, const fp* y, wave12_s
     int lo = b0 + q * chunk, hi = lo + chunk;
     if (hi > e0) hi = e0;
     if (lo > e0) lo = e0;
-    s.part[l] = w_sparse_sum<(PMAX + W12_QP - 1) / W12_QP>(s.prod, T + PENT, lo, hi);
+    u13 acc = u13_kp2<QMAX>();
+    w_lazy_sum<QMAX>(acc, s.prod, T + PENT, lo, hi);
+    s.part[l] = acc;
   }
   __syncthreads();
   fp r;
   if (l < 12) {
-    r = s.part[W12_QP * l];
-    TB_UNROLL for (int q = 1; q < W12_QP; q++) r = fp_add(r, s.part[W12_QP * l + q]);
-    if (LMAX > 0) r = fp_add(r, w_sparse_sum<LMAX>(x, T + LENT, T[LOFF + l], T[LOFF + l + 1]));
+    // 5 partials < 4 QMAX p each, plus the linear terms: < 170p < 2^389
+    // (reduce13 holds for any v < 2^390)
+    u13 acc = s.part[W12_QP * l];
+    TB_UNROLL for (int q = 1; q < W12_QP; q++) u13_add(acc, s.part[W12_QP * l + q]);
+    if (LMAX > 0) {
+      u13_add(acc, u13_kp2<LMAX>());
+      w_lazy_sum<LMAX>(acc, x, T + LENT, T[LOFF + l], T[LOFF + l + 1]);
+    }
+    r = reduce13(acc);
   }
   __syncthreads();
   if (l < 12) dst[l] = r;

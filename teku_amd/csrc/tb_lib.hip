@@ -280,6 +280,12 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
       hipLaunchKernelGGL(k_sig_check, g, blk, 0, sb, b.sigs, n, Q + n, skip + n, w + L.sig_code, (uint32_t*)(w + L.n_bad), 1u);
   }
   TB_EV(5, sb);
+  // Large split batches: the main pairs' line kernel needs only the signature
+  // codes from this stream, not the bucket sums and the extra pairs' lines
+  // (one 64-lane launch of ~2.5 ms): it waits on e_sig, and only the
+  // accumulator launch that absorbs the extra lines waits on e_join[1].
+  const bool late_join = !serial && pp.msm && pp.split && pp.n_spread;
+  if (late_join) HIPCHK(hipEventRecord(c.e_sig, sb));
   TB_EV(8, sb);
   if (pp.msm) {
     hipLaunchKernelGGL(k_msm_bucket, dim3(TB_MSM_PARTS / TB_BLOCK), blk, 0, sb, (const g2a*)(w + L.sig_aff), (const uint8_t*)(w + L.sig_use),
@@ -309,7 +315,8 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
   if (n) hipLaunchKernelGGL(k_set_hash, g, blk, 0, s, b.msgs, b.msg_off, dst, dlen, n, Q, skip);
   TB_EV(7, s);
   HIPCHK(hipStreamWaitEvent(s, c.e_join[0], 0));
-  HIPCHK(hipStreamWaitEvent(s, c.e_join[1], 0));
+  HIPCHK(hipStreamWaitEvent(s, late_join ? c.e_sig : c.e_join[1], 0));
+  bool joined = !late_join;
   // --- Miller loops of all pairs (pairs of invalid sets contribute 1) ---------
   const uint32_t np = pp.n_pairs, nf = pp.n_f();
   TB_EV(10, s);
@@ -327,6 +334,10 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
         const uint32_t ex = lo + m == pp.n_main ? pp.n_spread : 0u;
         hipLaunchKernelGGL(k_miller_lines, dim3((m + TB_BLOCK - 1) / TB_BLOCK), blk, 0, s, (const g1a*)P + lo, (const g2a*)Q + lo,
                            (const uint8_t*)skip + lo, ca + lo, cb + lo, m, lines);
+        if (ex && !joined) {  // this accumulator launch reads the extra pairs' lines and skip flags
+          HIPCHK(hipStreamWaitEvent(s, c.e_join[1], 0));
+          joined = true;
+        }
         hipLaunchKernelGGL(pp.per == 2 ? k_miller_acc2 : k_miller_acc1, dim3((mt + TB_BLOCK - 1) / TB_BLOCK), blk, 0, s,
                            (const uint4*)lines, (const uint8_t*)skip + lo, ca + lo, cb + lo, m, (const uint4*)(w + L.xlines),
                            (const uint8_t*)skip + pp.n_main, ex, f + lo / pp.per);
@@ -335,6 +346,7 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
       hipLaunchKernelGGL(pp.per == 1 ? k_miller1 : k_miller2, dim3((nf + TB_BLOCK - 1) / TB_BLOCK), blk, 0, s, (const g1a*)P,
                          (const g2a*)Q, (const uint8_t*)skip, ca, cb, np, f);
   }
+  if (!joined) HIPCHK(hipStreamWaitEvent(s, c.e_join[1], 0));  // every stream joins before ws_release
   TB_EV(11, s);
   TB_EV(12, s);
   if (nf == 0) {  // no pairs at all: the partial product is 1

@@ -147,6 +147,24 @@ def test_miller_wave_matches_single_lane(run):
     assert O.final_exponentiation(wave[1]) == O.pairing(*pairs[1])
 
 
+def test_miller_prog_matches_single_lane(run):
+    """k_miller_wave's pipelined level program (tb_mprog.h, tables from
+    tools/gen_miller_prog.py) == the one-thread miller_loop up to a factor in
+    Fp (its doubling step works on 4T), and pairs to e(P, Q) after the final
+    exponentiation; the batch paths only ever use the final exponentiation."""
+    P1 = O.jac_to_affine(O.FP, O.jac_mul(O.FP, O.jac_from_affine(O.FP, O.G1_GEN), 12345))
+    pairs = [(O.G1_GEN, O.G2_GEN), (P1, O.hash_to_g2(b"wave miller")), (O.G1_GEN, O.hash_to_g2(b"x" * 32))]
+    recs = [enc_fp(P[0]) + enc_fp(P[1]) + enc_fp2(Q[0]) + enc_fp2(Q[1]) for P, Q in pairs]
+    single = [dec_fp12(x) for x in run("MILLER", recs)]
+    prog = [dec_fp12(x) for x in run("MILLER_PROG", recs)]
+    for s, w in zip(single, prog):
+        ratio = O.f12_mul(w, O.f12_inv(s))
+        flat = [c for f6 in ratio for f2_ in f6 for c in f2_]
+        assert flat[0] != 0 and all(c == 0 for c in flat[1:]), "ratio not in Fp"
+    for (P, Q), w in zip(pairs, prog):
+        assert O.final_exponentiation(w) == O.pairing(P, Q)
+
+
 def test_fp_bounds_of_weak_reduction(run):
     """The same bound checks on the GPU build (tests/opcodec.check_raw_ops)."""
     check_raw_ops(run, random.Random(12))
