@@ -182,7 +182,10 @@ __device__ TB_INLINE line3 dbl_step_f(g2p& T, const g1a& P) {
 }
 }  // namespace
 
-extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_MIN_WAVES)
+#ifndef TB_LINES_WAVES
+#define TB_LINES_WAVES TB_MIN_WAVES  // A/B: 2 caps the line kernel at 256 registers
+#endif
+extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_LINES_WAVES)
     k_miller_lines(const g1a* __restrict__ P, const g2a* __restrict__ Q, const uint8_t* __restrict__ skip,
                    const uint8_t* __restrict__ code_a, const uint8_t* __restrict__ code_b, uint32_t n, uint4* __restrict__ lines) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;

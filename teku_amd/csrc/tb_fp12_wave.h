@@ -58,18 +58,57 @@ __device__ TB_INLINE void u13_add(u13& acc, const u13& v) {
   TB_UNROLL for (int i = 0; i < 13; i++) acc.l[i] = addc32(acc.l[i], v.l[i], c, &c);
 }
 
+// Carry-save lazy sums.  A signed integer combination sum c_t v_t of
+// weakly reduced values (v_t < 2^384 as 12 limbs) accumulates on 13 64-bit
+// columns: a term with c >= 0 adds c * v_i to column i (one v_mad_u64_u32 per
+// limb, independent across limbs -- no carry chain per term); a term with
+// c = -m adds m * ~v_i, i.e. m (2^384 - 1 - v), and the sum of those m is
+// corrected once by adding M_neg * G with G = -(2^384 - 1) mod p.  The
+// columns are normalized once at the end (one 13-step carry chain).  The
+// result is congruent to sum c_t v_t mod p and below (sum |c_t| + M_neg) 2^384.
+TB_CONST uint32_t CS_G[12] = {0xfffcaaafu, 0x43f5ffffu, 0xed47fffdu, 0x32b7fff2u, 0xa2e99d69u, 0x07e83a49u,
+                              0x8332bb7au, 0xeca8f331u, 0xa0f4c069u, 0xef148d1eu, 0x3eff0206u, 0x040ab326u};
+
+struct c13 {
+  uint64_t c[12];
+  uint32_t mneg;
+};
+
+__device__ TB_INLINE void cs_zero(c13& a) {
+  TB_UNROLL for (int i = 0; i < 12; i++) a.c[i] = 0;
+  a.mneg = 0;
+}
+
+// a += c * v, c = neg ? -m : m
+__device__ TB_INLINE void cs_term(c13& a, const fp& v, uint32_t m, bool neg) {
+  const uint32_t sm = neg ? 0xffffffffu : 0u;
+  TB_UNROLL for (int i = 0; i < 12; i++) a.c[i] = (uint64_t)(v.l[i] ^ sm) * m + a.c[i];
+  a.mneg += neg ? m : 0u;
+}
+
+// normalized 13-limb value (the correction M_neg * G folded in)
+__device__ TB_INLINE u13 cs_norm(const c13& a) {
+  u13 r;
+  uint64_t carry = 0;
+  // columns < 2^32 (sum |c| + M_neg) < 2^42 for the bounded term counts of the
+  // callers (sum |c| <= 300): no 64-bit overflow anywhere in the chain
+  TB_UNROLL for (int i = 0; i < 12; i++) {
+    const uint64_t s = (uint64_t)CS_G[i] * a.mneg + a.c[i] + carry;
+    r.l[i] = (uint32_t)s;
+    carry = s >> 32;
+  }
+  r.l[12] = (uint32_t)carry;
+  return r;
+}
+
 // acc += (x & 1 ? -src[x >> 1] : src[x >> 1]) over the entries [b, e) (at most
 // MAXLEN; unrolled and predicated so the LDS reads issue early)
 template <int MAXLEN>
-__device__ TB_INLINE void w_lazy_sum(u13& acc, const fp* src, const uint16_t* ent, int b, int e) {
+__device__ TB_INLINE void w_cs_sum(c13& acc, const fp* src, const uint16_t* ent, int b, int e) {
   TB_UNROLL for (int t = 0; t < MAXLEN; t++) {
     if (b + t < e) {
       const uint32_t x = ent[b + t];
-      const fp v = src[x >> 1];
-      const uint32_t neg = x & 1u, m = 0u - neg;
-      uint32_t c = neg;
-      TB_UNROLL for (int i = 0; i < 12; i++) acc.l[i] = addc32(acc.l[i], v.l[i] ^ m, c, &c);
-      acc.l[12] = acc.l[12] + m + c;
+      cs_term(acc, src[x >> 1], 1u, (x & 1u) != 0);
     }
   }
 }
@@ -93,7 +132,7 @@ __device__ TB_INLINE fp fp_mul13(const u13& a, const u13& b) {
   return r;
 }
 
-// v in [0, 2^390) -> v mod p in [0, 2p): q = floor(t C / 2^50) with t = v >> 352
+// v in [0, 2^392) -> v mod p in [0, 2p): q = floor(t C / 2^50) with t = v >> 352
 // and C = floor(2^50 / (p_352 + 1)) underestimates v / p by at most 2, so
 // v - q p is in [0, 3p); one conditional subtraction of p lands in [0, 2p).
 __device__ TB_INLINE fp reduce13(const u13& v) {
@@ -120,14 +159,16 @@ __device__ TB_INLINE fp reduce13(const u13& v) {
 template <int NPROD, int AOFF, int AENT, int AMAX, int BOFF, int BENT, int BMAX, int POFF, int PENT, int PMAX, int LOFF,
           int LENT, int LMAX>
 __device__ TB_INLINE void w_bilinear(fp* dst, const fp* x, const fp* y, wave12_scratch& s) {
-  static_assert(AMAX <= 8 && BMAX <= 8 && (PMAX + W12_QP - 1) / W12_QP <= 8 && LMAX <= 8, "lazy-sum bound (< 2^386)");
+  static_assert(AMAX <= 8 && BMAX <= 8 && (PMAX + W12_QP - 1) / W12_QP <= 8 && LMAX <= 8, "lazy-sum bound (< 2^392)");
   const int l = threadIdx.x;
   const uint16_t* T = s.tab;
   if (l < NPROD) {
-    u13 a = u13_kp2<AMAX>(), b = u13_kp2<BMAX>();
-    w_lazy_sum<AMAX>(a, x, T + AENT, T[AOFF + l], T[AOFF + l + 1]);
-    w_lazy_sum<BMAX>(b, y, T + BENT, T[BOFF + l], T[BOFF + l + 1]);
-    s.prod[l] = fp_mul13(a, b);
+    c13 a, b;
+    cs_zero(a);
+    cs_zero(b);
+    w_cs_sum<AMAX>(a, x, T + AENT, T[AOFF + l], T[AOFF + l + 1]);
+    w_cs_sum<BMAX>(b, y, T + BENT, T[BOFF + l], T[BOFF + l + 1]);
+    s.prod[l] = fp_mul13(cs_norm(a), cs_norm(b));
   }
   __syncthreads();
   constexpr int QMAX = (PMAX + W12_QP - 1) / W12_QP;
@@ -138,20 +179,23 @@ __device__ TB_INLINE void w_bilinear(fp* dst, const fp* x, const fp* y, wave12_s
     int lo = b0 + q * chunk, hi = lo + chunk;
     if (hi > e0) hi = e0;
     if (lo > e0) lo = e0;
-    u13 acc = u13_kp2<QMAX>();
-    w_lazy_sum<QMAX>(acc, s.prod, T + PENT, lo, hi);
-    s.part[l] = acc;
+    c13 acc;
+    cs_zero(acc);
+    w_cs_sum<QMAX>(acc, s.prod, T + PENT, lo, hi);
+    s.part[l] = cs_norm(acc);
   }
   __syncthreads();
   fp r;
   if (l < 12) {
-    // 5 partials < 4 QMAX p each, plus the linear terms: < 170p < 2^389
-    // (reduce13 holds for any v < 2^390)
+    // 5 partials < 2 QMAX 2^384 each, plus the linear terms: < 2^391
+    // (reduce13 holds for any v < 2^392)
     u13 acc = s.part[W12_QP * l];
     TB_UNROLL for (int q = 1; q < W12_QP; q++) u13_add(acc, s.part[W12_QP * l + q]);
     if (LMAX > 0) {
-      u13_add(acc, u13_kp2<LMAX>());
-      w_lazy_sum<LMAX>(acc, x, T + LENT, T[LOFF + l], T[LOFF + l + 1]);
+      c13 lin;
+      cs_zero(lin);
+      w_cs_sum<LMAX>(lin, x, T + LENT, T[LOFF + l], T[LOFF + l + 1]);
+      u13_add(acc, cs_norm(lin));
     }
     r = reduce13(acc);
   }

@@ -79,10 +79,10 @@ struct dev_ctx {
   dbuf in, ws;  // device input staging, pipeline workspace
   dbuf fin;     // final-exponentiation scratch
   dbuf dstb;    // default DST for the device-resident API
-  hipStream_t aux[2] = {nullptr, nullptr};  // concurrent per-set stages
+  hipStream_t aux[3] = {nullptr, nullptr, nullptr};  // concurrent per-set stages (aux[2]: high priority, hash_to_G2)
   dbuf tab_aff, tab_code;                    // device-resident public-key table (tbls_pk_table_load)
   uint32_t tab_n = 0;
-  hipEvent_t e_fork = nullptr, e_join[2] = {nullptr, nullptr}, e_sig = nullptr;
+  hipEvent_t e_fork = nullptr, e_join[3] = {nullptr, nullptr, nullptr}, e_sig = nullptr;
   hipEvent_t e_t0 = nullptr, e_t1 = nullptr;  // per-call device timing (shard_launch), created once
   // Last use of `ws` on any stream.  The device-resident API queues work on the
   // caller's stream and returns; every later user of `ws` (on whatever stream)
@@ -113,6 +113,7 @@ size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
 // bucket sum by randomizer byte with 2040 bucket pairs (k_msm_*, k_sigs.hip);
 // below it, one signature pair (-[r_i] g1, sig_i) per set.
 #define TB_MSM_MIN 32768u
+#define TB_HASH_WAVE_MAX 512u  // k_set_hash_wave (one workgroup per set) up to this many sets: at 1024 its waves fill every SIMD and the key / signature stages can no longer run beside it (measured 9.8 vs 8.8 ms partial)
 #define TB_MSM_BUCKETS 2048u  // 8 windows x 256 digits (digit 0 unused)
 #define TB_MSM_NSUM 2040u     // 8 x 255 bucket sums (k_msm_bucket_sum)
 #define TB_MSM_XPAIRS 64u     // 8 windows x 8 digit bits: the signature side's pairs
@@ -205,7 +206,8 @@ struct ws_layout {
 #define TB_NSTAGE 7
 #define TB_NSTAGE_EV (2 * TB_NSTAGE)
 // Streams: keys on aux[0], signatures (+ bucket sums) on aux[1], hash_to_G2
-// on the caller's stream; all three join before the Miller loops.  At large n
+// on aux[2] (high priority); all three join the caller's stream before the
+// Miller loops.  At large n
 // every stage fills the GPU; at small n (config 1) the three per-set chains
 // run side by side.  TBLS_SERIAL=1 (or `serial`) runs everything on the
 // caller's stream, for exclusive per-stage timings.
@@ -229,6 +231,10 @@ void launch_set_pk(hipStream_t s, uint32_t n, uint32_t n_entries, const uint32_t
                      (const uint32_t*)mlist, (const uint32_t*)mcnt, P, set_code, n_bad, key_idx, tab_n);
 }
 
+extern "C" __global__ void k_set_hash_wave(const uint8_t* __restrict__ msgs, const uint32_t* __restrict__ msg_off,
+                                           const uint8_t* __restrict__ dst, uint32_t dlen, uint32_t n, g2a* __restrict__ Q,
+                                           uint8_t* __restrict__ skip);  // k_hwave.hip
+
 int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* partial_out, ws_layout& L,
                    const uint8_t* dst, uint32_t dlen, hipEvent_t* ev = nullptr, bool serial_req = false,
                    const uint32_t* key_idx = nullptr) {
@@ -245,7 +251,7 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
   uint8_t* w = c.ws.as<uint8_t>();
   static const bool serial_env = getenv("TBLS_SERIAL") && getenv("TBLS_SERIAL")[0] == '1';
   const bool serial = serial_env || serial_req;
-  hipStream_t sa = serial ? s : c.aux[0], sb = serial ? s : c.aux[1];
+  hipStream_t sa = serial ? s : c.aux[0], sb = serial ? s : c.aux[1], sh = serial ? s : c.aux[2];
 #define TB_EV(i, st) \
   if (ev) HIPCHK(hipEventRecord(ev[i], st))
   const dim3 blk(TB_BLOCK);
@@ -259,6 +265,7 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
     HIPCHK(hipEventRecord(c.e_fork, s));
     HIPCHK(hipStreamWaitEvent(sa, c.e_fork, 0));
     HIPCHK(hipStreamWaitEvent(sb, c.e_fork, 0));
+    HIPCHK(hipStreamWaitEvent(sh, c.e_fork, 0));
   }
   // --- stream b: signatures, then (large batches) the bucket sums -----------
   uint32_t* msm_cnt = (uint32_t*)(w + L.msm_cnt);
@@ -310,10 +317,21 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
                 pp.msm ? nullptr : P + n, c.comb.as<const g1a>());
   TB_EV(3, sa);
   HIPCHK(hipEventRecord(c.e_join[0], sa));
-  // --- caller's stream: hash_to_G2 per set ------------------------------------
-  TB_EV(6, s);
-  if (n) hipLaunchKernelGGL(k_set_hash, g, blk, 0, s, b.msgs, b.msg_off, dst, dlen, n, Q, skip);
-  TB_EV(7, s);
+  // --- high-priority stream: hash_to_G2 per set -------------------------------
+  // The longest per-set stage (2 wave rounds at 131k sets): with queue
+  // priority its waves are dispatched first and the shorter key / signature
+  // stages fill the SIMDs around them, instead of its last waves running
+  // alone after the others finish.
+  TB_EV(6, sh);
+  if (n && n <= TB_HASH_WAVE_MAX)  // one workgroup per set: the cofactor clearing lane-parallel
+    hipLaunchKernelGGL(k_set_hash_wave, dim3(n), dim3(64), 0, sh, b.msgs, b.msg_off, dst, dlen, n, Q, skip);
+  else if (n)
+    hipLaunchKernelGGL(k_set_hash, g, blk, 0, sh, b.msgs, b.msg_off, dst, dlen, n, Q, skip);
+  TB_EV(7, sh);
+  if (!serial) {
+    HIPCHK(hipEventRecord(c.e_join[2], sh));
+    HIPCHK(hipStreamWaitEvent(s, c.e_join[2], 0));
+  }
   HIPCHK(hipStreamWaitEvent(s, c.e_join[0], 0));
   HIPCHK(hipStreamWaitEvent(s, late_join ? c.e_sig : c.e_join[1], 0));
   bool joined = !late_join;
@@ -762,9 +780,13 @@ extern "C" int tbls_init(int n_devices, uint32_t flags) {
   for (int d = 0; d < count; d++) {
     dev_ctx* c = new dev_ctx();
     c->dev = d;
+    int prio_lo = 0, prio_hi = 0;
     if (hipSetDevice(d) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->aux[0], hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->aux[1], hipStreamNonBlocking) != hipSuccess ||
+        hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess ||
+        hipStreamCreateWithPriority(&c->aux[2], hipStreamNonBlocking, prio_hi) != hipSuccess ||
+        hipEventCreateWithFlags(&c->e_join[2], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->e_fork, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->e_join[0], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->e_join[1], hipEventDisableTiming) != hipSuccess ||
@@ -804,13 +826,13 @@ extern "C" void tbls_shutdown(void) {
     if (c->hin.p) (void)hipHostFree(c->hin.p);
     if (c->hout.p) (void)hipHostFree(c->hout.p);
     if (c->stream) (void)hipStreamDestroy(c->stream);
-    for (int i = 0; i < 2; i++)
+    for (int i = 0; i < 3; i++)
       if (c->aux[i]) (void)hipStreamDestroy(c->aux[i]);
     if (c->e_fork) (void)hipEventDestroy(c->e_fork);
     if (c->e_sig) (void)hipEventDestroy(c->e_sig);
     for (hipEvent_t e : {c->e_ws, c->e_t0, c->e_t1})
       if (e) (void)hipEventDestroy(e);
-    for (int i = 0; i < 2; i++)
+    for (int i = 0; i < 3; i++)
       if (c->e_join[i]) (void)hipEventDestroy(c->e_join[i]);
     delete c;
   }

@@ -2,7 +2,7 @@
 // tb_miller_prog.h (tools/gen_miller_prog.py) run by one 64-lane workgroup.
 //
 // Every level: lane l < np forms two operands as integer combinations of Fp
-// slots (lazy 13-limb sums, tb_fp12_wave.h), multiplies them (one Fp product
+// slots (carry-save sums, tb_fp12_wave.h), multiplies them (one Fp product
 // per lane) into a product slot; then lanes l < nq form signed partial sums of
 // the outputs' terms, and lanes l < no add their output's partials, reduce to
 // [0, 2p) and write the output slot.  The f chain (f^2, f * line) and the
@@ -22,30 +22,26 @@ struct mprog_lds {
   uint16_t tab[MP_TAB_N];
 };
 
-// acc += sum over entries [b, e) of coef * S[slot] (two's complement, 13 limbs)
+// acc += sum over entries [b, e) of coef * S[slot] (carry-save columns,
+// tb_fp12_wave.h cs_term)
 template <int MAXLEN>
-__device__ TB_INLINE void mp_csum(u13& acc, const fp* S, const uint16_t* ent, int b, int e) {
+__device__ TB_INLINE void mp_csum(c13& acc, const fp* S, const uint16_t* ent, int b, int e) {
   TB_UNROLL for (int t = 0; t < MAXLEN; t++) {
     if (b + t < e) {
       const uint32_t slot = ent[2 * (b + t)];
       const int c = (int16_t)ent[2 * (b + t) + 1];
-      const fp v = S[slot];
-      const uint32_t m = (uint32_t)(c < 0 ? -c : c);
-      const uint32_t mask = c < 0 ? 0xffffffffu : 0u;
-      uint64_t w = 0;
-      uint32_t cy = mask & 1u;
-      TB_UNROLL for (int i = 0; i < 12; i++) {
-        w = (uint64_t)v.l[i] * m + (w >> 32);
-        acc.l[i] = addc32(acc.l[i], (uint32_t)w ^ mask, cy, &cy);
-      }
-      acc.l[12] = acc.l[12] + ((uint32_t)(w >> 32) ^ mask) + cy;
+      cs_term(acc, S[slot], (uint32_t)(c < 0 ? -c : c), c < 0);
     }
   }
 }
 
-__device__ TB_INLINE void mp_level(mprog_lds& L, int type) {
+// One level of a generated program (tables staged in LDS at `tab`, this
+// level type's block at tab + off): products, partial sums, outputs.  The
+// term-count bounds are the program's (MP_AMAX ..., CF_AMAX ...).
+template <int AMAX, int BMAX, int QMAX, int OMAX>
+__device__ TB_INLINE void wprog_level(fp* S, u13* part, const uint16_t* tab, int off) {
   const int l = threadIdx.x;
-  const uint16_t* H = L.tab + MP_TYPE_OFF[type];
+  const uint16_t* H = tab + off;
   const int np = H[0], nq = H[1], no = H[2];
   const uint16_t* abeg = H + 3;
   const uint16_t* bbeg = abeg + np + 1;
@@ -55,32 +51,39 @@ __device__ TB_INLINE void mp_level(mprog_lds& L, int type) {
   const uint16_t* odst = obeg + no + 1;
   const uint16_t* ent = odst + no;
   if (l < np) {
-    u13 a = u13_kp2<MP_OPND_K>(), b = u13_kp2<MP_OPND_K>();
-    mp_csum<MP_AMAX>(a, L.S, ent, abeg[l], abeg[l + 1]);
-    mp_csum<MP_BMAX>(b, L.S, ent, bbeg[l], bbeg[l + 1]);
-    L.S[pout[l]] = fp_mul13(a, b);
+    c13 a, b;
+    cs_zero(a);
+    cs_zero(b);
+    mp_csum<AMAX>(a, S, ent, abeg[l], abeg[l + 1]);
+    mp_csum<BMAX>(b, S, ent, bbeg[l], bbeg[l + 1]);
+    S[pout[l]] = fp_mul13(cs_norm(a), cs_norm(b));
   }
   __syncthreads();
   if (l < nq) {
-    u13 acc;
-    TB_UNROLL for (int i = 0; i < 13; i++) acc.l[i] = 0;
-    mp_csum<MP_QMAX>(acc, L.S, ent, qbeg[l], qbeg[l + 1]);
-    L.part[l] = acc;
+    c13 acc;
+    cs_zero(acc);
+    mp_csum<QMAX>(acc, S, ent, qbeg[l], qbeg[l + 1]);
+    part[l] = cs_norm(acc);
   }
   __syncthreads();
   fp r;
   int dst = 0;
   if (l < no) {
-    u13 acc = u13_kp2<MP_OUT_K>();
+    u13 acc;
+    TB_UNROLL for (int i = 0; i < 13; i++) acc.l[i] = 0;
     const int j0 = obeg[l], j1 = obeg[l + 1];
-    TB_UNROLL for (int j = 0; j < MP_OMAX; j++)
-      if (j0 + j < j1) u13_add(acc, L.part[j0 + j]);
+    TB_UNROLL for (int j = 0; j < OMAX; j++)
+      if (j0 + j < j1) u13_add(acc, part[j0 + j]);
     r = reduce13(acc);
     dst = odst[l];
   }
   __syncthreads();
-  if (l < no) L.S[dst] = r;
+  if (l < no) S[dst] = r;
   __syncthreads();
+}
+
+__device__ TB_INLINE void mp_level(mprog_lds& L, int type) {
+  wprog_level<MP_AMAX, MP_BMAX, MP_QMAX, MP_OMAX>(L.S, L.part, L.tab, MP_TYPE_OFF[type]);
 }
 
 // f_{|x|,Q}(P) (up to a factor in Fp), conjugated, into L.S[0..12) -- the

@@ -7,6 +7,7 @@
 #include "../../teku_amd/csrc/tb_kdecl.h"
 #include "tb_testops.h"
 #include "../../teku_amd/csrc/tb_mprog.h"
+#include "../../teku_amd/csrc/tb_cofprog.h"
 
 using namespace tb;
 
@@ -57,9 +58,60 @@ extern "C" __global__ void __launch_bounds__(64) k_test_miller_prog(const uint8_
   if (threadIdx.x == 0) tio_put_fp12(out + (size_t)blockIdx.x * TB_TEST_OUT, fp12_from_coords(L.S + MP_S_F0));
 }
 
+// test hook: the wave cofactor-clearing program (tb_cofprog.h), one 64-lane
+// block per record: in = Jacobian X, Y, Z (Fp2 each, the TOP_CLEAR_COF layout
+// plus Z at +192), out = affine x, y and the ok flag at +384
+extern "C" __global__ void __launch_bounds__(64) k_test_clear_cof_prog(const uint8_t* in, uint8_t* out) {
+  __shared__ cf_lds L;
+  const uint8_t* r = in + (size_t)blockIdx.x * TB_TEST_IN;
+  cf_init(L);
+  if (threadIdx.x == 0) cf_load_lane0(L, g2j{tio_fp2(r), tio_fp2(r + 96), tio_fp2(r + 192)});
+  g2a a;
+  bool ok;
+  cf_run(L, a, ok);
+  if (threadIdx.x == 0) {
+    uint8_t* o = out + (size_t)blockIdx.x * TB_TEST_OUT;
+    tio_put_fp2(o, a.x);
+    tio_put_fp2(o + 96, a.y);
+    tio_put_u32(o + 384, ok ? 1u : 0u);
+  }
+}
+
+// test hook (timing): clock64() cycles of 64 chained Fp products on lane 0,
+// of 64 chained wave cyclotomic squarings and of 64 Miller-program levels, in
+// one 64-lane block; out = 3 x u64 cycle counts (+0, +8, +16)
+extern "C" __global__ void __launch_bounds__(64) k_test_wave_timing(const uint8_t* in, uint8_t* out) {
+  __shared__ final_exp_lds F;
+  __shared__ mprog_lds M;
+  w12_tabs_load(F.s);
+  for (int j = threadIdx.x; j < MP_TAB_N; j += blockDim.x) M.tab[j] = MP_TAB[j];
+  for (int j = threadIdx.x; j < MP_NSLOT; j += blockDim.x) M.S[j] = tio_fp(in);
+  if (threadIdx.x < 12) F.F[threadIdx.x] = tio_fp(in + 48 * threadIdx.x);
+  __syncthreads();
+  fp a = tio_fp(in), b = tio_fp(in + 48);
+  const long long t0 = clock64();
+  if (threadIdx.x == 0)
+    for (int k = 0; k < 64; k++) a = fp_mul(a, b);
+  __syncthreads();
+  const long long t1 = clock64();
+  for (int k = 0; k < 64; k++) w_cyc_sqr(F.F, F.F, F.s);
+  const long long t2 = clock64();
+  for (int k = 0; k < 64; k++) mp_level(M, MP_SEQ[8 + (k & 1)]);
+  const long long t3 = clock64();
+  if (threadIdx.x == 0) {
+    uint64_t* o = reinterpret_cast<uint64_t*>(out + (size_t)blockIdx.x * TB_TEST_OUT);
+    o[0] = (uint64_t)(t1 - t0);
+    o[1] = (uint64_t)(t2 - t1);
+    o[2] = (uint64_t)(t3 - t2);
+    tio_put_fp(out + (size_t)blockIdx.x * TB_TEST_OUT + 64, fp_add(a, F.F[0]));
+  }
+}
+
 #define TOP_FINAL_EXP_WAVE 29
 #define TOP_MILLER_WAVE 31
 #define TOP_MILLER_PROG 40  // tb_testops.h uses 1..35
+#define TOP_CLEAR_COF_PROG 41
+#define TOP_WAVE_TIMING 42
 
 // n records of TB_TEST_IN bytes -> n records of TB_TEST_OUT bytes on device 0.
 // Returns 0 on success, 8 (TBLS_DEVICE_ERROR) on any HIP failure.
@@ -75,6 +127,10 @@ extern "C" int tbls_test_ops(int op, const uint8_t* in, uint8_t* out, size_t n) 
       hipLaunchKernelGGL(k_test_miller_wave, dim3((uint32_t)n), dim3(64), 0, 0, din, dout);
     else if (op == TOP_MILLER_PROG)
       hipLaunchKernelGGL(k_test_miller_prog, dim3((uint32_t)n), dim3(64), 0, 0, din, dout);
+    else if (op == TOP_WAVE_TIMING)
+      hipLaunchKernelGGL(k_test_wave_timing, dim3((uint32_t)n), dim3(64), 0, 0, din, dout);
+    else if (op == TOP_CLEAR_COF_PROG)
+      hipLaunchKernelGGL(k_test_clear_cof_prog, dim3((uint32_t)n), dim3(64), 0, 0, din, dout);
     else
       hipLaunchKernelGGL(k_test_ops, dim3((uint32_t)((n + TB_BLOCK - 1) / TB_BLOCK)), dim3(TB_BLOCK), 0, 0, op, din, dout, (uint32_t)n);
     if (hipGetLastError() == hipSuccess && hipDeviceSynchronize() == hipSuccess &&

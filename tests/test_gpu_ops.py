@@ -165,6 +165,28 @@ def test_miller_prog_matches_single_lane(run):
         assert O.final_exponentiation(w) == O.pairing(P, Q)
 
 
+def test_clear_cofactor_prog(run):
+    """The wave cofactor-clearing program (tb_cofprog.h, tables from
+    tools/gen_cofactor_prog.py, used by k_set_hash_wave) == the oracle's
+    clear_cofactor_g2 on SSWU/isogeny points given with random Jacobian Z, on
+    G2 points, and -- through the one-lane fallback the kernel takes when the
+    program ends with Z = 0 -- on the point at infinity."""
+    rng = _rng()
+    pts = [O.iso_map_g2(O.map_to_curve_sswu_g2((rng.randrange(O.P), rng.randrange(O.P)))) for _ in range(3)] + [O.G2_GEN]
+    recs, exps = [], []
+    for q in pts:
+        z = (rng.randrange(1, O.P), rng.randrange(O.P))
+        zz = O.f2_sqr(z)
+        recs.append(enc_fp2(O.f2_mul(q[0], zz)) + enc_fp2(O.f2_mul(q[1], O.f2_mul(zz, z))) + enc_fp2(z))
+        exps.append(O.jac_to_affine(O.FP2, O.clear_cofactor_g2(O.jac_from_affine(O.FP2, q))))
+    recs.append(enc_fp2((1, 0)) + enc_fp2((1, 0)) + enc_fp2((0, 0)))  # infinity
+    out = run("CLEAR_COF_PROG", recs)
+    for o, e in zip(out, exps):
+        assert u32(o, 384) == 1
+        assert (dec_fp2(o[:96]), dec_fp2(o[96:192])) == e
+    assert u32(out[-1], 384) == 0
+
+
 def test_fp_bounds_of_weak_reduction(run):
     """The same bound checks on the GPU build (tests/opcodec.check_raw_ops)."""
     check_raw_ops(run, random.Random(12))

@@ -339,6 +339,16 @@ def run_tables(blocks, seq, slot, Pa, Qa):
 
 
 def main():
+    text = generate()
+    path = os.path.join(ROOT, "teku_amd", "csrc", "tb_miller_prog.h")
+    open(path, "w").write(text)
+    print("wrote", path)
+
+
+def generate(check_pairs=2, verbose=True):
+    """Header text of tb_miller_prog.h; the emitted tables are executed on
+    field values for check_pairs random (P, Q) and compared with the oracle
+    pairing first."""
     levels = build_levels()
     slot = slot_table(levels)
     assert len(slot) < 256
@@ -351,23 +361,24 @@ def main():
         seq.append(keys.index(k))
     # numeric check against the oracle pairing
     rng = random.Random(5)
-    for trial in range(2):
+    for trial in range(check_pairs):
         a, b = rng.randrange(1, O.R), rng.randrange(1, O.R)
-        Pa = O.g1_mul(O.G1_GEN, a) if hasattr(O, "g1_mul") else None
         Pa = O.jac_to_affine(O.FP, O.jac_mul(O.FP, O.jac_from_affine(O.FP, O.G1_GEN), a))
         Qa = O.jac_to_affine(O.FP2, O.jac_mul(O.FP2, O.jac_from_affine(O.FP2, O.G2_GEN), b))
         f = run_tables(blocks, seq, slot, Pa, Qa)
         got = O.final_exponentiation(O.f12_conj(f))
         assert got == O.pairing(Pa, Qa), "pairing mismatch"
-    print("levels", len(seq), "types", len(keys), "slots", len(slot))
-    for k, b in zip(keys, blocks):
-        print("  %-8s products %2d partials %2d outputs %2d maxlen %s" % (k, b[0][0], b[0][1], b[0][2], b[2]))
+    if verbose:
+        print("levels", len(seq), "types", len(keys), "slots", len(slot))
+        for k, b in zip(keys, blocks):
+            print("  %-8s products %2d partials %2d outputs %2d maxlen %s" % (k, b[0][0], b[0][1], b[0][2], b[2]))
     allv, offs = [], []
     for b in blocks:
         offs.append(len(allv))
         allv += b[0]
     mx = {c: max(b[2][c] for b in blocks) for c in "ABQO"}
-    print("max sum|coef|: operand %d (cap %d), output %d (cap %d)" % (STATS["op"], OPND_CAP, STATS["out"], OUT_CAP))
+    if verbose:
+        print("max sum|coef|: operand %d (cap %d), output %d (cap %d)" % (STATS["op"], OPND_CAP, STATS["out"], OUT_CAP))
     out = ["// GENERATED by tools/gen_miller_prog.py -- do not edit.", "#pragma once", "#include <stdint.h>", "namespace tb {"]
     out.append("#define MP_NSLOT %d" % len(slot))
     for nm in SLOTS_FIXED:
@@ -382,9 +393,7 @@ def main():
     out.append("TB_CONST uint8_t MP_SEQ[%d] = {%s};" % (len(seq), ", ".join(map(str, seq))))
     out.append("TB_CONST uint16_t MP_TAB[%d] = {%s};" % (len(allv), ", ".join(map(str, allv))))
     out.append("}  // namespace tb")
-    path = os.path.join(ROOT, "teku_amd", "csrc", "tb_miller_prog.h")
-    open(path, "w").write("\n".join(out) + "\n")
-    print("wrote", path, "entries", len(allv))
+    return "\n".join(out) + "\n"
 
 
 if __name__ == "__main__":
