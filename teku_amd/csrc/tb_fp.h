@@ -121,6 +121,58 @@ TB_HD TB_INLINE void mont29(uint32_t (&r)[N][14], const uint32_t (&a)[N][14], co
   TB_UNROLL for (int j = 0; j < N; j++) r[j][13] = (uint32_t)A[j];
 }
 
+// Latency form of mont29 (the same products, the same result): all 27
+// a x b columns first -- independent across columns, so a lone wave issues
+// them back to back instead of waiting on one accumulator's multiply-add
+// chain -- then the m-digit pass: m_k from column k, its 14 products with p
+// added into columns k .. k+13 at once (independent), the carry into k+1.
+// The critical path per digit is a few dependent ops instead of the column's
+// 28 chained multiply-adds.  Columns stay < 2^63 (<= 28 products < 2^58 plus
+// carries < 2^35).  Used by the wave kernels' Fp products (fp_mul13): a wave
+// cyclotomic squaring 11.8k -> 10.7k cycles, a Miller-program level 14.6k ->
+// 13.7k (tools/hash_parts.py --timing).  A lone wave's product stays issue-
+// bound (7,040 cycles for mont29<1>: ~500 instructions at the one-wave issue
+// rate), and the same form in the one-lane stage kernels measured slower
+// (hash stage 4.22 -> 4.37 ms at 128 sets), so they keep mont29.
+template <int N, bool SQR>
+TB_HD TB_INLINE void mont29_lat(uint32_t (&r)[N][14], const uint32_t (&a)[N][14], const uint32_t (&b)[N][14]) {
+  uint64_t col[N][28];
+  TB_UNROLL for (int k = 0; k < 27; k++) {
+    const int lo = k < 14 ? 0 : k - 13;
+    const int hi = k < 14 ? k : 13;
+    TB_UNROLL for (int j = 0; j < N; j++) {
+      uint64_t acc = 0;
+      if (SQR) {
+        TB_UNROLL for (int i = lo; i <= hi; i++) {
+          if (i < k - i)
+            mad29(acc, a[j][i] << 1, a[j][k - i]);
+          else if (i == k - i)
+            mad29(acc, a[j][i], a[j][i]);
+        }
+      } else {
+        TB_UNROLL for (int i = lo; i <= hi; i++) mad29(acc, a[j][i], b[j][k - i]);
+      }
+      col[j][k] = acc;
+    }
+  }
+  TB_UNROLL for (int j = 0; j < N; j++) col[j][27] = 0;
+  TB_UNROLL for (int k = 0; k < 14; k++) {
+    TB_UNROLL for (int j = 0; j < N; j++) {
+      const uint32_t m = ((uint32_t)col[j][k] * N0_29) & M29;
+      mad29(col[j][k], m, P29[0]);
+      TB_UNROLL for (int i = 1; i < 14; i++) mad29(col[j][k + i], m, P29[i]);
+      col[j][k + 1] += col[j][k] >> 29;
+    }
+  }
+  TB_UNROLL for (int j = 0; j < N; j++) {
+    TB_UNROLL for (int k = 14; k < 27; k++) {
+      r[j][k - 14] = (uint32_t)col[j][k] & M29;
+      col[j][k + 1] += col[j][k] >> 29;
+    }
+    r[j][13] = (uint32_t)col[j][27];
+  }
+}
+
 // r[j] = a[j] * b[j] (Montgomery), j < N, interleaved
 template <int N>
 TB_HD TB_INLINE void fp_mul_n(fp (&r)[N], const fp (&a)[N], const fp (&b)[N]) {

@@ -126,7 +126,7 @@ __device__ TB_INLINE fp fp_mul13(const u13& a, const u13& b) {
     x[0][i] = va & M29;
     y[0][i] = vb & M29;
   }
-  mont29<1, false>(z, x, y);
+  mont29_lat<1, false>(z, x, y);
   fp r;
   from29(r, z[0]);
   return r;

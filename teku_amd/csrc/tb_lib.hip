@@ -113,6 +113,9 @@ size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
 // bucket sum by randomizer byte with 2040 bucket pairs (k_msm_*, k_sigs.hip);
 // below it, one signature pair (-[r_i] g1, sig_i) per set.
 #define TB_MSM_MIN 32768u
+#ifndef TB_ORDER_DEFAULT
+#define TB_ORDER_DEFAULT 1  // measured 52.5 vs 53.3 ms per 131k step (2.71M vs 2.63M sigs/s with the key table)
+#endif
 #define TB_HASH_WAVE_MAX 512u  // k_set_hash_wave (one workgroup per set) up to this many sets: at 1024 its waves fill every SIMD and the key / signature stages can no longer run beside it (measured 9.8 vs 8.8 ms partial)
 #define TB_MSM_BUCKETS 2048u  // 8 windows x 256 digits (digit 0 unused)
 #define TB_MSM_NSUM 2040u     // 8 x 255 bucket sums (k_msm_bucket_sum)
@@ -251,7 +254,15 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
   uint8_t* w = c.ws.as<uint8_t>();
   static const bool serial_env = getenv("TBLS_SERIAL") && getenv("TBLS_SERIAL")[0] == '1';
   const bool serial = serial_env || serial_req;
-  hipStream_t sa = serial ? s : c.aux[0], sb = serial ? s : c.aux[1], sh = serial ? s : c.aux[2];
+  // TBLS_ORDER=1 (default; large batches): the per-set stages in sequence on
+  // the caller's stream (signatures, keys, hash -- each kernel alone fills the
+  // GPU in whole wave rounds, no tail of lone hash waves), only the
+  // bucket-sum chain on a side stream; 0: the three per-set streams run
+  // concurrently (small batches always do).
+  static const int order_env = getenv("TBLS_ORDER") ? atoi(getenv("TBLS_ORDER")) : TB_ORDER_DEFAULT;
+  const bool chain = !serial && pp.msm && order_env == 1;
+  hipStream_t sa = (serial || chain) ? s : c.aux[0], sb = serial ? s : c.aux[1], sh = (serial || chain) ? s : c.aux[2];
+  hipStream_t ssig = chain ? s : sb;
 #define TB_EV(i, st) \
   if (ev) HIPCHK(hipEventRecord(ev[i], st))
   const dim3 blk(TB_BLOCK);
@@ -278,21 +289,25 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
     hipLaunchKernelGGL(k_msm_scan, dim3(1), dim3(256), 0, sb, (const uint32_t*)msm_cnt, msm_off, cur);
     hipLaunchKernelGGL(k_msm_scatter, g, blk, 0, sb, b.rand, n, cur, msm_idx);
   }
-  TB_EV(4, sb);
+  TB_EV(4, ssig);
   if (n) {
     if (pp.msm)
-      hipLaunchKernelGGL(k_sig_check, g, blk, 0, sb, b.sigs, n, (g2a*)(w + L.sig_aff), w + L.sig_use, w + L.sig_code,
+      hipLaunchKernelGGL(k_sig_check, g, blk, 0, ssig, b.sigs, n, (g2a*)(w + L.sig_aff), w + L.sig_use, w + L.sig_code,
                          (uint32_t*)(w + L.n_bad), 0u);
     else  // the set's signature pair: Q[n + i] = sig_i, skip[n + i] = infinite / invalid
-      hipLaunchKernelGGL(k_sig_check, g, blk, 0, sb, b.sigs, n, Q + n, skip + n, w + L.sig_code, (uint32_t*)(w + L.n_bad), 1u);
+      hipLaunchKernelGGL(k_sig_check, g, blk, 0, ssig, b.sigs, n, Q + n, skip + n, w + L.sig_code, (uint32_t*)(w + L.n_bad), 1u);
   }
-  TB_EV(5, sb);
+  TB_EV(5, ssig);
+  if (chain) {  // the bucket sums need the decoded signatures
+    HIPCHK(hipEventRecord(c.e_sig, s));
+    HIPCHK(hipStreamWaitEvent(sb, c.e_sig, 0));
+  }
   // Large split batches: the main pairs' line kernel needs only the signature
   // codes from this stream, not the bucket sums and the extra pairs' lines
   // (one 64-lane launch of ~2.5 ms): it waits on e_sig, and only the
   // accumulator launch that absorbs the extra lines waits on e_join[1].
   const bool late_join = !serial && pp.msm && pp.split && pp.n_spread;
-  if (late_join) HIPCHK(hipEventRecord(c.e_sig, sb));
+  if (late_join && !chain) HIPCHK(hipEventRecord(c.e_sig, sb));
   TB_EV(8, sb);
   if (pp.msm) {
     hipLaunchKernelGGL(k_msm_bucket, dim3(TB_MSM_PARTS / TB_BLOCK), blk, 0, sb, (const g2a*)(w + L.sig_aff), (const uint8_t*)(w + L.sig_use),
@@ -333,7 +348,10 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
     HIPCHK(hipStreamWaitEvent(s, c.e_join[2], 0));
   }
   HIPCHK(hipStreamWaitEvent(s, c.e_join[0], 0));
-  HIPCHK(hipStreamWaitEvent(s, late_join ? c.e_sig : c.e_join[1], 0));
+  if (!late_join)
+    HIPCHK(hipStreamWaitEvent(s, c.e_join[1], 0));
+  else if (!chain)
+    HIPCHK(hipStreamWaitEvent(s, c.e_sig, 0));
   bool joined = !late_join;
   // --- Miller loops of all pairs (pairs of invalid sets contribute 1) ---------
   const uint32_t np = pp.n_pairs, nf = pp.n_f();
