@@ -141,10 +141,16 @@ static uint32_t miller_wave_max() {
 
 // Pairs of a batch of n sets: [0, n) the sets' (r_i apk_i, H(m_i)), then the
 // signature side -- n pairs (-[r_i] g1, sig_i) below TB_MSM_MIN sets (ordinary
-// pairs of the Miller kernels), else TB_MSM_XPAIRS bit-sum pairs whose lines
-// the split Miller loop spreads over its accumulators (k_lines.hip).
+// pairs of the Miller kernels), else TB_MSM_XPAIRS bit-sum pairs.  With the
+// split Miller loop the bit-sum pairs run one 64-lane wave each (k_miller_wave,
+// n_xwave of them) on the bucket-sum stream, into the Miller values after the
+// accumulators' (TB_SPREAD_EXTRA=1: their lines spread over the accumulators,
+// k_lines.hip, the round-1/2 form).
+#ifndef TB_SPREAD_EXTRA
+#define TB_SPREAD_EXTRA 0
+#endif
 struct pair_plan {
-  uint32_t n, n_extra, n_pairs, n_main, n_spread, per;
+  uint32_t n, n_extra, n_pairs, n_main, n_spread, n_xwave, per;
   bool msm, wave, split;
   explicit pair_plan(uint32_t n_) : n(n_) {
     msm = n >= TB_MSM_MIN;
@@ -152,11 +158,13 @@ struct pair_plan {
     n_pairs = n + n_extra;
     wave = n_pairs <= miller_wave_max();
     split = !wave && miller_split();
-    n_spread = split && msm ? n_extra : 0u;  // pairs spread line by line
-    n_main = n_pairs - n_spread;             // pairs owned by accumulator threads
+    n_spread = split && msm && TB_SPREAD_EXTRA ? n_extra : 0u;  // pairs spread line by line
+    n_xwave = split && msm && !TB_SPREAD_EXTRA ? n_extra : 0u;  // pairs on their own waves
+    n_main = n_pairs - n_spread - n_xwave;                       // pairs owned by accumulator threads
     per = wave ? 1u : split ? (n_main >= TB_MILLER_PER2_MIN ? 2u : 1u) : (n_pairs <= TB_MILLER1_MAX ? 1u : 2u);
   }
-  uint32_t n_f() const { return (n_main + per - 1) / per; }  // Miller values
+  uint32_t n_f_main() const { return (n_main + per - 1) / per; }
+  uint32_t n_f() const { return n_f_main() + n_xwave; }  // Miller values: accumulators, then the wave pairs'
   uint32_t line_pairs() const { return split ? std::min(n_main, TB_LINE_CHUNK) : 0u; }
 };
 
@@ -306,7 +314,7 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
   // codes from this stream, not the bucket sums and the extra pairs' lines
   // (one 64-lane launch of ~2.5 ms): it waits on e_sig, and only the
   // accumulator launch that absorbs the extra lines waits on e_join[1].
-  const bool late_join = !serial && pp.msm && pp.split && pp.n_spread;
+  const bool late_join = !serial && pp.msm && pp.split;
   if (late_join && !chain) HIPCHK(hipEventRecord(c.e_sig, sb));
   TB_EV(8, sb);
   if (pp.msm) {
@@ -315,6 +323,9 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
     hipLaunchKernelGGL(k_msm_bucket_sum, dim3(TB_MSM_NSUM), dim3(64), 0, sb, (const g2j*)(w + L.msm_part), (g2j*)(w + L.msm_sum));
     hipLaunchKernelGGL(k_msm_bitsum_pairs, dim3(TB_MSM_XPAIRS), dim3(64), 0, sb, (const g2j*)(w + L.msm_sum), c.comb.as<const g1a>(),
                        P + n, Q + n, skip + n);
+    if (pp.n_xwave)  // their Miller loops, one wave each, on this stream: f[n_f_main ..)
+      hipLaunchKernelGGL(k_miller_wave, dim3(pp.n_xwave), dim3(64), 0, sb, (const g1a*)P + n, (const g2a*)Q + n, (const uint8_t*)skip + n,
+                         (const uint8_t*)(w + L.set_code + n), (const uint8_t*)(w + L.sig_code + n), pp.n_xwave, (fp12*)(w + L.f) + pp.n_f_main());
     if (pp.n_spread)  // their lines now, on this stream (the main pairs' kernel would take a whole extra wave round)
       hipLaunchKernelGGL(k_miller_lines, dim3(1), dim3(TB_MSM_XPAIRS), 0, sb, (const g1a*)P + n, (const g2a*)Q + n, (const uint8_t*)skip + n,
                          w + L.set_code + n, w + L.sig_code + n, TB_MSM_XPAIRS, (uint4*)(w + L.xlines));
