@@ -95,6 +95,12 @@ TB_HD TB_INLINE fp12 fp12_mul_by_line_i(const fp12& f, const fp2& A, const fp2& 
 // step temporaries, and the Fp12 kernel holds f, one line and the product
 // temporaries.
 // ---------------------------------------------------------------------------
+#ifndef TB_SPREAD_EXTRA
+#define TB_SPREAD_EXTRA 0  // tb_lib.hip pair_plan: the bit-sum pairs run as wave Miller loops, no spread lines
+#endif
+#ifndef TB_ACC_COMPACT
+#define TB_ACC_COMPACT 1
+#endif
 #define TB_LINE_STEPS 68  // 63 doubling + 5 addition steps of |x| = 0xd201000000010000
 #define TB_LINE_G 18      // 16-byte groups per line (3 Fp2 = 72 words)
 
@@ -209,7 +215,7 @@ extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_LINES_WAVES)
 // spreading the extra pairs one line at a time keeps every thread's work
 // within one line product (+0.5 %) instead of adding whole Miller loops to a
 // few threads (a tail as long as the kernel).
-template <int PER>
+template <int PER, bool EXTRA>
 __device__ TB_INLINE void miller_acc_body(const uint4* __restrict__ lines, const uint8_t* __restrict__ skip,
                                           const uint8_t* __restrict__ code_a, const uint8_t* __restrict__ code_b, uint32_t n,
                                           const uint4* __restrict__ xlines, const uint8_t* __restrict__ xskip, uint32_t n_extra,
@@ -228,13 +234,34 @@ __device__ TB_INLINE void miller_acc_body(const uint4* __restrict__ lines, const
   // always_inline: an outlined call here (one per step) made the caller save
   // and restore its live accumulator registers through scratch every step
   auto extra = [&](int step) __attribute__((always_inline)) {
-    if (!n_extra) return;
+    if (!EXTRA || !n_extra) return;
     const uint32_t e = (t + T - (uint32_t)(step * n_extra) % T) % T;
     if (e < n_extra && xskip[e] == 0) {
       const line3 l = line_load(xlines, n_extra, e, step);
       f = fp12_mul_by_line_i(f, l.a, l.b, l.c);
     }
   };
+#if TB_ACC_COMPACT
+  // one squaring site and one line-product site (the PER pairs and the
+  // addition steps loop over them): a quarter of the unrolled code, which
+  // fits the instruction cache better and keeps fewer values live
+  uint32_t usem = 0;
+  TB_UNROLL for (int j = 0; j < PER; j++) usem |= use[j] ? (1u << j) : 0u;
+  TB_NOUNROLL for (int b = 62; b >= 0; --b) {
+    const int reps = ((X_ABS >> b) & 1) ? 2 : 1;
+    TB_NOUNROLL for (int r = 0; r < reps; r++) {
+      if (r == 0 && b != 62) f = fp12_sqr_i(f);
+      TB_NOUNROLL for (int j = 0; j < PER; j++) {
+        if ((usem >> j) & 1u) {
+          const line3 l = line_load(lines, n, i0 + j, s);
+          f = fp12_mul_by_line_i(f, l.a, l.b, l.c);
+        }
+      }
+      extra(s);
+      s++;
+    }
+  }
+#else
   TB_NOUNROLL for (int b = 62; b >= 0; --b) {
     if (b != 62) f = fp12_sqr_i(f);
     TB_UNROLL for (int j = 0; j < PER; j++) {
@@ -256,6 +283,7 @@ __device__ TB_INLINE void miller_acc_body(const uint4* __restrict__ lines, const
       s++;
     }
   }
+#endif
   f_out[t] = fp12_conj(f);
 }
 
@@ -263,12 +291,12 @@ extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_MIN_WAVES)
     k_miller_acc1(const uint4* __restrict__ lines, const uint8_t* __restrict__ skip, const uint8_t* __restrict__ code_a,
                   const uint8_t* __restrict__ code_b, uint32_t n, const uint4* __restrict__ xlines, const uint8_t* __restrict__ xskip,
                   uint32_t n_extra, fp12* __restrict__ f) {
-  miller_acc_body<1>(lines, skip, code_a, code_b, n, xlines, xskip, n_extra, f);
+  miller_acc_body<1, TB_SPREAD_EXTRA != 0>(lines, skip, code_a, code_b, n, xlines, xskip, n_extra, f);
 }
 
 extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_MIN_WAVES)
     k_miller_acc2(const uint4* __restrict__ lines, const uint8_t* __restrict__ skip, const uint8_t* __restrict__ code_a,
                   const uint8_t* __restrict__ code_b, uint32_t n, const uint4* __restrict__ xlines, const uint8_t* __restrict__ xskip,
                   uint32_t n_extra, fp12* __restrict__ f) {
-  miller_acc_body<2>(lines, skip, code_a, code_b, n, xlines, xskip, n_extra, f);
+  miller_acc_body<2, TB_SPREAD_EXTRA != 0>(lines, skip, code_a, code_b, n, xlines, xskip, n_extra, f);
 }
