@@ -350,7 +350,7 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
   // alone after the others finish.
   TB_EV(6, sh);
   if (n && n <= TB_HASH_WAVE_MAX)  // one workgroup per set: the cofactor clearing lane-parallel
-    hipLaunchKernelGGL(k_set_hash_wave, dim3(n), dim3(64), 0, sh, b.msgs, b.msg_off, dst, dlen, n, Q, skip);
+    hipLaunchKernelGGL(k_set_hash_wave, dim3(n), dim3(128), 0, sh, b.msgs, b.msg_off, dst, dlen, n, Q, skip);
   else if (n)
     hipLaunchKernelGGL(k_set_hash, g, blk, 0, sh, b.msgs, b.msg_off, dst, dlen, n, Q, skip);
   TB_EV(7, sh);
