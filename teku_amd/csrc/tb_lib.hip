@@ -268,8 +268,11 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
   // bucket-sum chain on a side stream; 0: the three per-set streams run
   // concurrently (small batches always do).
   static const int order_env = getenv("TBLS_ORDER") ? atoi(getenv("TBLS_ORDER")) : TB_ORDER_DEFAULT;
-  const bool chain = !serial && pp.msm && order_env == 1;
-  hipStream_t sa = (serial || chain) ? s : c.aux[0], sb = serial ? s : c.aux[1], sh = (serial || chain) ? s : c.aux[2];
+  // TBLS_ORDER=2: hash then signatures on the caller's stream, the keys beside
+  // them on aux[0] (A/B).
+  const bool chain = !serial && pp.msm && (order_env == 1 || order_env == 2);
+  const bool hash_first = chain && order_env == 2;
+  hipStream_t sa = (serial || (chain && !hash_first)) ? s : c.aux[0], sb = serial ? s : c.aux[1], sh = (serial || chain) ? s : c.aux[2];
   hipStream_t ssig = chain ? s : sb;
 #define TB_EV(i, st) \
   if (ev) HIPCHK(hipEventRecord(ev[i], st))
@@ -285,6 +288,19 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
     HIPCHK(hipStreamWaitEvent(sa, c.e_fork, 0));
     HIPCHK(hipStreamWaitEvent(sb, c.e_fork, 0));
     HIPCHK(hipStreamWaitEvent(sh, c.e_fork, 0));
+  }
+  auto launch_hash = [&]() -> int {
+    TB_EV(6, sh);
+    if (n && n <= TB_HASH_WAVE_MAX)  // one workgroup per set: the cofactor clearing lane-parallel
+      hipLaunchKernelGGL(k_set_hash_wave, dim3(n), dim3(128), 0, sh, b.msgs, b.msg_off, dst, dlen, n, Q, skip);
+    else if (n)
+      hipLaunchKernelGGL(k_set_hash, g, blk, 0, sh, b.msgs, b.msg_off, dst, dlen, n, Q, skip);
+    TB_EV(7, sh);
+    return TBLS_SUCCESS;
+  };
+  if (hash_first) {
+    const int rc = launch_hash();
+    if (rc != TBLS_SUCCESS) return rc;
   }
   // --- stream b: signatures, then (large batches) the bucket sums -----------
   uint32_t* msm_cnt = (uint32_t*)(w + L.msm_cnt);
@@ -348,12 +364,10 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
   // priority its waves are dispatched first and the shorter key / signature
   // stages fill the SIMDs around them, instead of its last waves running
   // alone after the others finish.
-  TB_EV(6, sh);
-  if (n && n <= TB_HASH_WAVE_MAX)  // one workgroup per set: the cofactor clearing lane-parallel
-    hipLaunchKernelGGL(k_set_hash_wave, dim3(n), dim3(128), 0, sh, b.msgs, b.msg_off, dst, dlen, n, Q, skip);
-  else if (n)
-    hipLaunchKernelGGL(k_set_hash, g, blk, 0, sh, b.msgs, b.msg_off, dst, dlen, n, Q, skip);
-  TB_EV(7, sh);
+  if (!hash_first) {
+    const int rc = launch_hash();
+    if (rc != TBLS_SUCCESS) return rc;
+  }
   if (!serial) {
     HIPCHK(hipEventRecord(c.e_join[2], sh));
     HIPCHK(hipStreamWaitEvent(s, c.e_join[2], 0));
