@@ -212,6 +212,17 @@ int tbls_dev_batch_stage_profile(int device, const tbls_dev_batch* b, void* stre
  * exponentiation: *ok = 1 iff no invalid set and the product is 1. */
 int tbls_dev_final_verify(int device, const void* partials, uint32_t g, void* stream, int* ok);
 
+/* Asynchronous form for a pipelined service (the final exponentiation of one
+ * batch overlapping the next batch's stages): queues the same work on
+ * `stream` and writes the verdict (1 / 0) to *ok_dev in DEVICE memory;
+ * returns without synchronizing.  The records must stay untouched until the
+ * work on `stream` has run.  One in flight per device at a time: calls on one
+ * stream serialize, calls on different streams of one device must not
+ * overlap (they share the function's workspace).  Replaces the synchronous
+ * completeBatchVerify tail (BlstBLS12381.java:184-189) for services that keep
+ * several batches in flight. */
+int tbls_dev_final_verify_async(int device, const void* partials, uint32_t g, void* stream, int* ok_dev);
+
 /* ---- batched generation of synthetic workloads (sk big-endian, 32 B) ---- */
 int tbls_sk_to_pk_many(const uint8_t* sks, size_t n, uint8_t* out /* n*48 */);
 int tbls_sign_many(const uint8_t* sks, const uint8_t* msgs, const uint32_t* msg_off /* n+1 */, size_t n, const uint8_t* dst,

@@ -78,6 +78,7 @@ struct dev_ctx {
   std::mutex mu;
   dbuf in, ws;  // device input staging, pipeline workspace
   dbuf fin;     // final-exponentiation scratch
+  dbuf fin_async;  // tbls_dev_final_verify_async's scratch
   dbuf dstb;    // default DST for the device-resident API
   hipStream_t aux[3] = {nullptr, nullptr, nullptr};  // concurrent per-set stages (aux[2]: high priority, hash_to_G2)
   dbuf tab_aff, tab_code;                    // device-resident public-key table (tbls_pk_table_load)
@@ -861,6 +862,7 @@ extern "C" void tbls_shutdown(void) {
     if (c->in.p) (void)hipFree(c->in.p);
     if (c->ws.p) (void)hipFree(c->ws.p);
     if (c->fin.p) (void)hipFree(c->fin.p);
+    if (c->fin_async.p) (void)hipFree(c->fin_async.p);
     if (c->dstb.p) (void)hipFree(c->dstb.p);
     if (c->recs.p) (void)hipFree(c->recs.p);
     if (c->comb.p) (void)hipFree(c->comb.p);
@@ -1445,6 +1447,34 @@ extern "C" int tbls_sign_many(const uint8_t* sks, const uint8_t* msgs, const uin
                        (const uint32_t*)(d + oo), d + od, (uint32_t)dlen, (uint32_t)n, c.ws.as<uint8_t>(0));
     return fetch(c, out, c.ws.p, 96 * n);
   });
+}
+
+// Asynchronous final verification (pipelined services): the product of the
+// records and the final exponentiation queued on `s`, the verdict written to
+// device memory; its own workspace (fin_async), no host synchronization.
+int launch_final_async(dev_ctx& c, const void* recs, uint32_t g, hipStream_t s, int* ok_dev) {
+  const size_t need = align_up((size_t)g * sizeof(fp12)) + align_up(sizeof(fp12)) + 256;
+  if (need > c.fin_async.cap) {  // growing frees the old buffer: drain its users first
+    HIPCHK(hipStreamSynchronize(s));
+    if (c.fin_async.ensure(need)) return TBLS_DEVICE_ERROR;
+  }
+  uint8_t* w = c.fin_async.as<uint8_t>();
+  fp12* f = (fp12*)w;
+  uint32_t* nbad = (uint32_t*)(w + align_up((size_t)g * sizeof(fp12)) + align_up(sizeof(fp12)));
+  hipLaunchKernelGGL(k_gather_partials, dim3(1), dim3(64), 0, s, (const uint8_t*)recs, g, f, nbad);
+  hipLaunchKernelGGL(k_final_verify_wave, dim3(1), dim3(64), 0, s, (const fp12*)f, g, (const uint32_t*)nbad, ok_dev);
+  HIPCHK(hipGetLastError());
+  return TBLS_SUCCESS;
+}
+
+extern "C" int tbls_dev_final_verify_async(int device, const void* partials, uint32_t g, void* stream, int* ok_dev) {
+  if (!partials || !ok_dev || g == 0) return TBLS_BAD_ARGUMENT;
+  if (ensure_init()) return TBLS_DEVICE_ERROR;
+  dev_ctx* c = ctx_for(device);
+  if (!c) return TBLS_DEVICE_ERROR;
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIPCHK(hipSetDevice(c->dev));
+  return launch_final_async(*c, partials, g, stream ? (hipStream_t)stream : c->stream, ok_dev);
 }
 
 extern "C" int tbls_dev_final_verify(int device, const void* partials, uint32_t g, void* stream, int* ok) {

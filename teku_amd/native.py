@@ -150,6 +150,10 @@ _SIGS = {
         ctypes.c_int,
         [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)],
     ),
+    "tbls_dev_final_verify_async": (
+        ctypes.c_int,
+        [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p],
+    ),
     "tbls_dev_batch_partial_timed": (
         ctypes.c_int,
         [ctypes.c_int, ctypes.POINTER(TblsDevBatch), ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_float)],

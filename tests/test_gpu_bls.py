@@ -149,6 +149,16 @@ def test_simulated_shards_equal_single_device(hip, sets8):
     native.check(L.tbls_dev_final_verify(0, recs.data_ptr(), 2, stream, ctypes.byref(ok)), "final")
     assert ok.value == 0
     assert pks_bak is pks
+    # the asynchronous form (pipelined services): verdicts in device memory,
+    # the same as the synchronous call's, on a second stream
+    s2 = torch.cuda.Stream(dev)
+    good = torch.cat([shard(0, 4), shard(4, 8)])
+    oks = torch.full((2,), 7, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+    native.check(L.tbls_dev_final_verify_async(0, good.data_ptr(), 2, s2.cuda_stream, oks[0:1].data_ptr()), "final_async")
+    native.check(L.tbls_dev_final_verify_async(0, recs.data_ptr(), 2, s2.cuda_stream, oks[1:2].data_ptr()), "final_async")
+    torch.cuda.synchronize()
+    assert oks.tolist() == [1, 0]
 
 
 def test_hash_sign_keys_bit_exact(hip):
