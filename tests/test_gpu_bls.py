@@ -369,22 +369,29 @@ def test_validator_key_table(hip, sets8):
     assert table.size == 10 and L.tbls_pk_table_size() == 10
     assert table.codes[:8] == [0] * 8
     assert table.codes[8] == native.PK_IS_INFINITY and table.codes[9] != 0
+    tab_keys = pkb + [inf_pk, BAD_PK]
+
+    def oracle(batch):  # the pinned oracle on the same sets, keys by bytes
+        return O.batch_verify([[tab_keys[k] for k in ks] for ks, _, _ in batch], [m_ for _, m_, _ in batch], [s_ for _, _, s_ in batch])
+
     sets = [([i], msgs[i], sigs[i]) for i in range(8)]
     rands = [random.getrandbits(64) | 1 for _ in sets]
-    assert table.batch_verify(sets, rands)
+    assert table.batch_verify(sets, rands) is oracle(sets) is True
     assert _raw(bls, pkb, msgs, sigs, rands)
     bad = list(sets)
     bad[3] = ([3], msgs[3], sigs[4])
-    assert not table.batch_verify(bad, rands)
+    assert table.batch_verify(bad, rands) is oracle(bad) is False
     for k in (8, 9):
         bad = list(sets)
         bad[2] = ([2, k], msgs[2], sigs[2])
-        assert not table.batch_verify(bad, rands)
+        assert table.batch_verify(bad, rands) is oracle(bad) is False
     # one set signed by keys 0..3 on one message (fastAggregateVerify shape)
     m = b"\x42" * 32
     agg = O.aggregate_sigs([O.sign(sks[i], m) for i in range(4)])
-    assert table.batch_verify(sets + [([0, 1, 2, 3], m, agg)], rands + [12345])
-    assert not table.batch_verify(sets + [([0, 1, 2, 5], m, agg)], rands + [12345])
+    good4 = sets + [([0, 1, 2, 3], m, agg)]
+    bad4 = sets + [([0, 1, 2, 5], m, agg)]
+    assert table.batch_verify(good4, rands + [12345]) is oracle(good4) is True
+    assert table.batch_verify(bad4, rands + [12345]) is oracle(bad4) is False
     with pytest.raises(ValueError):
         table.batch_verify([([10], msgs[0], sigs[0])], [1])
 
