@@ -8,7 +8,7 @@
 namespace tb {
 
 struct cf_lds {
-  fp S[CF_NSLOT];
+  fp S[2 * CF_NSLOT];  // values, then their negations (tb_mprog.h wprog_level)
   u13 part[64];
   uint16_t tab[CF_TAB_N];
   g2j J;
@@ -44,9 +44,9 @@ __device__ TB_INLINE void cf_load_lane0(cf_lds& L, const g2j& h) {
 // recomputes with the one-lane g2_clear_cofactor, so the result is always
 // the one-lane code's.
 __device__ TB_INLINE void cf_run(cf_lds& L, g2a& a, bool& ok) {
-  __syncthreads();
+  wprog_negate_all<CF_NSLOT>(L.S);
   for (int k = 0; k < CF_NLEVEL; k++)
-    wprog_level<CF_AMAX, CF_BMAX, CF_QMAX, CF_OMAX>(L.S, L.part, L.tab, CF_TYPE_OFF[CF_SEQ[k]]);
+    wprog_level<CF_AMAX, CF_BMAX, CF_QMAX, CF_OMAX, CF_NSLOT>(L.S, L.part, L.tab, CF_TYPE_OFF[CF_SEQ[k]]);
   ok = true;
   if (threadIdx.x == 0) {
     const fp2 X = {L.S[CF_S_RX0], L.S[CF_S_RX1]}, Y = {L.S[CF_S_RY0], L.S[CF_S_RY1]}, Z = {L.S[CF_S_RZ0], L.S[CF_S_RZ1]};

@@ -17,28 +17,51 @@
 namespace tb {
 
 struct mprog_lds {
-  fp S[MP_NSLOT];
+  fp S[2 * MP_NSLOT];  // values, then their negations 2p - v (wprog_level)
   u13 part[64];
   uint16_t tab[MP_TAB_N];
 };
 
-// acc += sum over entries [b, e) of coef * S[slot] (carry-save columns,
-// tb_fp12_wave.h cs_term)
-template <int MAXLEN>
+// Every slot is kept twice: S[k] = v and S[NSLOT + k] = 2p - v (written by
+// the same lane that writes v), so a negative coefficient reads the negated
+// copy and every term is a plain non-negative multiply-accumulate
+// (cs_term_pos: no complement, no correction) -- the sums are half the
+// instructions of the levels.
+__device__ TB_INLINE fp fp_neg2p(const fp& v) {  // 2p - v, in (0, 2p] for v in [0, 2p)
+  fp r;
+  uint32_t br = 0;
+  TB_UNROLL for (int i = 0; i < 12; i++) r.l[i] = subc32(P2_MOD[i], v.l[i], br, &br);
+  return r;
+}
+
+__device__ TB_INLINE void cs_term_pos(c13& a, const fp& v, uint32_t m) {
+  TB_UNROLL for (int i = 0; i < 12; i++) a.c[i] = (uint64_t)v.l[i] * m + a.c[i];
+}
+
+// acc += sum over entries [b, e) of coef * S[slot] (carry-save columns)
+template <int MAXLEN, int NSLOT>
 __device__ TB_INLINE void mp_csum(c13& acc, const fp* S, const uint16_t* ent, int b, int e) {
   TB_UNROLL for (int t = 0; t < MAXLEN; t++) {
     if (b + t < e) {
       const uint32_t slot = ent[2 * (b + t)];
       const int c = (int16_t)ent[2 * (b + t) + 1];
-      cs_term(acc, S[slot], (uint32_t)(c < 0 ? -c : c), c < 0);
+      cs_term_pos(acc, S[c < 0 ? NSLOT + slot : slot], (uint32_t)(c < 0 ? -c : c));
     }
   }
+}
+
+// negated copies of slots [0, NSLOT) after an initialization (whole workgroup)
+template <int NSLOT>
+__device__ TB_INLINE void wprog_negate_all(fp* S) {
+  __syncthreads();
+  for (int k = threadIdx.x; k < NSLOT; k += blockDim.x) S[NSLOT + k] = fp_neg2p(S[k]);
+  __syncthreads();
 }
 
 // One level of a generated program (tables staged in LDS at `tab`, this
 // level type's block at tab + off): products, partial sums, outputs.  The
 // term-count bounds are the program's (MP_AMAX ..., CF_AMAX ...).
-template <int AMAX, int BMAX, int QMAX, int OMAX>
+template <int AMAX, int BMAX, int QMAX, int OMAX, int NSLOT>
 __device__ TB_INLINE void wprog_level(fp* S, u13* part, const uint16_t* tab, int off) {
   const int l = threadIdx.x;
   const uint16_t* H = tab + off;
@@ -54,15 +77,17 @@ __device__ TB_INLINE void wprog_level(fp* S, u13* part, const uint16_t* tab, int
     c13 a, b;
     cs_zero(a);
     cs_zero(b);
-    mp_csum<AMAX>(a, S, ent, abeg[l], abeg[l + 1]);
-    mp_csum<BMAX>(b, S, ent, bbeg[l], bbeg[l + 1]);
-    S[pout[l]] = fp_mul13(cs_norm(a), cs_norm(b));
+    mp_csum<AMAX, NSLOT>(a, S, ent, abeg[l], abeg[l + 1]);
+    mp_csum<BMAX, NSLOT>(b, S, ent, bbeg[l], bbeg[l + 1]);
+    const fp pr = fp_mul13(cs_norm(a), cs_norm(b));
+    S[pout[l]] = pr;
+    S[NSLOT + pout[l]] = fp_neg2p(pr);
   }
   __syncthreads();
   if (l < nq) {
     c13 acc;
     cs_zero(acc);
-    mp_csum<QMAX>(acc, S, ent, qbeg[l], qbeg[l + 1]);
+    mp_csum<QMAX, NSLOT>(acc, S, ent, qbeg[l], qbeg[l + 1]);
     part[l] = cs_norm(acc);
   }
   __syncthreads();
@@ -78,12 +103,15 @@ __device__ TB_INLINE void wprog_level(fp* S, u13* part, const uint16_t* tab, int
     dst = odst[l];
   }
   __syncthreads();
-  if (l < no) S[dst] = r;
+  if (l < no) {
+    S[dst] = r;
+    S[NSLOT + dst] = fp_neg2p(r);
+  }
   __syncthreads();
 }
 
 __device__ TB_INLINE void mp_level(mprog_lds& L, int type) {
-  wprog_level<MP_AMAX, MP_BMAX, MP_QMAX, MP_OMAX>(L.S, L.part, L.tab, MP_TYPE_OFF[type]);
+  wprog_level<MP_AMAX, MP_BMAX, MP_QMAX, MP_OMAX, MP_NSLOT>(L.S, L.part, L.tab, MP_TYPE_OFF[type]);
 }
 
 // f_{|x|,Q}(P) (up to a factor in Fp), conjugated, into L.S[0..12) -- the
@@ -107,7 +135,7 @@ __device__ TB_INLINE void miller_loop_prog(mprog_lds& L, const g1a& P, const g2a
     L.S[MP_S_PX] = P.x;
     L.S[MP_S_PY] = P.y;
   }
-  __syncthreads();
+  wprog_negate_all<MP_NSLOT>(L.S);
   for (int k = 0; k < MP_NLEVEL; k++) mp_level(L, MP_SEQ[k]);
   w_conj(L.S + MP_S_F0, L.S + MP_S_F0);
 }
