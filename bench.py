@@ -163,11 +163,26 @@ def cpu_model():
 
 
 def cpu_threads():
-    n = os.cpu_count() or 1
-    for var in ("OMP_NUM_THREADS", "MAX_JOBS"):  # the box's CPU share
+    """(threads, env_cap, quota): the CPUs this process may run on
+    (sched_getaffinity -- BASELINE.md's `nproc`), the environment's thread cap
+    (OMP_NUM_THREADS / MAX_JOBS: the box's CPU share) and the cgroup CPU quota
+    in cores (cpu.max; None when unlimited or unreadable)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    cap = None
+    for var in ("OMP_NUM_THREADS", "MAX_JOBS"):
         if os.environ.get(var, "").isdigit():
-            n = min(n, int(os.environ[var]))
-    return max(1, n)
+            cap = min(cap or n, int(os.environ[var]))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    return max(1, n), cap, quota
 
 
 def cpu_baseline_oracle(pks, msgs, sigs, sample_sets=4096, sample_1t=512):
@@ -177,7 +192,7 @@ def cpu_baseline_oracle(pks, msgs, sigs, sample_sets=4096, sample_1t=512):
     the p50 of a 128-set batch (config 1) on every core."""
     from oracle import c_oracle as C
 
-    T = cpu_threads()
+    T, cap, quota = cpu_threads()
     pk = [pks[48 * j : 48 * j + 48] for j in range(sample_sets)]
     ms = [msgs[32 * j : 32 * j + 32] for j in range(sample_sets)]
     sg = [sigs[96 * j : 96 * j + 96] for j in range(sample_sets)]
@@ -189,6 +204,11 @@ def cpu_baseline_oracle(pks, msgs, sigs, sample_sets=4096, sample_1t=512):
     assert C.batch_verify(pk[:sample_1t], ms[:sample_1t], sg[:sample_1t], rr[:sample_1t], threads=1)
     dt1 = time.perf_counter() - t0
     lat = timed(lambda: C.batch_verify(pk[:128], ms[:128], sg[:128], rr[:128], threads=T), 7)
+    dt_cap = None
+    if cap and cap < T:  # the same sample on the environment's thread cap
+        t0 = time.perf_counter()
+        assert C.batch_verify(pk, ms, sg, rr, threads=cap)
+        dt_cap = time.perf_counter() - t0
     return {
         "value": sample_sets / dt,
         "unit": "sigs/s",
@@ -197,6 +217,10 @@ def cpu_baseline_oracle(pks, msgs, sigs, sample_sets=4096, sample_1t=512):
         "sample": f"oracle/c batch_verify of the first {sample_sets} sets of this workload on {T} pthreads ({dt:.1f} s) and of the first "
         f"{sample_1t} on 1 thread ({dt1:.1f} s); the build's own C restatement (6x64-bit CIOS Montgomery), not blst",
         "value_1thread": sample_1t / dt1,
+        "threads_affinity": T,
+        "env_thread_cap": cap,
+        "value_env_cap": sample_sets / dt_cap if dt_cap else None,
+        "cgroup_cpu_quota_cores": quota,
         "cpu_model": cpu_model(),
         "machine_cpus": os.cpu_count(),
         "p50_latency_ms_128": statistics.median(lat),
@@ -380,6 +404,7 @@ def main():
     ap.add_argument("--extra-reps", type=int, default=20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip configs 2/3/4")
+    ap.add_argument("--no-1m", action="store_true", help="skip config 5 at its full 1,048,576-set size on this one GPU")
     ap.add_argument("--serial", action="store_true", help="timed steps with every stage alone on the stream (profiling)")
     ap.add_argument("--no-kzg", action="store_true", help="skip the KZG leg (SURVEY.md 8(f) rank 4)")
     ap.add_argument("--kzg-only", action="store_true", help="profiling: run only the KZG leg and print its JSON")
@@ -481,6 +506,38 @@ def main():
         dist.destroy_process_group()
         return
 
+    # Config 5 at its stated size (1,048,576 sets) on this one GPU: one device
+    # batch of all sets (offsets, the bucket MSM and 4 line-buffer chunks at
+    # 1M); single-GPU runs only (the driver's N>1 runs shard config 5 instead).
+    one_m = None
+    if world == 1 and not args.no_1m:
+        n1m = 1 << 20
+        del batch
+        t_g = time.perf_counter()
+        pk1, ms1, sg1 = synth.single_signer(0, n1m, seed=5)
+        b1m = DevBatch(pk1, [1] * n1m, ms1, [32] * n1m, sg1, device)
+        del pk1, ms1, sg1
+        gen1 = time.perf_counter() - t_g
+
+        def step_1m():
+            native.check(L.tbls_dev_batch_partial(local, ctypes.byref(b1m.desc), stream, partial.data_ptr()), "partial_1m")
+            native.check(L.tbls_dev_final_verify(local, partial.data_ptr(), 1, stream, ctypes.byref(ok)), "final_1m")
+            if ok.value != 1:
+                raise RuntimeError("valid synthetic 1M batch rejected")
+
+        step_1m()
+        torch.cuda.synchronize()
+        k1m = 3
+        t0 = time.perf_counter()
+        for _ in range(k1m):
+            step_1m()
+        torch.cuda.synchronize()
+        dt1m = (time.perf_counter() - t0) / k1m
+        one_m = {"value": n1m / dt1m, "unit": "sigs/s", "ms_per_batch": dt1m * 1e3, "steps": k1m, "gen_s": gen1,
+                 "what": "config 5 at 1,048,576 sets as ONE device batch on this GPU (partial + final exponentiation, inputs in HBM)"}
+        del b1m
+        batch = DevBatch(pks, [1] * S, msgs, [32] * S, sigs, device)  # the profiled steps below use the 131k shard
+
     stage_ms = [a / args.steps for a in stage_acc]
     # Exclusive per-stage kernel times (every stage alone on the stream): the
     # roofline's denominators.  In the timed steps the stages overlap, so
@@ -523,6 +580,8 @@ def main():
             "parallelism": "data-parallel shards, dp%d" % world,
         },
         "serial_stages": bool(args.serial),
+        "value_1m": one_m["value"] if one_m else None,
+        "config5_1m": one_m,
         "value_key_table": total_sets / dt_tab,
         "ms_per_step_key_table": dt_tab / args.steps * 1e3,
         "key_table": "value_key_table: same steps with keys from the device-resident validator table (%d keys decompressed "

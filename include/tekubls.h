@@ -215,12 +215,12 @@ int tbls_dev_final_verify(int device, const void* partials, uint32_t g, void* st
 /* Asynchronous form for a pipelined service (the final exponentiation of one
  * batch overlapping the next batch's stages): queues the same work on
  * `stream` and writes the verdict (1 / 0) to *ok_dev in DEVICE memory;
- * returns without synchronizing.  The records must stay untouched until the
- * work on `stream` has run.  One in flight per device at a time: calls on one
- * stream serialize, calls on different streams of one device must not
- * overlap (they share the function's workspace).  Replaces the synchronous
- * completeBatchVerify tail (BlstBLS12381.java:184-189) for services that keep
- * several batches in flight. */
+ * returns without synchronizing.  The kernel reads the records in place and
+ * writes nothing but *ok_dev, so calls may overlap freely on any streams; the
+ * caller orders `stream` after the work that wrote the records (an event) and
+ * keeps the records untouched until the work on `stream` has run.  Replaces
+ * the synchronous completeBatchVerify tail (BlstBLS12381.java:184-189) for
+ * services that keep several batches in flight. */
 int tbls_dev_final_verify_async(int device, const void* partials, uint32_t g, void* stream, int* ok_dev);
 
 /* ---- batched generation of synthetic workloads (sk big-endian, 32 B) ---- */

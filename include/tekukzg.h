@@ -73,8 +73,9 @@ int tkzg_compute_kzg_proof(uint8_t proof_out[48], uint8_t y_out[32], const uint8
 int tkzg_verify_kzg_proof(int* ok, const uint8_t commitment[48], const uint8_t z[32], const uint8_t y[32], const uint8_t proof[48]);
 
 /* Device-resident batch (bench / service use): d_blobs, d_commitments and
- * d_proofs already in device-0 memory; stream a hipStream_t (NULL: the
- * library's own).  Blocks until the verdict is known. */
+ * d_proofs already in device-0 memory, each 16-byte aligned (the kernels read
+ * them as 16-byte vectors; a misaligned pointer -> TKZG_BADARGS); stream a
+ * hipStream_t (NULL: the library's own).  Blocks until the verdict is known. */
 int tkzg_dev_verify_blob_kzg_proof_batch(int* ok, const uint8_t* d_blobs, const uint8_t* d_commitments, const uint8_t* d_proofs, size_t count,
                                          void* stream);
 
@@ -89,7 +90,8 @@ int tkzg_last_stage_ms(float ms[6]);
 
 /* Test hook: the batch's per-blob challenges z_i and evaluations y_i (32 bytes
  * big-endian each) and the batch challenge r, as computed on the device by
- * the last verify call (n == 1: r is zero). */
+ * the last verify call (n == 1: r is zero).  Any other call in between (which
+ * may reuse the workspace) forgets the transcript: TKZG_BADARGS. */
 int tkzg_last_transcript(uint8_t* zs, uint8_t* ys, size_t n, uint8_t r[32]);
 
 /* Message of the last TKZG_BADARGS / TKZG_ERROR on this thread (the JNI

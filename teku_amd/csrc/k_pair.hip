@@ -60,6 +60,29 @@ extern "C" __global__ void __launch_bounds__(64) k_final_verify_wave(const fp12*
   if (threadIdx.x == 0) result[0] = (n_bad[0] == 0 && fp12_is_one(fp12_from_coords(L.F))) ? 1 : 0;
 }
 
+// The same verdict straight from g partial records (TB_PARTIAL_BYTES apart:
+// the 576-byte Fp12 product, then the uint32 invalid-set count), as the
+// records come from tbls_dev_batch_partial / the multi-GPU gather.  Reads
+// only the caller's records and writes only *result: no device scratch, so
+// any number of these may be in flight on different streams at once.
+extern "C" __global__ void __launch_bounds__(64) k_final_verify_recs(const uint8_t* __restrict__ recs, uint32_t g,
+                                                                     int* __restrict__ result) {
+  __shared__ final_exp_lds L;
+  tb_latency_prio();
+  w12_tabs_load(L.s);
+  w_load(L.F, reinterpret_cast<const fp12*>(recs));
+  for (uint32_t i = 1; i < g; i++) {
+    w_load(L.X, reinterpret_cast<const fp12*>(recs + (size_t)i * TB_PARTIAL_BYTES));
+    w_mul(L.F, L.F, L.X, L.s);
+  }
+  final_exp_wave(L);
+  if (threadIdx.x == 0) {
+    uint32_t bad = 0;
+    for (uint32_t i = 0; i < g; i++) bad += *reinterpret_cast<const uint32_t*>(recs + (size_t)i * TB_PARTIAL_BYTES + sizeof(fp12));
+    result[0] = (bad == 0 && fp12_is_one(fp12_from_coords(L.F))) ? 1 : 0;
+  }
+}
+
 // single-lane reference version (kept for A/B timing)
 extern "C" __global__ void k_final_verify(const fp12* __restrict__ f, const uint32_t* __restrict__ n_bad, int* __restrict__ result) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;

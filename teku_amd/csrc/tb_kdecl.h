@@ -90,3 +90,5 @@ extern "C" __global__ void k_fp12_one(fp12* __restrict__ f);
 extern "C" __global__ void k_fp12_prod_wave(const fp12* __restrict__ in, uint32_t n, uint32_t chunk, fp12* __restrict__ out);
 extern "C" __global__ void k_final_verify_wave(const fp12* __restrict__ f, uint32_t g, const uint32_t* __restrict__ n_bad, int* __restrict__ result);
 extern "C" __global__ void k_final_verify(const fp12* __restrict__ f, const uint32_t* __restrict__ n_bad, int* __restrict__ result);
+#define TB_PARTIAL_BYTES 580u  // one device's partial record (= TBLS_PARTIAL_BYTES, include/tekubls.h)
+extern "C" __global__ void k_final_verify_recs(const uint8_t* __restrict__ recs, uint32_t g, int* __restrict__ result);

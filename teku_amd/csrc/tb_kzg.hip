@@ -17,6 +17,7 @@
 
 #include "../../include/tekukzg.h"
 #include "tb_kzg_decl.h"
+#include "tb_host.h"
 
 using namespace tb;
 
@@ -284,11 +285,16 @@ int prove(kzg_state& g, const uint8_t* blob, const uint8_t* com, const uint8_t* 
   return TKZG_OK;
 }
 
+// Every call that may reuse or reallocate the workspace drops the last
+// verify's transcript pointers first (they point into it); only
+// tkzg_last_transcript reads them (keep_transcript).
 template <typename F>
-int with_setup(F&& fn) {
+int with_setup(F&& fn, bool keep_transcript = false) {
+  const tb::caller_device keep;
   kzg_state& g = st();
   std::lock_guard<std::mutex> lk(g.mu);
   if (!g.loaded) return fail(TKZG_ERROR, "Trusted Setup is not loaded.");
+  if (!keep_transcript) g.last_n = 0;
   KCHK(hipSetDevice(0));
   return fn(g);
 }
@@ -315,6 +321,7 @@ void free_setup(kzg_state& g) {
 extern "C" int tkzg_load_trusted_setup(const uint8_t* g1_monomial, size_t g1_monomial_len, const uint8_t* g1_lagrange, size_t g1_lagrange_len,
                                        const uint8_t* g2_monomial, size_t g2_monomial_len, uint64_t precompute) {
   (void)precompute;
+  const tb::caller_device keep;
   kzg_state& g = st();
   std::lock_guard<std::mutex> lk(g.mu);
   if (g1_monomial_len != 48u * N) return fail(TKZG_BADARGS, "Invalid g1MonomialBytes size. Expected %u bytes but got %zu.", 48u * N, g1_monomial_len);
@@ -376,6 +383,7 @@ extern "C" int tkzg_free_trusted_setup(void) {
   kzg_state& g = st();
   std::lock_guard<std::mutex> lk(g.mu);
   if (!g.loaded) return fail(TKZG_ERROR, "Trusted Setup is not loaded.");
+  const tb::caller_device keep;
   (void)hipSetDevice(0);
   free_setup(g);
   return TKZG_OK;
@@ -409,6 +417,10 @@ static int dev_verify(int* ok, const uint8_t* d_blobs, const uint8_t* d_commitme
       *ok = 1;
       return (int)TKZG_OK;
     }
+    // the challenge and evaluation kernels read blobs and commitments as
+    // 16-byte vectors (k_kzg.hip)
+    if (((uintptr_t)d_blobs | (uintptr_t)d_commitments | (uintptr_t)d_proofs) & 15u)
+      return fail(TKZG_BADARGS, "device blobs, commitments and proofs must be 16-byte aligned");
     if (g.ws.ensure(verify_ws_bytes(count))) return fail(TKZG_MALLOC, "workspace allocation failed");
     return verify_dev(g, d_blobs, d_commitments, d_proofs, count, stream ? (hipStream_t)stream : g.s, g.ws.b(), ok, timed);
   });
@@ -541,7 +553,7 @@ extern "C" int tkzg_last_transcript(uint8_t* zs, uint8_t* ys, size_t n, uint8_t 
     memcpy(ys, h.data() + 32 * n, 32 * n);
     memcpy(r_out, h.data() + 64 * n, 32);
     return (int)TKZG_OK;
-  });
+  }, /*keep_transcript=*/true);
 }
 
 extern "C" const char* tkzg_last_error(void) { return t_err.c_str(); }

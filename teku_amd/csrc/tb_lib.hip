@@ -12,6 +12,7 @@
 #include <mutex>
 #include <algorithm>
 #include <dlfcn.h>
+#include <map>
 #include <sys/random.h>
 #include <rccl/rccl.h>  // types and prototypes only: RCCL is resolved with dlopen (gather_partials)
 #include <thread>
@@ -20,6 +21,11 @@
 
 #include "../../include/tekubls.h"
 #include "tb_kdecl.h"
+#include "tb_host.h"
+
+static_assert(TB_PARTIAL_BYTES == TBLS_PARTIAL_BYTES, "partial record size");
+
+using tb::caller_device;
 
 namespace {
 
@@ -77,8 +83,7 @@ struct dev_ctx {
   hipStream_t stream = nullptr;
   std::mutex mu;
   dbuf in, ws;  // device input staging, pipeline workspace
-  dbuf fin;     // final-exponentiation scratch
-  dbuf fin_async;  // tbls_dev_final_verify_async's scratch
+  dbuf fin;     // the synchronous final verification's verdict word (under the device lock)
   dbuf dstb;    // default DST for the device-resident API
   hipStream_t aux[3] = {nullptr, nullptr, nullptr};  // concurrent per-set stages (aux[2]: high priority, hash_to_G2)
   dbuf tab_aff, tab_code;                    // device-resident public-key table (tbls_pk_table_load)
@@ -437,28 +442,13 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
   return TBLS_SUCCESS;
 }
 
-// final: product of g partial records -> final exponentiation
-__global__ void k_gather_partials(const uint8_t* __restrict__ recs, uint32_t g, fp12* __restrict__ f, uint32_t* __restrict__ n_bad) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  uint32_t bad = 0;
-  for (uint32_t i = 0; i < g; i++) {
-    f[i] = *reinterpret_cast<const fp12*>(recs + (size_t)i * TBLS_PARTIAL_BYTES);
-    bad += *reinterpret_cast<const uint32_t*>(recs + (size_t)i * TBLS_PARTIAL_BYTES + sizeof(fp12));
-  }
-  n_bad[0] = bad;
-}
-
+// final: product of g partial records -> final exponentiation, straight from
+// the records (k_final_verify_recs reads them in place; the only device state
+// it writes is the verdict word)
 int launch_final(dev_ctx& c, const void* recs, uint32_t g, hipStream_t s, int* result_host) {
-  const size_t need = align_up((size_t)g * sizeof(fp12)) + 2 * align_up(sizeof(fp12)) + 256;
-  if (c.fin.ensure(need)) return TBLS_DEVICE_ERROR;
-  uint8_t* w = c.fin.as<uint8_t>();
-  fp12* f = (fp12*)w;
-  fp12* prod = (fp12*)(w + align_up((size_t)g * sizeof(fp12)));
-  uint32_t* nbad = (uint32_t*)(w + align_up((size_t)g * sizeof(fp12)) + align_up(sizeof(fp12)));
-  int* res = (int*)(nbad + 1);
-  hipLaunchKernelGGL(k_gather_partials, dim3(1), dim3(64), 0, s, (const uint8_t*)recs, g, f, nbad);
-  (void)prod;
-  hipLaunchKernelGGL(k_final_verify_wave, dim3(1), dim3(64), 0, s, (const fp12*)f, g, (const uint32_t*)nbad, res);
+  if (c.fin.ensure(256)) return TBLS_DEVICE_ERROR;
+  int* res = c.fin.as<int>();
+  hipLaunchKernelGGL(k_final_verify_recs, dim3(1), dim3(64), 0, s, (const uint8_t*)recs, g, res);
   HIPCHK(hipGetLastError());
   if (c.hout.ensure(16)) return TBLS_DEVICE_ERROR;
   HIPCHK(hipMemcpyAsync(c.hout.p, res, 4, hipMemcpyDeviceToHost, s));
@@ -646,13 +636,17 @@ struct rccl_api {
   decltype(&ncclGather) Gather = nullptr;
   decltype(&ncclGroupStart) GroupStart = nullptr;
   decltype(&ncclGroupEnd) GroupEnd = nullptr;
-  std::vector<ncclComm_t> comms;
+  // One single-process communicator per participating-device count G, over
+  // devices 0 .. G-1: a batch sharded over G < (initialised devices) gathers
+  // on a G-rank communicator, so no rank of the collective is left waiting
+  // (batches smaller than the device count, or n_gpus < device count).
+  std::map<int, std::vector<ncclComm_t>> comms;
 };
 rccl_api g_rccl;
 
 // RCCL resolved at run time (an already-loaded librccl.so.1 -- e.g. torch's --
-// is reused by its soname), one communicator per device; g_mu held.
-bool rccl_ready_locked() {
+// is reused by its soname); g_mu held.
+bool rccl_load_locked() {
   if (g_rccl.tried) return g_rccl.ok;
   g_rccl.tried = true;
   void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
@@ -663,35 +657,47 @@ bool rccl_ready_locked() {
   g_rccl.Gather = (decltype(g_rccl.Gather))dlsym(h, "ncclGather");
   g_rccl.GroupStart = (decltype(g_rccl.GroupStart))dlsym(h, "ncclGroupStart");
   g_rccl.GroupEnd = (decltype(g_rccl.GroupEnd))dlsym(h, "ncclGroupEnd");
-  if (!g_rccl.CommInitAll || !g_rccl.CommDestroy || !g_rccl.Gather || !g_rccl.GroupStart || !g_rccl.GroupEnd) return false;
-  std::vector<int> devs;
-  for (dev_ctx* c : g_ctx) devs.push_back(c->dev);
-  g_rccl.comms.assign(devs.size(), nullptr);
-  if (g_rccl.CommInitAll(g_rccl.comms.data(), (int)devs.size(), devs.data()) != ncclSuccess) {
-    g_rccl.comms.clear();
-    return false;
-  }
-  g_rccl.ok = true;
-  return true;
+  g_rccl.ok = g_rccl.CommInitAll && g_rccl.CommDestroy && g_rccl.Gather && g_rccl.GroupStart && g_rccl.GroupEnd;
+  return g_rccl.ok;
 }
 
-// Device records dpart[g] (on each device's stream) -> c0->recs (device 0)
+// The G-rank communicator (created on first use); nullptr if RCCL is absent.
+const std::vector<ncclComm_t>* rccl_comms_locked(int G) {
+  if (!rccl_load_locked() || G < 1 || G > (int)g_ctx.size()) return nullptr;
+  auto it = g_rccl.comms.find(G);
+  if (it != g_rccl.comms.end()) return &it->second;
+  std::vector<int> devs;
+  for (int g = 0; g < G; g++) devs.push_back(g_ctx[g]->dev);
+  std::vector<ncclComm_t> cm(G, nullptr);
+  if (g_rccl.CommInitAll(cm.data(), G, devs.data()) != ncclSuccess) return nullptr;
+  return &(g_rccl.comms[G] = cm);
+}
+
+// Device records dpart[g] (on each device's stream) -> c0->recs (device 0).
+// Leaves the calling thread on device 0 (the caller's caller_device restores).
 int gather_partials(gather_mode mode, int G, const std::vector<uint8_t*>& dpart) {
   dev_ctx* c0 = ctx_for(0);
   HIPCHK(hipSetDevice(c0->dev));
   if (c0->recs.ensure((size_t)G * TBLS_PARTIAL_BYTES)) return TBLS_DEVICE_ERROR;
   uint8_t* recv = c0->recs.as<uint8_t>();
   if (mode == GATHER_RCCL) {
+    const std::vector<ncclComm_t>* cm = nullptr;
     {
       std::lock_guard<std::mutex> lk(g_mu);
-      if (!rccl_ready_locked()) return TBLS_DEVICE_ERROR;
+      cm = rccl_comms_locked(G);
     }
+    // ncclGather writes comm_size * 580 bytes at the root: recv holds G records
+    if (!cm || (int)cm->size() != G) return TBLS_DEVICE_ERROR;
+    for (int g = 0; g < G; g++) HIPCHK(hipSetDevice(ctx_for(g)->dev));  // every device reachable before the group opens
     if (g_rccl.GroupStart() != ncclSuccess) return TBLS_DEVICE_ERROR;
     int bad = 0;
     for (int g = 0; g < G; g++) {
       dev_ctx* c = ctx_for(g);
-      bad |= hipSetDevice(c->dev) != hipSuccess;
-      bad |= g_rccl.Gather(dpart[g], g == 0 ? recv : nullptr, TBLS_PARTIAL_BYTES, ncclUint8, 0, g_rccl.comms[g], c->stream) != ncclSuccess;
+      if (hipSetDevice(c->dev) != hipSuccess) {  // every rank must still join: the group ends below
+        bad = 1;
+        continue;
+      }
+      bad |= g_rccl.Gather(dpart[g], g == 0 ? recv : nullptr, TBLS_PARTIAL_BYTES, ncclUint8, 0, (*cm)[g], c->stream) != ncclSuccess;
     }
     bad |= g_rccl.GroupEnd() != ncclSuccess;
     if (bad) return TBLS_DEVICE_ERROR;
@@ -747,6 +753,7 @@ struct upload {
 };
 
 int with_device0(const std::function<int(dev_ctx&)>& fn) {
+  const caller_device keep;
   if (ensure_init()) return TBLS_DEVICE_ERROR;
   dev_ctx* c = ctx_for(0);
   std::lock_guard<std::mutex> lk(c->mu);
@@ -813,6 +820,7 @@ bool sk_in_range(const uint8_t sk[32]) {
 // ===========================================================================
 extern "C" int tbls_init(int n_devices, uint32_t flags) {
   (void)flags;
+  const caller_device keep;
   std::lock_guard<std::mutex> lk(g_mu);
   if (g_inited) return g_ctx.empty() ? TBLS_DEVICE_ERROR : TBLS_SUCCESS;
   int count = 0;
@@ -853,8 +861,10 @@ extern "C" int tbls_init(int n_devices, uint32_t flags) {
 
 extern "C" void tbls_shutdown(void) {
   std::lock_guard<std::mutex> lk(g_mu);
+  const caller_device keep;
   if (g_rccl.ok)
-    for (ncclComm_t cm : g_rccl.comms) (void)g_rccl.CommDestroy(cm);
+    for (auto& kv : g_rccl.comms)
+      for (ncclComm_t cm : kv.second) (void)g_rccl.CommDestroy(cm);
   g_rccl.comms.clear();
   g_rccl.ok = g_rccl.tried = false;
   for (dev_ctx* c : g_ctx) {
@@ -862,7 +872,6 @@ extern "C" void tbls_shutdown(void) {
     if (c->in.p) (void)hipFree(c->in.p);
     if (c->ws.p) (void)hipFree(c->ws.p);
     if (c->fin.p) (void)hipFree(c->fin.p);
-    if (c->fin_async.p) (void)hipFree(c->fin_async.p);
     if (c->dstb.p) (void)hipFree(c->dstb.p);
     if (c->recs.p) (void)hipFree(c->recs.p);
     if (c->comb.p) (void)hipFree(c->comb.p);
@@ -893,6 +902,7 @@ extern "C" int tbls_device_count(void) {
 template <class SET>
 int batch_verify_impl(const SET* sets, size_t n, const uint64_t* rand, int n_gpus, int* ok, tbls_timing* t) {
   auto t0 = std::chrono::steady_clock::now();
+  const caller_device keep;
   *ok = 0;
   if (ensure_init()) return TBLS_DEVICE_ERROR;
   if (n == 0) return TBLS_SUCCESS;  // BLS.java:240-241
@@ -966,6 +976,7 @@ extern "C" int tbls_batch_verify(const tbls_set* sets, size_t n, const uint64_t*
 // device-resident public-key table
 // --------------------------------------------------------------------------
 extern "C" int tbls_pk_table_load(const uint8_t* pks, size_t K, uint8_t* codes) {
+  const caller_device keep;
   if (ensure_init()) return TBLS_DEVICE_ERROR;
   if (K == 0 || K > 0xffffffffu / 96) return TBLS_BAD_ARGUMENT;
   std::vector<dev_ctx*> devs;
@@ -1008,6 +1019,7 @@ extern "C" int tbls_batch_verify_idx(const tbls_set_idx* sets, size_t n, const u
 // core_verify through the same pipeline with r = 1 (one set, no randomizer)
 static int verify_one(const uint8_t* pks, uint32_t n_pks, const uint8_t* msg, size_t len, const uint8_t sig[96], const uint8_t* dst,
                       size_t dlen, int* ok, uint8_t* code_out) {
+  const caller_device keep;
   *ok = 0;
   if (ensure_init()) return TBLS_DEVICE_ERROR;
   if (dlen > 255) return TBLS_BAD_ARGUMENT;
@@ -1087,6 +1099,7 @@ static int run_each(int d, const tbls_set* sets, size_t lo, size_t hi, uint8_t* 
 #define TB_EACH_CHUNK 65536u  // sets per device pass (bounds staging and workspace)
 
 extern "C" int tbls_verify_each(const tbls_set* sets, size_t n, int n_gpus, int* ok_per_set) {
+  const caller_device keep;
   if (ensure_init()) return TBLS_DEVICE_ERROR;
   if (n == 0) return TBLS_SUCCESS;
   int G = (int)g_ctx.size();
@@ -1148,6 +1161,7 @@ extern "C" int tbls_fast_aggregate_verify_many(const tbls_set* sets, size_t n, i
 
 extern "C" int tbls_aggregate_verify(const uint8_t* pks, const uint8_t* const* msgs, const uint32_t* msg_lens, size_t n, const uint8_t sig[96],
                                      int* ok) {
+  const caller_device keep;
   *ok = 0;
   if (ensure_init()) return TBLS_DEVICE_ERROR;
   if (n == 0) return TBLS_SUCCESS;
@@ -1351,6 +1365,7 @@ extern "C" int tbls_dev_batch_partial(int device, const tbls_dev_batch* b, void*
   dev_ctx* c = ctx_for(device);
   if (!c) return TBLS_DEVICE_ERROR;
   std::lock_guard<std::mutex> lk(c->mu);
+  const caller_device keep;
   HIPCHK(hipSetDevice(c->dev));
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
   if (!c->dstb.p) {
@@ -1366,6 +1381,7 @@ extern "C" int tbls_dev_batch_partial_idx(int device, const tbls_dev_batch* b, c
   dev_ctx* c = ctx_for(device);
   if (!c) return TBLS_DEVICE_ERROR;
   std::lock_guard<std::mutex> lk(c->mu);
+  const caller_device keep;
   if (!c->tab_n || !key_idx) return TBLS_BAD_ARGUMENT;
   HIPCHK(hipSetDevice(c->dev));
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
@@ -1382,6 +1398,7 @@ static int partial_timed(int device, const tbls_dev_batch* b, void* stream, void
   dev_ctx* c = ctx_for(device);
   if (!c) return TBLS_DEVICE_ERROR;
   std::lock_guard<std::mutex> lk(c->mu);
+  const caller_device keep;
   HIPCHK(hipSetDevice(c->dev));
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
   if (!c->dstb.p) {
@@ -1451,18 +1468,13 @@ extern "C" int tbls_sign_many(const uint8_t* sks, const uint8_t* msgs, const uin
 
 // Asynchronous final verification (pipelined services): the product of the
 // records and the final exponentiation queued on `s`, the verdict written to
-// device memory; its own workspace (fin_async), no host synchronization.
-int launch_final_async(dev_ctx& c, const void* recs, uint32_t g, hipStream_t s, int* ok_dev) {
-  const size_t need = align_up((size_t)g * sizeof(fp12)) + align_up(sizeof(fp12)) + 256;
-  if (need > c.fin_async.cap) {  // growing frees the old buffer: drain its users first
-    HIPCHK(hipStreamSynchronize(s));
-    if (c.fin_async.ensure(need)) return TBLS_DEVICE_ERROR;
-  }
-  uint8_t* w = c.fin_async.as<uint8_t>();
-  fp12* f = (fp12*)w;
-  uint32_t* nbad = (uint32_t*)(w + align_up((size_t)g * sizeof(fp12)) + align_up(sizeof(fp12)));
-  hipLaunchKernelGGL(k_gather_partials, dim3(1), dim3(64), 0, s, (const uint8_t*)recs, g, f, nbad);
-  hipLaunchKernelGGL(k_final_verify_wave, dim3(1), dim3(64), 0, s, (const fp12*)f, g, (const uint32_t*)nbad, ok_dev);
+// device memory.  k_final_verify_recs reads the records in place and writes
+// only *ok_dev, so the call owns no device scratch: any number of calls may be
+// in flight on any streams (round 2 kept the records' Fp12 copies and the
+// invalid count in one per-device scratch buffer that two finals on different
+// streams overwrote -- see DESIGN.md, "Asynchronous final verification").
+int launch_final_async(const void* recs, uint32_t g, hipStream_t s, int* ok_dev) {
+  hipLaunchKernelGGL(k_final_verify_recs, dim3(1), dim3(64), 0, s, (const uint8_t*)recs, g, ok_dev);
   HIPCHK(hipGetLastError());
   return TBLS_SUCCESS;
 }
@@ -1472,9 +1484,9 @@ extern "C" int tbls_dev_final_verify_async(int device, const void* partials, uin
   if (ensure_init()) return TBLS_DEVICE_ERROR;
   dev_ctx* c = ctx_for(device);
   if (!c) return TBLS_DEVICE_ERROR;
-  std::lock_guard<std::mutex> lk(c->mu);
-  HIPCHK(hipSetDevice(c->dev));
-  return launch_final_async(*c, partials, g, stream ? (hipStream_t)stream : c->stream, ok_dev);
+  const caller_device keep;
+  HIPCHK(hipSetDevice(c->dev));  // no device state is touched: no lock needed
+  return launch_final_async(partials, g, stream ? (hipStream_t)stream : c->stream, ok_dev);
 }
 
 extern "C" int tbls_dev_final_verify(int device, const void* partials, uint32_t g, void* stream, int* ok) {
@@ -1482,6 +1494,7 @@ extern "C" int tbls_dev_final_verify(int device, const void* partials, uint32_t 
   dev_ctx* c = ctx_for(device);
   if (!c) return TBLS_DEVICE_ERROR;
   std::lock_guard<std::mutex> lk(c->mu);
+  const caller_device keep;
   HIPCHK(hipSetDevice(c->dev));
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
   return launch_final(*c, partials, g, s, ok);

@@ -161,6 +161,61 @@ def test_simulated_shards_equal_single_device(hip, sets8):
     assert oks.tolist() == [1, 0]
 
 
+def test_async_final_pipelined_two_streams(hip):
+    """The shape that rejected a valid batch in round 2 (bench_r02ab): batch k's
+    tbls_dev_final_verify_async on stream B runs beside batch k+1's
+    tbls_dev_batch_partial on stream A, with double-buffered records; valid
+    and tampered batches alternate.  Also two finals on two streams at once
+    (the library keeps no scratch for them).  Verdicts must alternate 1, 0."""
+    import torch
+
+    from teku_amd import synth
+
+    bls, native, L, _ = hip
+    dev = torch.device("cuda", 0)
+    n = 96
+    pks, msgs, sigs = synth.single_signer(3000, n, seed=31)
+    bad_sigs = bytearray(sigs)
+    bad_sigs[96 * 40 : 96 * 41] = sigs[96 * 41 : 96 * 42]  # set 40 carries set 41's signature
+    u8 = lambda b: torch.frombuffer(bytearray(b), dtype=torch.uint8).to(dev)  # noqa: E731
+
+    def batch(sg):
+        t = dict(pks=u8(pks), msgs=u8(msgs), sigs=u8(sg), pk_off=torch.arange(0, n + 1, dtype=torch.int32, device=dev),
+                 msg_off=torch.arange(0, 32 * (n + 1), 32, dtype=torch.int32, device=dev),
+                 rand=torch.randint(1, 1 << 62, (n,), dtype=torch.int64, device=dev))
+        t["desc"] = native.TblsDevBatch(t["pks"].data_ptr(), t["pk_off"].data_ptr(), n, t["msgs"].data_ptr(), t["msg_off"].data_ptr(),
+                                        t["sigs"].data_ptr(), t["rand"].data_ptr(), n)
+        return t
+
+    batches = [batch(sigs), batch(bytes(bad_sigs))]
+    K = 8
+    sa, sb = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    recs = [torch.empty(native.PARTIAL_BYTES, dtype=torch.uint8, device=dev) for _ in range(2)]
+    oks = torch.full((K,), 7, dtype=torch.int32, device=dev)
+    done = [torch.cuda.Event() for _ in range(K)]
+    torch.cuda.synchronize()
+    for k in range(K):
+        slot = k % 2
+        if k >= 2:  # the record slot is free once batch k-2's final has run
+            sa.wait_event(done[k - 2])
+        native.check(L.tbls_dev_batch_partial(0, ctypes.byref(batches[k % 2]["desc"]), sa.cuda_stream, recs[slot].data_ptr()), "partial")
+        ready = torch.cuda.Event()
+        ready.record(sa)
+        sb.wait_event(ready)
+        native.check(L.tbls_dev_final_verify_async(0, recs[slot].data_ptr(), 1, sb.cuda_stream, oks[k : k + 1].data_ptr()), "final_async")
+        done[k].record(sb)
+    torch.cuda.synchronize()
+    assert oks.tolist() == [1, 0] * (K // 2)
+    # two finals at once on two streams, over the two (now stable) records
+    oks2 = torch.full((2,), 7, dtype=torch.int32, device=dev)
+    s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    for _ in range(3):
+        native.check(L.tbls_dev_final_verify_async(0, recs[0].data_ptr(), 1, s1.cuda_stream, oks2[0:1].data_ptr()), "final_async")
+        native.check(L.tbls_dev_final_verify_async(0, recs[1].data_ptr(), 1, s2.cuda_stream, oks2[1:2].data_ptr()), "final_async")
+    torch.cuda.synchronize()
+    assert oks2.tolist() == [1, 0]
+
+
 def test_hash_sign_keys_bit_exact(hip):
     bls, native, L, _ = hip
     for msg, dst in [(b"", O.ETH2_DST), (b"abc", O.ETH2_DST), (b"\x42" * 32, O.ETH2_DST), (b"abc", NUL_DST), (bytes(range(200)), O.ETH2_DST)]:

@@ -18,6 +18,7 @@ Inputs are the synthetic sets of SURVEY.md 8(d) (teku_amd/synth.py: interop keys
 sha256 messages, GPU-signed); the oracle verifies the same bytes.
 """
 
+import ctypes
 import os
 
 import pytest
@@ -125,6 +126,82 @@ def test_config4_16k_through_service(S):
     assert got == exp
     assert [i for i, v in enumerate(got) if not v] == sorted(bad)
     assert svc.device_passes == 2
+
+
+N5, SHARD5 = 1048576, 131072  # config 5: 8 GPUs x 131,072 sets
+
+
+@pytest.fixture(scope="module")
+def cfg5(S):
+    """Config 5 at its stated size: 1,048,576 single-signer sets (keys cyclic
+    over the first 65,536 interop keys, distinct messages)."""
+    return S.single_signer(0, N5, seed=5)
+
+
+def _dev_partial(native, L, torch, dev, stream, pks, msgs, sigs, rands):
+    n = len(sigs) // 96
+    u8 = lambda b: torch.frombuffer(bytearray(b), dtype=torch.uint8).to(dev)  # noqa: E731
+    t = dict(pks=u8(pks), msgs=u8(msgs), sigs=u8(sigs), pk_off=torch.arange(0, n + 1, dtype=torch.int32, device=dev),
+             msg_off=torch.arange(0, 32 * (n + 1), 32, dtype=torch.int32, device=dev),
+             rand=torch.tensor([x - (1 << 64) if x >= (1 << 63) else x for x in rands], dtype=torch.int64, device=dev))
+    d = native.TblsDevBatch(t["pks"].data_ptr(), t["pk_off"].data_ptr(), n, t["msgs"].data_ptr(), t["msg_off"].data_ptr(), t["sigs"].data_ptr(),
+                            t["rand"].data_ptr(), n)
+    out = torch.empty(native.PARTIAL_BYTES, dtype=torch.uint8, device=dev)
+    native.check(L.tbls_dev_batch_partial(0, ctypes.byref(d), stream, out.data_ptr()), "partial")
+    torch.cuda.synchronize()
+    return out
+
+
+def test_config5_1m_as_8_simulated_shards(S, cfg5):
+    """SURVEY.md 8(e) at config 5's stated size on one GPU: 8 shards of
+    131,072 sets -> 8 partial records -> one gathered final exponentiation
+    (tbls_dev_final_verify with g = 8), valid, then with one tampered set in
+    shard 0 and in shard 7 (the oracle decides each tampered set alone)."""
+    import torch
+
+    from teku_amd import native
+
+    L = native.lib()
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    pks, msgs, sigs = cfg5
+    rands = S.random_multipliers(N5)
+
+    def shard(g, sg=None):
+        lo, hi = g * SHARD5, (g + 1) * SHARD5
+        return _dev_partial(native, L, torch, dev, stream, pks[48 * lo : 48 * hi], msgs[32 * lo : 32 * hi],
+                            (sg if sg is not None else sigs)[96 * lo : 96 * hi], rands[lo:hi])
+
+    recs = [shard(g) for g in range(8)]
+
+    def final(rs):
+        ok = ctypes.c_int(7)
+        allr = torch.cat(rs)
+        native.check(L.tbls_dev_final_verify(0, allr.data_ptr(), len(rs), stream, ctypes.byref(ok)), "final")
+        return ok.value
+
+    assert final(recs) == 1
+    for g, j in ((0, 17), (7, 7 * SHARD5 + 100000)):
+        bad = bytearray(sigs)
+        bad[96 * j : 96 * j + 96] = sigs[96 * (j + 1) : 96 * (j + 2)]  # set j carries set j+1's signature
+        assert C.verify_each([[pks[48 * j : 48 * j + 48]]], [msgs[32 * j : 32 * j + 32]], [bytes(bad[96 * j : 96 * j + 96])])[0] is False
+        rs = list(recs)
+        rs[g] = shard(g, bytes(bad))
+        assert final(rs) == 0, (g, j)
+    assert final(recs) == 1  # the untouched records still verify
+
+
+def test_config5_1m_one_device_batch(S, cfg5):
+    """One tbls_batch_verify of all 1,048,576 sets on one device (offsets, the
+    bucket MSM and the chunked line buffers at 1M), valid and one tampered."""
+    pks, msgs, sigs = cfg5
+    r = S.random_multipliers(N5)
+    assert S.SetArray.single(pks, msgs, sigs).batch_verify(r, n_gpus=1) is True
+    j = N5 - 5
+    bad = bytearray(sigs)
+    bad[96 * j : 96 * j + 96] = bytes(96)  # the all-zero signature (BlstSignatureTest.java:54-57)
+    assert C.verify_each([[pks[48 * j : 48 * j + 48]]], [msgs[32 * j : 32 * j + 32]], [bytes(96)])[0] is False
+    assert S.SetArray.single(pks, msgs, bytes(bad)).batch_verify(r, n_gpus=1) is False
 
 
 def test_config5_131k_shard(S):

@@ -7,11 +7,11 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 SETS=${SETS:-131072}
-PARGS="--steps 1 --warmup 0 --sets-per-gpu $SETS --lat-reps 0 --no-cpu-baseline"
+PARGS="--steps 1 --warmup 0 --sets-per-gpu $SETS --lat-reps 0 --no-cpu-baseline --no-1m"
 echo "== pytest -m gpu" && timeout -k 10 900 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; rc=$?; tail -4 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
 echo "== bench" && timeout -k 10 600 python bench.py --sets-per-gpu $SETS > gpurun_out/bench.json 2> gpurun_out/bench.err; rc=$?; cat gpurun_out/bench.json; tail -3 gpurun_out/bench.err; [ $rc -eq 0 ] || exit $rc
 [ -n "$NOPROF" ] && exit 0
-echo "== kernel trace" && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --sets-per-gpu $SETS --lat-reps 0 --no-cpu-baseline > gpurun_out/prof.log 2>&1 || exit $?
+echo "== kernel trace" && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --sets-per-gpu $SETS --lat-reps 0 --no-cpu-baseline --no-1m > gpurun_out/prof.log 2>&1 || exit $?
 tail -1 gpurun_out/prof.log
 echo "== pmc FETCH_SIZE" && timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 bench.py $PARGS > gpurun_out/pmc_fetch.log 2>&1 || exit $?
 echo "== pmc WRITE_SIZE" && timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python3 bench.py $PARGS > gpurun_out/pmc_write.log 2>&1 || exit $?
