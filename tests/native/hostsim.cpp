@@ -50,3 +50,40 @@ extern "C" unsigned long long tbls_hostsim_fp2mul_count(int reset) {
   return 0;
 #endif
 }
+
+// ---- lane-cooperative Fp (tb_coop.h), host emulation of one 16-lane row ----
+#include "../../teku_amd/csrc/tb_coop.h"
+
+// n products of digit vectors (16 int32 each: digit j of lane j)
+extern "C" int tbls_hostsim_coop_mul_digits(const int32_t* a, const int32_t* b, int32_t* out, size_t n) {
+  for (size_t k = 0; k < n; k++) {
+    tb::coop::c32 x, y;
+    for (int j = 0; j < 16; j++) {
+      x.v[j] = a[16 * k + j];
+      y.v[j] = b[16 * k + j];
+    }
+    const tb::coop::c32 r = tb::coop::cmul(x, y);
+    for (int j = 0; j < 16; j++) out[16 * k + j] = r.v[j];
+  }
+  return 0;
+}
+
+// 12-word [0, 2p) operands -> digits (cfrom_words) -> cmul -> cdigits_to_fp
+extern "C" int tbls_hostsim_coop_mul_fp(const uint32_t* a, const uint32_t* b, uint32_t* out, size_t n) {
+  for (size_t k = 0; k < n; k++) {
+    const tb::coop::c32 x = tb::coop::cfrom_words(a + 12 * k), y = tb::coop::cfrom_words(b + 12 * k);
+    const tb::coop::c32 r = tb::coop::cmul(x, y);
+    const tb::fp f = tb::coop::cdigits_to_fp(r.v);
+    for (int j = 0; j < 12; j++) out[12 * k + j] = f.l[j];
+  }
+  return 0;
+}
+
+// digits -> [0, 2p) (cdigits_to_fp), for checking conversions
+extern "C" int tbls_hostsim_coop_to_fp(const int32_t* d, uint32_t* out, size_t n) {
+  for (size_t k = 0; k < n; k++) {
+    const tb::fp f = tb::coop::cdigits_to_fp(d + 16 * k);
+    for (int j = 0; j < 12; j++) out[12 * k + j] = f.l[j];
+  }
+  return 0;
+}

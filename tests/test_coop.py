@@ -1,0 +1,125 @@
+"""Lane-cooperative Fp products (teku_amd/csrc/tb_coop.h) on the host emulation
+of a 16-lane row, checked against Python integers.
+
+The digit-class bounds of the file comment are exercised with worst-case
+digits (every digit at its class bound, both signs), the conversions from and
+to the 12 x 32-bit [0, 2p) form with edge values, and a chain of products fed
+back as operands (what the serial exponentiations do).  Test infrastructure
+only: the product path runs the same source on the GPU (tests/test_gpu_ops.py).
+"""
+
+import ctypes
+import random
+
+import numpy as np
+import pytest
+
+from oracle import bls12_381 as O
+
+P = O.P
+R = 1 << 406
+RINV = pow(R, -1, P)
+
+
+@pytest.fixture(scope="module")
+def lib():
+    import __graft_entry__ as ge
+
+    L = ctypes.CDLL(ge.build_hostsim())
+    for name in ("tbls_hostsim_coop_mul_digits", "tbls_hostsim_coop_mul_fp"):
+        getattr(L, name).argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
+    L.tbls_hostsim_coop_to_fp.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
+    return L
+
+
+def val(d):
+    return sum(int(x) << (29 * j) for j, x in enumerate(d[:14]))
+
+
+def mul_digits(L, A, B):
+    a = np.ascontiguousarray(np.array(A, dtype=np.int32))
+    b = np.ascontiguousarray(np.array(B, dtype=np.int32))
+    out = np.zeros_like(a)
+    L.tbls_hostsim_coop_mul_digits(a.ctypes.data, b.ctypes.data, out.ctypes.data, len(A))
+    return out
+
+
+def rnd_digits(rng, T, top=31, worst=False):
+    """14 digits of class T (|d| <= T 2^28), lanes 14, 15 zero."""
+    lim = T << 28
+    if worst:
+        d = [rng.choice((-lim, lim - 1)) for _ in range(13)]
+    else:
+        d = [rng.randint(-lim, lim - 1) for _ in range(13)]
+    return d + [rng.randint(-top, top), 0, 0]
+
+
+def check(L, A, B):
+    out = mul_digits(L, A, B)
+    for a, b, r in zip(A, B, out):
+        assert r[14] == 0 and r[15] == 0
+        assert all(abs(int(x)) <= (1 << 28) + 8 for x in r[:13]), "output digit class"
+        assert abs(int(r[13])) < 32, "output top digit"
+        v = val(r)
+        assert abs(v) < P + P // 100
+        assert (v - val(a) * val(b) * RINV) % P == 0
+    return out
+
+
+@pytest.mark.parametrize("ta,tb", [(1, 1), (1, 7), (7, 1), (2, 3), (3, 2), (1, 2), (2, 2)])
+def test_coop_mul_classes(lib, ta, tb):
+    rng = random.Random(1000 * ta + tb)
+    for worst in (False, True):
+        A = [rnd_digits(rng, ta, worst=worst) for _ in range(300)]
+        B = [rnd_digits(rng, tb, worst=worst) for _ in range(300)]
+        check(lib, A, B)
+
+
+def test_coop_mul_chain(lib):
+    """Outputs fed back as operands, and sums of up to 7 outputs times an output."""
+    rng = random.Random(7)
+    x = [rnd_digits(rng, 1) for _ in range(64)]
+    y = [rnd_digits(rng, 1) for _ in range(64)]
+    for _ in range(30):
+        z = check(lib, x, y)
+        x, y = y, [list(map(int, r)) for r in z]
+    s = [[sum(int(r[j]) for r in (x[i], y[i], x[i], y[i], x[i], y[i], x[i])) for j in range(16)] for i in range(64)]
+    check(lib, s, y)
+
+
+def test_coop_fp_roundtrip(lib):
+    """[0, 2p) 12-word operands through cfrom_words / cmul / cdigits_to_fp equal
+    fp_mul's residue, with the result back in [0, 2p)."""
+    rng = random.Random(3)
+    vals = [0, 1, P - 1, P, P + 1, 2 * P - 1] + [rng.randrange(2 * P) for _ in range(200)]
+    A = vals
+    B = list(reversed(vals))
+    w = lambda v: np.array([(v >> (32 * i)) & 0xFFFFFFFF for i in range(12)], dtype=np.uint32)  # noqa: E731
+    a = np.ascontiguousarray(np.stack([w(v) for v in A]))
+    b = np.ascontiguousarray(np.stack([w(v) for v in B]))
+    out = np.zeros_like(a)
+    lib.tbls_hostsim_coop_mul_fp(a.ctypes.data, b.ctypes.data, out.ctypes.data, len(A))
+    for x, y, r in zip(A, B, out):
+        v = sum(int(r[i]) << (32 * i) for i in range(12))
+        assert v < 2 * P
+        assert v % P == x * y * RINV % P
+
+
+def test_coop_to_fp_signed(lib):
+    """cdigits_to_fp on signed digit vectors of |value| < 64p."""
+    rng = random.Random(4)
+    D = []
+    for _ in range(300):
+        v = rng.choice([rng.randrange(-64 * P + 1, 64 * P), rng.randrange(-P, P), -64 * P + 1, 64 * P - 1])
+        d = []
+        for _ in range(13):
+            lo = ((v + (1 << 28)) & ((1 << 29) - 1)) - (1 << 28)
+            d.append(lo)
+            v = (v - lo) >> 29
+        D.append(d + [v, 0, 0])
+    d = np.ascontiguousarray(np.array(D, dtype=np.int32))
+    out = np.zeros((len(D), 12), dtype=np.uint32)
+    lib.tbls_hostsim_coop_to_fp(d.ctypes.data, out.ctypes.data, len(D))
+    for dd, r in zip(D, out):
+        v = sum(int(r[i]) << (32 * i) for i in range(12))
+        assert v < 2 * P and v % P == val(dd) % P

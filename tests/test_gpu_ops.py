@@ -123,6 +123,10 @@ def test_pairing_pieces(run):
     single = [dec_fp12(x) for x in run("FINAL_EXP", [enc_fp12(x) for x in fs])]
     wave = [dec_fp12(x) for x in run("FINAL_EXP_WAVE", [enc_fp12(x) for x in fs])]
     assert wave == single
+    # lane-cooperative final exponentiation (tb_cfe.h) == the same, bit for bit
+    out = run("FINAL_EXP_COOP", [enc_fp12(x) for x in fs])
+    assert [dec_fp12(x) for x in out] == single
+    print("\ncoop final exponentiation: %d cycles" % int.from_bytes(out[0][576:584], "little"))
 
 
 def test_miller2_shared_accumulator(run):
@@ -190,3 +194,46 @@ def test_clear_cofactor_prog(run):
 def test_fp_bounds_of_weak_reduction(run):
     """The same bound checks on the GPU build (tests/opcodec.check_raw_ops)."""
     check_raw_ops(run, random.Random(12))
+
+
+def test_coop_mul_and_timing(run):
+    """Lane-cooperative products (tb_coop.h) on the GPU: one product per 16-lane
+    row equals the oracle's a*b; a 64-long chain of products equals a b^64; the
+    clock64 cycles of the chains (one and two interleaved per row) against the
+    lone-lane fp_mul chain are printed (tools/hash_parts.py reads them too)."""
+    rng = _rng()
+    A = [rng.randrange(O.P) for _ in range(61)] + [0, 1, O.P - 1]
+    B = [rng.randrange(O.P) for _ in range(61)] + [O.P - 1, O.P - 1, 2]
+    out = run("COOP_MUL", [enc_fp(a) + enc_fp(b) for a, b in zip(A, B)])
+    assert [dec_fp(x) for x in out] == [a * b % O.P for a, b in zip(A, B)]
+    a, b = 0x1234567 * 0x9ABCDEF0123, O.P - 12345
+    o = run("COOP_TIMING", [enc_fp(a) + enc_fp(b)])[0]
+    cyc = [int.from_bytes(o[8 * i : 8 * i + 8], "little") / 64 for i in range(3)]
+    print("\ncoop cycles per product: chain %.0f, two interleaved chains %.0f per step; lone-lane fp_mul %.0f" % tuple(cyc))
+    assert int.from_bytes(o[64:112], "big") == a * pow(b, 64, O.P) % O.P
+    assert int.from_bytes(o[112:160], "big") == b * pow(a, 64, O.P) % O.P
+    assert int.from_bytes(o[160:208], "big") == a * pow(b, 64, O.P) % O.P
+
+
+def test_cfe_ops(run):
+    """Single lane-cooperative Fp12 ops (tb_cfe.h) vs the oracle: product,
+    cyclotomic squaring (on f^((p^6-1)(p^2+1))), Frobenius, conjugation."""
+    rng = _rng()
+    rf12 = lambda: tuple(tuple((rng.randrange(O.P), rng.randrange(O.P)) for _ in range(3)) for _ in range(2))  # noqa: E731
+    f, g = rf12(), rf12()
+    c = O.f12_pow(f, (O.P ** 6 - 1) * (O.P ** 2 + 1))
+    op = lambda k: k.to_bytes(4, "little")  # noqa: E731
+    recs = [enc_fp12(f) + enc_fp12(g) + op(0), enc_fp12(c) + enc_fp12(g) + op(1), enc_fp12(f) + enc_fp12(g) + op(2),
+            enc_fp12(f) + enc_fp12(g) + op(3), enc_fp12(f) + enc_fp12(g) + op(4)]
+    got = [dec_fp12(x) for x in run("CFE_OPS", recs)]
+    exp = [O.f12_mul(f, g), O.f12_mul(c, c), O.f12_pow(f, O.P), O.f12_conj(f) if hasattr(O, "f12_conj") else None, f]
+    names = ["mul", "cyc_sqr", "frob", "conj", "copy"]
+    bad = [n for n, a, b in zip(names, got, exp) if b is not None and a != b]
+    X = -0xD201000000010000
+    t = O.f12_pow(f, (O.P ** 6 - 1) * (O.P ** 2 + 1))
+    recs = [enc_fp12(f) + enc_fp12(g) + op(5), enc_fp12(c) + enc_fp12(g) + op(6), enc_fp12(f) + enc_fp12(g) + op(7)]
+    got = [dec_fp12(x) for x in run("CFE_OPS", recs)]
+    e = O.final_exponentiation(f)
+    exp = [t, O.f12_conj(O.f12_pow(c, -X)), O.f12_mul(O.f12_mul(e, e), e)]  # the device chain computes the 3 x hard part
+    bad += [n for n, a, b in zip(["easy", "exp_x", "final"], got, exp) if a != b]
+    assert not bad, bad
