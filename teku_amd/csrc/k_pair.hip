@@ -1,5 +1,6 @@
 // Pairings: the Fp12 product of the Miller values and the final exponentiation.
 #include "tb_kdecl.h"
+#include "tb_cfe.h"
 
 using namespace tb;
 
@@ -81,6 +82,39 @@ extern "C" __global__ void __launch_bounds__(64) k_final_verify_recs(const uint8
     for (uint32_t i = 0; i < g; i++) bad += *reinterpret_cast<const uint32_t*>(recs + (size_t)i * TB_PARTIAL_BYTES + sizeof(fp12));
     result[0] = (bad == 0 && fp12_is_one(fp12_from_coords(L.F))) ? 1 : 0;
   }
+}
+
+// The lane-cooperative final exponentiation (tb_cfe.h): one 256-thread
+// workgroup, 16 rows of 16 lanes; the product of the g records first.  Same
+// verdict as k_final_verify_recs (tests/test_gpu_bls.py, test_gpu_ops.py).
+__device__ TB_INLINE void final_verify_coop(const uint8_t* recs, size_t stride, uint32_t g, uint32_t bad_in, bool count_bad,
+                                            int* result) {
+  __shared__ cfe_lds L;
+  tb_latency_prio();
+  cfe::init(L);
+  cfe::load_coords(L.F, reinterpret_cast<const fp*>(recs));
+  for (uint32_t i = 1; i < g; i++) {
+    cfe::load_coords(L.X, reinterpret_cast<const fp*>(recs + (size_t)i * stride));
+    cfe::mul(L.F, L.F, L.X, L);
+  }
+  const bool one = cfe::final_exp_is_one(L);
+  if (threadIdx.x == 0) {
+    uint32_t bad = bad_in;
+    if (count_bad)
+      for (uint32_t i = 0; i < g; i++) bad += *reinterpret_cast<const uint32_t*>(recs + (size_t)i * stride + sizeof(fp12));
+    result[0] = (bad == 0 && one) ? 1 : 0;
+  }
+}
+
+extern "C" __global__ void __launch_bounds__(CFE_THREADS) k_final_verify_recs_coop(const uint8_t* __restrict__ recs, uint32_t g,
+                                                                                 int* __restrict__ result) {
+  final_verify_coop(recs, TB_PARTIAL_BYTES, g, 0u, true, result);
+}
+
+// on g contiguous Fp12 values (the KZG pairing check's two Miller values)
+extern "C" __global__ void __launch_bounds__(CFE_THREADS) k_final_verify_coop(const fp12* __restrict__ f, uint32_t g,
+                                                                            const uint32_t* __restrict__ n_bad, int* __restrict__ result) {
+  final_verify_coop(reinterpret_cast<const uint8_t*>(f), sizeof(fp12), g, n_bad[0], false, result);
 }
 
 // single-lane reference version (kept for A/B timing)

@@ -26,12 +26,24 @@ namespace tb {
 
 typedef int32_t cdig[16];  // one coop element in LDS: digit d at [d]
 
+// A bilinear op's tables re-laid for branch-free digit sums: every product
+// slot (16 rows x K) and every output coordinate gets exactly MAXLEN entries,
+// each a packed (coefficient << 16 | source index) word with coefficient
+// +1 / -1, padding 0 (index 0): a term is one LDS load and one
+// multiply-add, no branches, no selects.
+template <int K, int AMAX, int BMAX, int PMAX, int LMAX>
+struct cfe_ptab {
+  int32_t a[16 * K][AMAX], b[16 * K][BMAX], post[12][PMAX], lin[12][LMAX > 0 ? LMAX : 1];
+};
+#define CFE_PTAB(P) cfe_ptab<(P##_NPROD + 15) / 16, P##_A_MAXLEN, P##_B_MAXLEN, P##_POST_MAXLEN, P##_LIN_MAXLEN>
+
 struct cfe_lds {
   cdig F[12], T[12], A[12], B[12], C[12], E[12], X[12], Y[12];
   cdig prod[64];
   cdig gam[5][3];  // Frobenius constants gamma_wp: g0, g1, g0 + g1 (wp = 1..5)
   fp tmp[12];      // 12 x 32-bit staging (conversions, the inversion)
-  uint16_t tab[W12_ALL_N];
+  CFE_PTAB(W12M) tm;
+  CFE_PTAB(W12C) tc;
   int flag;
 };
 
@@ -42,45 +54,52 @@ using coop::c64;
 __device__ TB_INLINE int row() { return (int)(threadIdx.x >> 4); }
 __device__ TB_INLINE int dig() { return (int)(threadIdx.x & 15u); }
 
-// one carry step from a 64-bit digit sum (|sum| < 2^38 per digit)
-__device__ TB_INLINE c32 cnorm64(c64 x) {
-  const c32 l = coop::sel_lt(13, coop::bal_lo(x), (c32)x);
-  const c32 c = coop::keep_lt(13, (c32)((x - (c64)l) >> 29));
-  return l + coop::shr<1>(c);
-}
+using coop::cnorm64;
+using coop::creduce64;
 
-// sum of table entries [b, e) of +-src[idx][d] (entry = idx << 1 | neg)
+// sum over a padded entry row of coef * src[idx][d]: all loads issued up
+// front, one multiply-add per term
 template <int MAXLEN>
-__device__ TB_INLINE c64 tsum(const cdig* src, const uint16_t* ent, int b, int e) {
+__device__ TB_INLINE c64 tsum(const cdig* src, const int32_t* ent) {
   const int d = dig();
+  int32_t e[MAXLEN], v[MAXLEN];
+  TB_UNROLL for (int t = 0; t < MAXLEN; t++) e[t] = ent[t];
+  TB_UNROLL for (int t = 0; t < MAXLEN; t++) v[t] = src[e[t] & 0xffff][d];
   c64 acc = 0;
-  TB_UNROLL for (int t = 0; t < MAXLEN; t++) {
-    if (b + t < e) {
-      const uint32_t x = ent[b + t];
-      const c64 v = src[x >> 1][d];
-      acc += (x & 1u) ? -v : v;
-    }
-  }
+  TB_UNROLL for (int t = 0; t < MAXLEN; t++) acc += coop::mulw(v[t], e[t] >> 16);
   return acc;
 }
+__device__ TB_INLINE int32_t pent(uint32_t x) { return (int32_t)((x >> 1) | ((x & 1u) ? 0xffff0000u : 0x00010000u)); }
 
+// re-lay one op's W12 tables (tb_fp12_wave_tables.h offsets) into PT
 template <int NPROD, int AOFF, int AENT, int AMAX, int BOFF, int BENT, int BMAX, int POFF, int PENT, int PMAX, int LOFF,
-          int LENT, int LMAX>
-__device__ TB_INLINE void bilinear(cdig* dst, const cdig* x, const cdig* y, cfe_lds& L) {
+          int LENT, int LMAX, typename PTAB>
+__device__ TB_INLINE void ptab_build(PTAB& pt) {
+  constexpr int K = (NPROD + 15) / 16;
+  for (int t = threadIdx.x; t < 16 * K; t += blockDim.x) {
+    const int ab = t < NPROD ? W12_ALL[AOFF + t] : 0, ae = t < NPROD ? W12_ALL[AOFF + t + 1] : 0;
+    const int bb = t < NPROD ? W12_ALL[BOFF + t] : 0, be = t < NPROD ? W12_ALL[BOFF + t + 1] : 0;
+    for (int j = 0; j < AMAX; j++) pt.a[t][j] = ab + j < ae ? pent(W12_ALL[AENT + ab + j]) : 0;
+    for (int j = 0; j < BMAX; j++) pt.b[t][j] = bb + j < be ? pent(W12_ALL[BENT + bb + j]) : 0;
+  }
+  for (int g = threadIdx.x; g < 12; g += blockDim.x) {
+    const int pb = W12_ALL[POFF + g], pe = W12_ALL[POFF + g + 1];
+    for (int j = 0; j < PMAX; j++) pt.post[g][j] = pb + j < pe ? pent(W12_ALL[PENT + pb + j]) : 0;
+    const int lb = W12_ALL[LOFF + g], le = W12_ALL[LOFF + g + 1];
+    for (int j = 0; j < (LMAX > 0 ? LMAX : 1); j++) pt.lin[g][j] = lb + j < le ? pent(W12_ALL[LENT + lb + j]) : 0;
+  }
+}
+
+template <int NPROD, int AMAX, int BMAX, int PMAX, int LMAX, typename PTAB>
+__device__ TB_INLINE void bilinear(cdig* dst, const cdig* x, const cdig* y, const PTAB& pt, cfe_lds& L) {
   constexpr int K = (NPROD + CFE_ROWS - 1) / CFE_ROWS;
   static_assert(AMAX <= 8 && BMAX <= 8, "operand sums: class <= 8 before the carry step");
   const int g = row(), d = dig();
-  const uint16_t* T = L.tab;
   c32 pa[K], pb[K], pr[K];
   TB_UNROLL for (int k = 0; k < K; k++) {
     const int t = g + CFE_ROWS * k;
-    c64 sa = 0, sb = 0;
-    if (t < NPROD) {  // uniform per row
-      sa = tsum<AMAX>(x, T + AENT, T[AOFF + t], T[AOFF + t + 1]);
-      sb = tsum<BMAX>(y, T + BENT, T[BOFF + t], T[BOFF + t + 1]);
-    }
-    pa[k] = cnorm64(sa);
-    pb[k] = cnorm64(sb);
+    pa[k] = cnorm64(tsum<AMAX>(x, pt.a[t]));
+    pb[k] = cnorm64(tsum<BMAX>(y, pt.b[t]));
   }
   TB_UNROLL for (int k = 0; k < K; k++) pr[k] = coop::cmul(pa[k], pb[k]);
   TB_UNROLL for (int k = 0; k < K; k++) {
@@ -90,17 +109,21 @@ __device__ TB_INLINE void bilinear(cdig* dst, const cdig* x, const cdig* y, cfe_
   __syncthreads();
   c32 out = 0;
   if (g < 12) {  // output coordinate g, digit d
-    c64 acc = tsum<PMAX>(L.prod, T + PENT, T[POFF + g], T[POFF + g + 1]);
-    if (LMAX > 0) acc += tsum<LMAX>(x, T + LENT, T[LOFF + g], T[LOFF + g + 1]);
-    out = cnorm64(acc);
+    c64 acc = tsum<PMAX>(L.prod, pt.post[g]);
+    if constexpr (LMAX > 0) acc += tsum<LMAX>(x, pt.lin[g]);
+    out = creduce64(acc);  // |v| < 1.6 p: no growth along the chain
   }
   __syncthreads();
   if (g < 12) dst[g][d] = out;
   __syncthreads();
 }
 
-__device__ TB_INLINE void mul(cdig* dst, const cdig* x, const cdig* y, cfe_lds& L) { bilinear<W12_TABS(W12M)>(dst, x, y, L); }
-__device__ TB_INLINE void cyc_sqr(cdig* dst, const cdig* x, cfe_lds& L) { bilinear<W12_TABS(W12C)>(dst, x, x, L); }
+__device__ TB_INLINE void mul(cdig* dst, const cdig* x, const cdig* y, cfe_lds& L) {
+  bilinear<W12M_NPROD, W12M_A_MAXLEN, W12M_B_MAXLEN, W12M_POST_MAXLEN, W12M_LIN_MAXLEN>(dst, x, y, L.tm, L);
+}
+__device__ TB_INLINE void cyc_sqr(cdig* dst, const cdig* x, cfe_lds& L) {
+  bilinear<W12C_NPROD, W12C_A_MAXLEN, W12C_B_MAXLEN, W12C_POST_MAXLEN, W12C_LIN_MAXLEN>(dst, x, x, L.tc, L);
+}
 
 __device__ TB_INLINE void copy(cdig* dst, const cdig* x) {
   const int g = row(), d = dig();
@@ -145,7 +168,7 @@ __device__ TB_INLINE void frob(cdig* dst, const cdig* x, cfe_lds& L) {
     } else {
       const int b3 = 3 * (j - 1);
       const c32 p0 = L.prod[b3][d], p1 = L.prod[b3 + 1][d], p2 = L.prod[b3 + 2][d];
-      out = cnorm64((g & 1) ? (c64)p2 - (c64)p0 + (c64)p1 : (c64)p0 + (c64)p1);
+      out = creduce64((g & 1) ? (c64)p2 - (c64)p0 + (c64)p1 : (c64)p0 + (c64)p1);
     }
   }
   __syncthreads();
@@ -182,7 +205,8 @@ __device__ TB_INLINE void store_coords(const cdig* src, cfe_lds& L) {
 
 // tables and Frobenius constants into LDS (whole workgroup)
 __device__ TB_INLINE void init(cfe_lds& L) {
-  for (int i = threadIdx.x; i < W12_ALL_N; i += blockDim.x) L.tab[i] = W12_ALL[i];
+  ptab_build<W12_TABS(W12M)>(L.tm);
+  ptab_build<W12_TABS(W12C)>(L.tc);
   const int g = row(), d = dig();
   if (g < 10) {  // gamma_wp, wp = g/2 + 1, coordinate g & 1
     const uint32_t(*G)[12] = nullptr;
@@ -201,16 +225,44 @@ __device__ TB_INLINE void init(cfe_lds& L) {
   __syncthreads();
 }
 
+// dst = x^-1 (x != dst; uses X, Y, A, B, C, E as scratch unless they alias
+// x / dst -- the caller's final_exp passes F and X).  Norms down the tower,
+// every step on the coop levels above, one lone-lane Fp inversion:
+//   N = x conj(x) in Fp6;  u = N^(p^2) N^(p^4);  v = N u in Fp2;
+//   n = v0^2 + v1^2 in Fp;  x^-1 = conj(x) u conj2(v) / n
+__device__ TB_INLINE void inv(cdig* dst, const cdig* x, cfe_lds& L) {
+  const int g = row(), d = dig();
+  conj(L.Y, x);
+  mul(L.A, x, L.Y, L);    // N
+  frob(L.B, L.A, L);
+  frob(L.B, L.B, L);      // N^(p^2)
+  frob(L.C, L.B, L);
+  frob(L.C, L.C, L);      // N^(p^4)
+  mul(L.C, L.B, L.C, L);  // u
+  mul(L.E, L.A, L.C, L);  // v = N u (coordinates 0, 1)
+  // n = v0^2 + v1^2 on rows 0, 1; n^-1 on one lane
+  const c32 vi = g < 2 ? L.E[g][d] : 0;
+  const c32 sq = coop::cmul(vi, vi);
+  if (g < 2) L.prod[g][d] = sq;
+  __syncthreads();
+  if (g == 0) L.prod[2][d] = creduce64((c64)L.prod[0][d] + (c64)L.prod[1][d]);
+  __syncthreads();
+  if (threadIdx.x == 0) L.tmp[0] = fp_inv(coop::cdigits_to_fp(L.prod[2]));
+  __syncthreads();
+  // w = conj2(v) / n: coordinates 0, 1 (rows 0, 1), zero elsewhere
+  const c32 ninv = coop::cfrom_words(L.tmp[0].l);
+  const c32 wv = coop::cmul(vi, ninv);
+  __syncthreads();
+  if (g < 12) L.B[g][d] = g == 0 ? wv : (g == 1 ? -wv : 0);
+  __syncthreads();
+  mul(L.C, L.C, L.B, L);   // u / v = N^-1
+  mul(dst, L.Y, L.C, L);   // conj(x) / N = x^-1
+}
+
 // L.F <- final_exp(L.F) (tb_pairing.h final_exp's chain; whole workgroup)
 __device__ TB_INLINE void final_exp(cfe_lds& L) {
-  // easy part: t = conj(f) / f, the Fp12 inversion on one lane
-  store_coords(L.F, L);
-  if (threadIdx.x == 0) {
-    const fp12 inv = fp12_inv(fp12_from_coords(L.tmp));
-    fp12_to_coords(L.tmp, inv);
-  }
-  __syncthreads();
-  load_coords(L.X, L.tmp);
+  // easy part: t = conj(f) / f
+  inv(L.X, L.F, L);
   conj(L.Y, L.F);
   mul(L.T, L.Y, L.X, L);
   frob(L.X, L.T, L);

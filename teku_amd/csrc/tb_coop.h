@@ -39,6 +39,9 @@
 // arithmetic above is unit-tested on the CPU from this exact source.
 #pragma once
 #include "tb_fp.h"
+#if !defined(__HIPCC__)
+#include <cmath>
+#endif
 
 namespace tb {
 namespace coop {
@@ -225,6 +228,9 @@ inline c32 lane_const(const int32_t* tab) {
 #endif
 
 TB_CONST int32_t H28 = 1 << 28;
+// p's balanced digits per lane (lanes 14, 15: 0) for lane-indexed loads
+TB_CONST int32_t CP_BAL16[16] = {CP_BAL[0], CP_BAL[1], CP_BAL[2],  CP_BAL[3],  CP_BAL[4],  CP_BAL[5],  CP_BAL[6], CP_BAL[7],
+                                 CP_BAL[8], CP_BAL[9], CP_BAL[10], CP_BAL[11], CP_BAL[12], CP_BAL[13], 0,         0};
 
 // balanced low 29 bits of x, in [-2^28, 2^28) (x + 2^28 wraps in 32 bits:
 // only its low 29 bits are kept)
@@ -248,6 +254,37 @@ TBC_FN c32 cnorm(c32 x) {
   const c32 c = keep_lt(13, (x - l) >> 29);
   return l + shr<1>(c);
 }
+
+// One carry step from 64-bit digit sums (|sum| < 2^40 per digit): T = 1
+// digits, the top digit (lane 13) takes the carry unsplit.  Same value.
+TBC_FN c32 cnorm64(c64 x) {
+  const c32 l = sel_lt(13, bal_lo(x), narrow(x));
+  const c32 c = keep_lt(13, narrow((x - wide(l)) >> 29));
+  return l + shr<1>(c);
+}
+
+// Value reduction of a sum of coop values (64-bit digit sums, |v| < 2^395):
+// q = round(v / p) from the top two digits (v ~ d13 2^377 + d12 2^348; the
+// lower digits move v / p by less than 2^-33), v - q p digit-wise, one more
+// carry step.  Result: T = 1 digits, |v| < 1.6 p -- what keeps long chains of
+// lazy sums (the final exponentiation's levels, the wave programs' slots)
+// from growing.
+TB_CONST float CQ_SCALE = 1.43257367e-10f;  // 2^348 / p
+TBC_FN c32 creduce64(c64 x) {
+  const c32 d = cnorm64(x);
+#if defined(__HIPCC__)
+  const float t = (float)d * 536870912.0f + (float)shr<1>(d);  // lane 13: d13 2^29 + d12
+  const c32 q = bcast<13>((int32_t)__builtin_rintf(t * CQ_SCALE));
+  return cnorm64((c64)d - mulw(q, lane_const(CP_BAL16)));
+#else
+  const c32 d12 = shr<1>(d);
+  const int32_t q = (int32_t)std::nearbyint(((float)d.v[13] * 536870912.0f + (float)d12.v[13]) * CQ_SCALE);
+  c64 y;
+  for (int j = 0; j < 16; j++) y.v[j] = (int64_t)d.v[j] - (int64_t)q * CP_BAL16[j];
+  return cnorm64(y);
+#endif
+}
+TBC_FN c32 creduce(c32 x) { return creduce64(wide(x)); }
 
 // Montgomery product a b R^-1 (mod p): the five steps of the file comment.
 TBC_FN c32 cmul(c32 a, c32 b) {
@@ -314,6 +351,39 @@ TBC_FN c32 cmul(c32 a, c32 b) {
 }
 
 TBC_FN c32 csqr(c32 a) { return cmul(a, a); }
+
+// N independent products interleaved (one instruction stream, N chains: the
+// row's latency-bound product issues N x the work in about the same time)
+template <int N>
+TBC_FN void cmul_n(c32 (&r)[N], const c32 (&a)[N], const c32 (&b)[N]) {
+  TB_UNROLL for (int k = 0; k < N; k++) r[k] = cmul(a[k], b[k]);
+}
+
+// a^e for the fixed exponents of tb_fp.h fp_pow_win (sliding window w = 4:
+// sched[k] = squarings << 4 | (table index < 8 ? multiply by a^(2i+1) : none)),
+// for N bases at once (interleaved chains).
+template <int N>
+TBC_FN void cpow_win_n(c32 (&r)[N], const c32 (&a)[N], uint32_t first, const uint16_t* sched, int nstep) {
+  c32 tab[8][N], a2[N];
+  TB_UNROLL for (int k = 0; k < N; k++) tab[0][k] = a[k];
+  cmul_n<N>(a2, a, a);
+  TB_UNROLL for (int i = 1; i < 8; i++) cmul_n<N>(tab[i], tab[i - 1], a2);
+  TB_UNROLL for (int k = 0; k < N; k++) r[k] = tab[0][k];
+  TB_UNROLL for (int i = 1; i < 8; i++)
+    if (first == (uint32_t)i) TB_UNROLL for (int k = 0; k < N; k++) r[k] = tab[i][k];
+  TB_NOUNROLL for (int s = 0; s < nstep; s++) {
+    const uint32_t e = sched[s];
+    TB_NOUNROLL for (uint32_t j = 0; j < (e >> 4); j++) cmul_n<N>(r, r, r);
+    const uint32_t t = e & 15u;
+    if (t < 8u) {
+      c32 m[N];
+      TB_UNROLL for (int k = 0; k < N; k++) m[k] = tab[0][k];
+      TB_UNROLL for (int i = 1; i < 8; i++)
+        if (t == (uint32_t)i) TB_UNROLL for (int k = 0; k < N; k++) m[k] = tab[i][k];
+      cmul_n<N>(r, r, m);
+    }
+  }
+}
 
 // ---------------------------------------------------------------------------
 // Conversions from / to the 12 x 32-bit form (tb_fp.h: [0, 2p), same R)

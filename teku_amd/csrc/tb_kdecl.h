@@ -22,6 +22,7 @@
 // Every thread's work is independent; reductions are two-level (block tree
 // in LDS, then one block over the block partials).
 #pragma once
+#include <cstdlib>
 #include "tb_stages.h"
 #include "tb_fp12_wave.h"
 
@@ -92,3 +93,19 @@ extern "C" __global__ void k_final_verify_wave(const fp12* __restrict__ f, uint3
 extern "C" __global__ void k_final_verify(const fp12* __restrict__ f, const uint32_t* __restrict__ n_bad, int* __restrict__ result);
 #define TB_PARTIAL_BYTES 580u  // one device's partial record (= TBLS_PARTIAL_BYTES, include/tekubls.h)
 extern "C" __global__ void k_final_verify_recs(const uint8_t* __restrict__ recs, uint32_t g, int* __restrict__ result);
+// lane-cooperative forms (tb_cfe.h), 256 threads: the default final exponentiation
+#define TB_CFE_THREADS 256
+extern "C" __global__ void k_final_verify_recs_coop(const uint8_t* __restrict__ recs, uint32_t g, int* __restrict__ result);
+extern "C" __global__ void k_final_verify_coop(const fp12* __restrict__ f, uint32_t g, const uint32_t* __restrict__ n_bad, int* __restrict__ result);
+// TBLS_FINAL_COOP=0 selects the one-wave final exponentiation (A/B)
+inline bool tb_final_coop() {
+  static const bool v = !(getenv("TBLS_FINAL_COOP") && getenv("TBLS_FINAL_COOP")[0] == '0');
+  return v;
+}
+// the final verification of g partial records on stream s (*result in device memory)
+inline void tb_launch_final_recs(const uint8_t* recs, uint32_t g, hipStream_t s, int* result) {
+  if (tb_final_coop())
+    hipLaunchKernelGGL(k_final_verify_recs_coop, dim3(1), dim3(TB_CFE_THREADS), 0, s, recs, g, result);
+  else
+    hipLaunchKernelGGL(k_final_verify_recs, dim3(1), dim3(64), 0, s, recs, g, result);
+}

@@ -448,7 +448,7 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
 int launch_final(dev_ctx& c, const void* recs, uint32_t g, hipStream_t s, int* result_host) {
   if (c.fin.ensure(256)) return TBLS_DEVICE_ERROR;
   int* res = c.fin.as<int>();
-  hipLaunchKernelGGL(k_final_verify_recs, dim3(1), dim3(64), 0, s, (const uint8_t*)recs, g, res);
+  tb_launch_final_recs((const uint8_t*)recs, g, s, res);
   HIPCHK(hipGetLastError());
   if (c.hout.ensure(16)) return TBLS_DEVICE_ERROR;
   HIPCHK(hipMemcpyAsync(c.hout.p, res, 4, hipMemcpyDeviceToHost, s));
@@ -1474,7 +1474,7 @@ extern "C" int tbls_sign_many(const uint8_t* sks, const uint8_t* msgs, const uin
 // invalid count in one per-device scratch buffer that two finals on different
 // streams overwrote -- see DESIGN.md, "Asynchronous final verification").
 int launch_final_async(const void* recs, uint32_t g, hipStream_t s, int* ok_dev) {
-  hipLaunchKernelGGL(k_final_verify_recs, dim3(1), dim3(64), 0, s, (const uint8_t*)recs, g, ok_dev);
+  tb_launch_final_recs((const uint8_t*)recs, g, s, ok_dev);
   HIPCHK(hipGetLastError());
   return TBLS_SUCCESS;
 }

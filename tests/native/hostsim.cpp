@@ -87,3 +87,29 @@ extern "C" int tbls_hostsim_coop_to_fp(const int32_t* d, uint32_t* out, size_t n
   }
   return 0;
 }
+
+// a^((p+1)/4) on the coop path (cpow_win_n<2>: bases a, b) vs fp_pow_win
+extern "C" int tbls_hostsim_coop_sqrt_cand(const uint32_t* a, uint32_t* out, size_t n) {
+  for (size_t k = 0; k + 1 < n + 1; k += 2) {
+    const size_t k1 = k + 1 < n ? k + 1 : k;
+    tb::coop::c32 x[2] = {tb::coop::cfrom_words(a + 12 * k), tb::coop::cfrom_words(a + 12 * k1)}, r[2];
+    tb::coop::cpow_win_n<2>(r, x, tb::EXPW_SQRT_FIRST, tb::EXPW_SQRT, tb::EXPW_SQRT_N);
+    const tb::fp f0 = tb::coop::cdigits_to_fp(r[0].v), f1 = tb::coop::cdigits_to_fp(r[1].v);
+    for (int j = 0; j < 12; j++) {
+      out[12 * k + j] = f0.l[j];
+      if (k1 != k) out[12 * k1 + j] = f1.l[j];
+    }
+  }
+  return 0;
+}
+
+// creduce64 on 64-bit digit sums (16 int64 per vector)
+extern "C" int tbls_hostsim_coop_reduce(const int64_t* x, int32_t* out, size_t n) {
+  for (size_t k = 0; k < n; k++) {
+    tb::coop::c64 v;
+    for (int j = 0; j < 16; j++) v.v[j] = x[16 * k + j];
+    const tb::coop::c32 r = tb::coop::creduce64(v);
+    for (int j = 0; j < 16; j++) out[16 * k + j] = r.v[j];
+  }
+  return 0;
+}

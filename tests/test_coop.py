@@ -123,3 +123,39 @@ def test_coop_to_fp_signed(lib):
     for dd, r in zip(D, out):
         v = sum(int(r[i]) << (32 * i) for i in range(12))
         assert v < 2 * P and v % P == val(dd) % P
+
+
+def test_coop_pow_win(lib):
+    """cpow_win_n<2> with the (p+1)/4 schedule equals a^((p+1)/4) (Montgomery
+    form in and out: the residue a R^-1 ... handled by comparing x^2 == a)."""
+    lib.tbls_hostsim_coop_sqrt_cand.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
+    rng = random.Random(9)
+    vals = [rng.randrange(P) for _ in range(6)] + [1, P - 1]
+    w = lambda v: np.array([(v >> (32 * i)) & 0xFFFFFFFF for i in range(12)], dtype=np.uint32)  # noqa: E731
+    a = np.ascontiguousarray(np.stack([w(v * R % P) for v in vals]))  # Montgomery form
+    out = np.zeros_like(a)
+    lib.tbls_hostsim_coop_sqrt_cand(a.ctypes.data, out.ctypes.data, len(vals))
+    for v, r in zip(vals, out):
+        m = sum(int(r[i]) << (32 * i) for i in range(12)) * RINV % P
+        assert m == pow(v, (P + 1) // 4, P)
+
+
+def test_coop_reduce(lib):
+    """creduce64: sums of up to 64 product outputs (64-bit digit sums, |v| up to
+    2^395) -> T = 1 digits with |v| < 1.6 p, same residue."""
+    lib.tbls_hostsim_coop_reduce.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
+    rng = random.Random(11)
+    X = []
+    for _ in range(400):
+        k = rng.choice([1, 2, 8, 36, 64, 4096])
+        d = [sum(rng.randint(-(1 << 28), 1 << 28) for _ in range(min(k, 8))) * max(1, k // 8) for _ in range(13)]
+        top = rng.randint(-(1 << 5), 1 << 5) * k
+        X.append(d + [top, 0, 0])
+    x = np.ascontiguousarray(np.array(X, dtype=np.int64))
+    out = np.zeros((len(X), 16), dtype=np.int32)
+    lib.tbls_hostsim_coop_reduce(x.ctypes.data, out.ctypes.data, len(X))
+    for a, r in zip(X, out):
+        assert r[14] == 0 and r[15] == 0
+        assert all(abs(int(v)) <= (1 << 28) + (1 << 12) for v in r[:13])
+        assert abs(val(r)) < 1.6 * P
+        assert (val(r) - val(a)) % P == 0

@@ -234,6 +234,9 @@ def test_cfe_ops(run):
     recs = [enc_fp12(f) + enc_fp12(g) + op(5), enc_fp12(c) + enc_fp12(g) + op(6), enc_fp12(f) + enc_fp12(g) + op(7)]
     got = [dec_fp12(x) for x in run("CFE_OPS", recs)]
     e = O.final_exponentiation(f)
-    exp = [t, O.f12_conj(O.f12_pow(c, -X)), O.f12_mul(O.f12_mul(e, e), e)]  # the device chain computes the 3 x hard part
-    bad += [n for n, a, b in zip(["easy", "exp_x", "final"], got, exp) if a != b]
+    exp = [O.f12_inv(f), O.f12_conj(O.f12_pow(c, -X)), O.f12_mul(O.f12_mul(e, e), e)]  # the device chain computes the 3 x hard part
+    bad += [n for n, a, b in zip(["inv", "exp_x", "final"], got, exp) if a != b]
     assert not bad, bad
+    o = run("CFE_OPS", [enc_fp12(c) + enc_fp12(g) + op(8)])[0]
+    cyc = [int.from_bytes(o[576 + 8 * i : 584 + 8 * i], "little") for i in range(3)]
+    print("\ncoop levels: cyc_sqr %.0f, mul %.0f cycles; inversion %d cycles" % (cyc[0] / 64, cyc[1] / 64, cyc[2]))
