@@ -47,3 +47,87 @@ extern "C" __global__ void __launch_bounds__(128)
     skip[i] = ok ? 0 : 1;
   }
 }
+
+// ---------------------------------------------------------------------------
+// Lane-cooperative form (tb_cprog.h), one 256-thread workgroup (16 rows) per
+// set: lane 0 runs expand_message_xmd / hash_to_field (serial SHA-256), rows
+// 0 and 1 run the two SSWU maps side by side as coop chains (the square-root
+// exponentiations are ~1k-cycle coop products instead of one lane's), lane 0
+// the E2' addition and the isogeny, all 16 rows the cofactor program through
+// the coop level interpreter, lane 0 the affine conversion.  Same Q_i and
+// skip_i as k_set_hash (the Z = 0 fallback included).
+// ---------------------------------------------------------------------------
+#include "tb_cprog.h"
+
+struct hcoop_lds {
+  cdig S[CF_NSLOT];
+  uint16_t tab[CF_TAB_N];
+  crow::rowbuf rb[16];
+  fp2 u[2];
+  g2a qm[2];
+  g2j J;
+  fp res[6];
+};
+
+extern "C" __global__ void __launch_bounds__(256)
+    k_set_hash_coop(const uint8_t* __restrict__ msgs, const uint32_t* __restrict__ msg_off, const uint8_t* __restrict__ dst,
+                    uint32_t dlen, uint32_t n, g2a* __restrict__ Q, uint8_t* __restrict__ skip) {
+  __shared__ hcoop_lds L;
+  const uint32_t i = blockIdx.x;
+  if (i >= n) return;
+  tb_latency_prio();
+  const coop::cctx K = coop::cctx_load();
+  const int g = crow::row(), d = crow::dig();
+  for (int j = threadIdx.x; j < CF_TAB_N; j += blockDim.x) L.tab[j] = CF_TAB[j];
+  for (int j = threadIdx.x; j < CF_NSLOT * 16; j += blockDim.x) (&L.S[0][0])[j] = 0;
+  if (threadIdx.x == 0) {
+    xmd_ctx c;
+    c.msg = msgs + msg_off[i];
+    c.mlen = msg_off[i + 1] - msg_off[i];
+    c.dst = dst;
+    c.dlen = dlen;
+    hash_to_field_fp2(L.u[0], L.u[1], c);
+  }
+  __syncthreads();
+  if (g < 2) {
+    const g2a q = crow::sswu(L.u[g], L.rb[g], K);
+    if (d == 0) L.qm[g] = q;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) L.J = iso_map_jac(e2p_add_aff_aff(L.qm[0], L.qm[1]));
+  __syncthreads();
+  // slots: the point (Jacobian, Fp2 coordinates) and the psi constants
+  if (g < 6) {
+    const fp* jw = g < 2 ? &L.J.x.c0 : (g < 4 ? &L.J.y.c0 : &L.J.z.c0);
+    L.S[CF_S_JX0 + g][d] = coop::cfrom_words(jw[g & 1].l);
+  } else if (g < 12) {
+    const uint32_t* cw = g == 6 ? PSI_CX[0] : g == 7 ? PSI_CX[1] : g == 8 ? PSI_CY[0] : g == 9 ? PSI_CY[1] : g == 10 ? PSI2_CX[0] : PSI2_CY[0];
+    const int slot = g < 10 ? CF_S_CPX0 + (g - 6) : (g == 10 ? CF_S_CQX : CF_S_CQY);
+    L.S[slot][d] = coop::cfrom_words(cw);
+  }
+  __syncthreads();
+  for (int k = 0; k < CF_NLEVEL; k++) crow::level<2, 2, CF_AMAX, CF_BMAX, CF_QMAX * CF_OMAX>(L.S, L.tab, CF_TYPE_OFF[CF_SEQ[k]], K);
+  if (g < 6) {
+    const fp v = crow::to_fp(L.S[CF_S_RX0 + g][d], L.rb[g].d, &L.rb[g].f);
+    if (d == 0) L.res[g] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const fp2 X = {L.res[0], L.res[1]}, Y = {L.res[2], L.res[3]}, Z = {L.res[4], L.res[5]};
+    g2a a;
+    bool ok = true;
+    if (fp2_is_zero(Z)) {
+      ok = jac_to_aff(a, g2_clear_cofactor(L.J));
+    } else {
+      const fp2 zi = fp2_inv(Z);
+      a.x = fp2_mul(X, zi);
+      a.y = fp2_mul(Y, zi);
+    }
+    if (!ok) {
+      a.x = fp2_zero();
+      a.y = fp2_zero();
+    }
+    Q[i] = a;
+    skip[i] = ok ? 0 : 1;
+  }
+}

@@ -92,12 +92,15 @@ __device__ TB_INLINE void final_verify_coop(const uint8_t* recs, size_t stride, 
   __shared__ cfe_lds L;
   tb_latency_prio();
   cfe::init(L);
+  cfe_regs R;
+  cfe::regs_load(R, L);
+  (void)R.K;
   cfe::load_coords(L.F, reinterpret_cast<const fp*>(recs));
   for (uint32_t i = 1; i < g; i++) {
     cfe::load_coords(L.X, reinterpret_cast<const fp*>(recs + (size_t)i * stride));
-    cfe::mul(L.F, L.F, L.X, L);
+    cfe::mul(L.F, L.F, L.X, L, R);
   }
-  const bool one = cfe::final_exp_is_one(L);
+  const bool one = cfe::final_exp_is_one(L, R);
   if (threadIdx.x == 0) {
     uint32_t bad = bad_in;
     if (count_bad)

@@ -47,9 +47,25 @@ struct cfe_lds {
   int flag;
 };
 
+// A row's table entries of one op, in registers (loaded once per kernel: the
+// per-level sums then read only the values from LDS)
+template <int KP, int AMAX, int BMAX, int PMAX, int LMAX>
+struct cfe_ents {
+  int32_t a[KP][AMAX], b[KP][BMAX], post[PMAX], lin[LMAX > 0 ? LMAX : 1];
+};
+#define CFE_ENTS(P) cfe_ents<(P##_NPROD + 15) / 16, P##_A_MAXLEN, P##_B_MAXLEN, P##_POST_MAXLEN, P##_LIN_MAXLEN>
+
+// everything a thread keeps in registers across the levels
+struct cfe_regs {
+  coop::cctx K;
+  CFE_ENTS(W12M) em;
+  CFE_ENTS(W12C) ec;
+};
+
 namespace cfe {
 using coop::c32;
 using coop::c64;
+using coop::cctx;
 
 __device__ TB_INLINE int row() { return (int)(threadIdx.x >> 4); }
 __device__ TB_INLINE int dig() { return (int)(threadIdx.x & 15u); }
@@ -90,39 +106,57 @@ __device__ TB_INLINE void ptab_build(PTAB& pt) {
   }
 }
 
-template <int NPROD, int AMAX, int BMAX, int PMAX, int LMAX, typename PTAB>
-__device__ TB_INLINE void bilinear(cdig* dst, const cdig* x, const cdig* y, const PTAB& pt, cfe_lds& L) {
-  constexpr int K = (NPROD + CFE_ROWS - 1) / CFE_ROWS;
+template <int KP, int AMAX, int BMAX, int PMAX, int LMAX, typename PTAB>
+__device__ TB_INLINE void ents_load(cfe_ents<KP, AMAX, BMAX, PMAX, LMAX>& e, const PTAB& pt) {
+  const int g = row();
+  TB_UNROLL for (int k = 0; k < KP; k++) {
+    TB_UNROLL for (int j = 0; j < AMAX; j++) e.a[k][j] = pt.a[g + 16 * k][j];
+    TB_UNROLL for (int j = 0; j < BMAX; j++) e.b[k][j] = pt.b[g + 16 * k][j];
+  }
+  TB_UNROLL for (int j = 0; j < PMAX; j++) e.post[j] = g < 12 ? pt.post[g][j] : 0;
+  TB_UNROLL for (int j = 0; j < (LMAX > 0 ? LMAX : 1); j++) e.lin[j] = g < 12 ? pt.lin[g][j] : 0;
+}
+
+template <int NPROD, int AMAX, int BMAX, int PMAX, int LMAX, typename ENTS>
+__device__ TB_INLINE void bilinear(cdig* dst, const cdig* x, const cdig* y, const ENTS& pt, cfe_lds& L, const cctx& K) {
+  constexpr int KP = (NPROD + CFE_ROWS - 1) / CFE_ROWS;
   static_assert(AMAX <= 8 && BMAX <= 8, "operand sums: class <= 8 before the carry step");
   const int g = row(), d = dig();
-  c32 pa[K], pb[K], pr[K];
-  TB_UNROLL for (int k = 0; k < K; k++) {
+  c32 pa[KP], pb[KP], pr[KP];
+  TB_UNROLL for (int k = 0; k < KP; k++) {
     const int t = g + CFE_ROWS * k;
-    pa[k] = cnorm64(tsum<AMAX>(x, pt.a[t]));
-    pb[k] = cnorm64(tsum<BMAX>(y, pt.b[t]));
+    pa[k] = cnorm64(tsum<AMAX>(x, pt.a[k]));
+    pb[k] = cnorm64(tsum<BMAX>(y, pt.b[k]));
   }
-  TB_UNROLL for (int k = 0; k < K; k++) pr[k] = coop::cmul(pa[k], pb[k]);
-  TB_UNROLL for (int k = 0; k < K; k++) {
+  TB_UNROLL for (int k = 0; k < KP; k++) pr[k] = coop::cmul(pa[k], pb[k], K);
+  TB_UNROLL for (int k = 0; k < KP; k++) {
     const int t = g + CFE_ROWS * k;
     if (t < NPROD) L.prod[t][d] = pr[k];
   }
   __syncthreads();
   c32 out = 0;
   if (g < 12) {  // output coordinate g, digit d
-    c64 acc = tsum<PMAX>(L.prod, pt.post[g]);
-    if constexpr (LMAX > 0) acc += tsum<LMAX>(x, pt.lin[g]);
-    out = creduce64(acc);  // |v| < 1.6 p: no growth along the chain
+    c64 acc = tsum<PMAX>(L.prod, pt.post);
+    if constexpr (LMAX > 0) acc += tsum<LMAX>(x, pt.lin);
+    out = creduce64(acc, K.plo[0]);  // |v| < 1.6 p: no growth along the chain
   }
   __syncthreads();
   if (g < 12) dst[g][d] = out;
   __syncthreads();
 }
 
-__device__ TB_INLINE void mul(cdig* dst, const cdig* x, const cdig* y, cfe_lds& L) {
-  bilinear<W12M_NPROD, W12M_A_MAXLEN, W12M_B_MAXLEN, W12M_POST_MAXLEN, W12M_LIN_MAXLEN>(dst, x, y, L.tm, L);
+__device__ TB_INLINE void mul(cdig* dst, const cdig* x, const cdig* y, cfe_lds& L, const cfe_regs& R) {
+  bilinear<W12M_NPROD, W12M_A_MAXLEN, W12M_B_MAXLEN, W12M_POST_MAXLEN, W12M_LIN_MAXLEN>(dst, x, y, R.em, L, R.K);
 }
-__device__ TB_INLINE void cyc_sqr(cdig* dst, const cdig* x, cfe_lds& L) {
-  bilinear<W12C_NPROD, W12C_A_MAXLEN, W12C_B_MAXLEN, W12C_POST_MAXLEN, W12C_LIN_MAXLEN>(dst, x, x, L.tc, L);
+__device__ TB_INLINE void cyc_sqr(cdig* dst, const cdig* x, cfe_lds& L, const cfe_regs& R) {
+  bilinear<W12C_NPROD, W12C_A_MAXLEN, W12C_B_MAXLEN, W12C_POST_MAXLEN, W12C_LIN_MAXLEN>(dst, x, x, R.ec, L, R.K);
+}
+
+// the registers of a thread (after init(L))
+__device__ TB_INLINE void regs_load(cfe_regs& R, const cfe_lds& L) {
+  R.K = coop::cctx_load();
+  ents_load(R.em, L.tm);
+  ents_load(R.ec, L.tc);
 }
 
 __device__ TB_INLINE void copy(cdig* dst, const cdig* x) {
@@ -148,7 +182,7 @@ __device__ TB_INLINE void conj(cdig* dst, const cdig* x) {
 // w-power wp(j) = 0, 2, 4, 1, 3, 5; c -> conj(c) gamma_wp.  Rows 0..14 run
 // the 15 products of the five pairs j = 1..5: (x0 - x1 u)(g0 + g1 u) =
 // (x0 g0 + x1 g1) + ((x0 - x1)(g0 + g1) - x0 g0 + x1 g1) u.
-__device__ TB_INLINE void frob(cdig* dst, const cdig* x, cfe_lds& L) {
+__device__ TB_INLINE void frob(cdig* dst, const cdig* x, cfe_lds& L, const cfe_regs& R) {
   const int g = row(), d = dig();
   c32 a = 0, b = 0;
   if (g < 15) {
@@ -157,7 +191,7 @@ __device__ TB_INLINE void frob(cdig* dst, const cdig* x, cfe_lds& L) {
     a = k == 0 ? x0 : (k == 1 ? x1 : x0 - x1);
     b = L.gam[wp - 1][k][d];
   }
-  const c32 pr = coop::cmul(a, b);
+  const c32 pr = coop::cmul(a, b, R.K);
   if (g < 15) L.prod[g][d] = pr;
   __syncthreads();
   c32 out = 0;
@@ -168,7 +202,7 @@ __device__ TB_INLINE void frob(cdig* dst, const cdig* x, cfe_lds& L) {
     } else {
       const int b3 = 3 * (j - 1);
       const c32 p0 = L.prod[b3][d], p1 = L.prod[b3 + 1][d], p2 = L.prod[b3 + 2][d];
-      out = creduce64((g & 1) ? (c64)p2 - (c64)p0 + (c64)p1 : (c64)p0 + (c64)p1);
+      out = creduce64((g & 1) ? (c64)p2 - (c64)p0 + (c64)p1 : (c64)p0 + (c64)p1, R.K.plo[0]);
     }
   }
   __syncthreads();
@@ -177,11 +211,11 @@ __device__ TB_INLINE void frob(cdig* dst, const cdig* x, cfe_lds& L) {
 }
 
 // dst = src^x (conj of src^|x|) for src in the cyclotomic subgroup (dst != src)
-__device__ TB_INLINE void cyc_exp_x(cdig* dst, const cdig* src, cfe_lds& L) {
+__device__ TB_INLINE void cyc_exp_x(cdig* dst, const cdig* src, cfe_lds& L, const cfe_regs& R) {
   copy(dst, src);
   for (int i = 62; i >= 0; --i) {
-    cyc_sqr(dst, dst, L);
-    if ((X_ABS >> i) & 1) mul(dst, dst, src, L);
+    cyc_sqr(dst, dst, L, R);
+    if ((X_ABS >> i) & 1) mul(dst, dst, src, L, R);
   }
   conj(dst, dst);
 }
@@ -230,69 +264,69 @@ __device__ TB_INLINE void init(cfe_lds& L) {
 // every step on the coop levels above, one lone-lane Fp inversion:
 //   N = x conj(x) in Fp6;  u = N^(p^2) N^(p^4);  v = N u in Fp2;
 //   n = v0^2 + v1^2 in Fp;  x^-1 = conj(x) u conj2(v) / n
-__device__ TB_INLINE void inv(cdig* dst, const cdig* x, cfe_lds& L) {
+__device__ TB_INLINE void inv(cdig* dst, const cdig* x, cfe_lds& L, const cfe_regs& R) {
   const int g = row(), d = dig();
   conj(L.Y, x);
-  mul(L.A, x, L.Y, L);    // N
-  frob(L.B, L.A, L);
-  frob(L.B, L.B, L);      // N^(p^2)
-  frob(L.C, L.B, L);
-  frob(L.C, L.C, L);      // N^(p^4)
-  mul(L.C, L.B, L.C, L);  // u
-  mul(L.E, L.A, L.C, L);  // v = N u (coordinates 0, 1)
+  mul(L.A, x, L.Y, L, R);    // N
+  frob(L.B, L.A, L, R);
+  frob(L.B, L.B, L, R);      // N^(p^2)
+  frob(L.C, L.B, L, R);
+  frob(L.C, L.C, L, R);      // N^(p^4)
+  mul(L.C, L.B, L.C, L, R);  // u
+  mul(L.E, L.A, L.C, L, R);  // v = N u (coordinates 0, 1)
   // n = v0^2 + v1^2 on rows 0, 1; n^-1 on one lane
   const c32 vi = g < 2 ? L.E[g][d] : 0;
-  const c32 sq = coop::cmul(vi, vi);
+  const c32 sq = coop::cmul(vi, vi, R.K);
   if (g < 2) L.prod[g][d] = sq;
   __syncthreads();
-  if (g == 0) L.prod[2][d] = creduce64((c64)L.prod[0][d] + (c64)L.prod[1][d]);
+  if (g == 0) L.prod[2][d] = creduce64((c64)L.prod[0][d] + (c64)L.prod[1][d], R.K.plo[0]);
   __syncthreads();
   if (threadIdx.x == 0) L.tmp[0] = fp_inv(coop::cdigits_to_fp(L.prod[2]));
   __syncthreads();
   // w = conj2(v) / n: coordinates 0, 1 (rows 0, 1), zero elsewhere
   const c32 ninv = coop::cfrom_words(L.tmp[0].l);
-  const c32 wv = coop::cmul(vi, ninv);
+  const c32 wv = coop::cmul(vi, ninv, R.K);
   __syncthreads();
   if (g < 12) L.B[g][d] = g == 0 ? wv : (g == 1 ? -wv : 0);
   __syncthreads();
-  mul(L.C, L.C, L.B, L);   // u / v = N^-1
-  mul(dst, L.Y, L.C, L);   // conj(x) / N = x^-1
+  mul(L.C, L.C, L.B, L, R);   // u / v = N^-1
+  mul(dst, L.Y, L.C, L, R);   // conj(x) / N = x^-1
 }
 
 // L.F <- final_exp(L.F) (tb_pairing.h final_exp's chain; whole workgroup)
-__device__ TB_INLINE void final_exp(cfe_lds& L) {
+__device__ TB_INLINE void final_exp(cfe_lds& L, const cfe_regs& R) {
   // easy part: t = conj(f) / f
-  inv(L.X, L.F, L);
+  inv(L.X, L.F, L, R);
   conj(L.Y, L.F);
-  mul(L.T, L.Y, L.X, L);
-  frob(L.X, L.T, L);
-  frob(L.X, L.X, L);
-  mul(L.T, L.X, L.T, L);  // t = f^((p^6-1)(p^2+1))
+  mul(L.T, L.Y, L.X, L, R);
+  frob(L.X, L.T, L, R);
+  frob(L.X, L.X, L, R);
+  mul(L.T, L.X, L.T, L, R);  // t = f^((p^6-1)(p^2+1))
   // hard part (x3)
-  cyc_exp_x(L.E, L.T, L);
+  cyc_exp_x(L.E, L.T, L, R);
   conj(L.X, L.T);
-  mul(L.A, L.E, L.X, L);  // a = t^(x-1)
-  cyc_exp_x(L.E, L.A, L);
+  mul(L.A, L.E, L.X, L, R);  // a = t^(x-1)
+  cyc_exp_x(L.E, L.A, L, R);
   conj(L.X, L.A);
-  mul(L.A, L.E, L.X, L);  // a = t^((x-1)^2)
-  cyc_exp_x(L.E, L.A, L);
-  frob(L.X, L.A, L);
-  mul(L.B, L.E, L.X, L);  // b = a^(x+p)
-  cyc_exp_x(L.E, L.B, L);
-  cyc_exp_x(L.C, L.E, L);
-  frob(L.X, L.B, L);
-  frob(L.X, L.X, L);
-  mul(L.C, L.C, L.X, L);
+  mul(L.A, L.E, L.X, L, R);  // a = t^((x-1)^2)
+  cyc_exp_x(L.E, L.A, L, R);
+  frob(L.X, L.A, L, R);
+  mul(L.B, L.E, L.X, L, R);  // b = a^(x+p)
+  cyc_exp_x(L.E, L.B, L, R);
+  cyc_exp_x(L.C, L.E, L, R);
+  frob(L.X, L.B, L, R);
+  frob(L.X, L.X, L, R);
+  mul(L.C, L.C, L.X, L, R);
   conj(L.X, L.B);
-  mul(L.C, L.C, L.X, L);  // c = b^(x^2+p^2-1)
-  cyc_sqr(L.X, L.T, L);
-  mul(L.X, L.X, L.T, L);  // t^3
-  mul(L.F, L.C, L.X, L);
+  mul(L.C, L.C, L.X, L, R);  // c = b^(x^2+p^2-1)
+  cyc_sqr(L.X, L.T, L, R);
+  mul(L.X, L.X, L.T, L, R);  // t^3
+  mul(L.F, L.C, L.X, L, R);
 }
 
 // final_exp(L.F) == 1 (whole workgroup; the verdict on every thread)
-__device__ TB_INLINE bool final_exp_is_one(cfe_lds& L) {
-  final_exp(L);
+__device__ TB_INLINE bool final_exp_is_one(cfe_lds& L, const cfe_regs& R) {
+  final_exp(L, R);
   store_coords(L.F, L);
   if (threadIdx.x == 0) L.flag = fp12_is_one(fp12_from_coords(L.tmp)) ? 1 : 0;
   __syncthreads();

@@ -270,13 +270,15 @@ TBC_FN c32 cnorm64(c64 x) {
 // lazy sums (the final exponentiation's levels, the wave programs' slots)
 // from growing.
 TB_CONST float CQ_SCALE = 1.43257367e-10f;  // 2^348 / p
-TBC_FN c32 creduce64(c64 x) {
+// pj: this lane's digit of p (lanes 14, 15: 0) -- cctx::plo[0]
+TBC_FN c32 creduce64(c64 x, c32 pj) {
   const c32 d = cnorm64(x);
 #if defined(__HIPCC__)
   const float t = (float)d * 536870912.0f + (float)shr<1>(d);  // lane 13: d13 2^29 + d12
   const c32 q = bcast<13>((int32_t)__builtin_rintf(t * CQ_SCALE));
-  return cnorm64((c64)d - mulw(q, lane_const(CP_BAL16)));
+  return cnorm64((c64)d - mulw(q, pj));
 #else
+  (void)pj;
   const c32 d12 = shr<1>(d);
   const int32_t q = (int32_t)std::nearbyint(((float)d.v[13] * 536870912.0f + (float)d12.v[13]) * CQ_SCALE);
   c64 y;
@@ -284,10 +286,44 @@ TBC_FN c32 creduce64(c64 x) {
   return cnorm64(y);
 #endif
 }
-TBC_FN c32 creduce(c32 x) { return creduce64(wide(x)); }
+
+
+// Per-lane constant windows of the product's two constant operands (loaded
+// once per kernel; 42 VGPRs): lane j holds
+//   np[i]  = N'_{j-i}        (i <= j)            step 2, Q_j = sum_i E_i np[i]
+//   plo[i] = p_{j-i}         (i <= j)            step 3, column j
+//   phi[i] = p_{j+16-i}      (j + 16 - i <= 13)  step 3, column j + 16
+// so those steps are a broadcast and one or two multiply-adds per digit, no
+// rotations or lane masks.
+struct cctx {
+  c32 np[14], plo[14], phi[14];
+};
+#if defined(__HIPCC__)
+TBC_FN cctx cctx_load() {
+  cctx k;
+  const int j = lane16();
+  TB_UNROLL for (int i = 0; i < 14; i++) {
+    k.np[i] = (j >= i && j - i <= 13) ? CNP_BAL[j - i] : 0;
+    k.plo[i] = (j >= i && j - i <= 13) ? CP_BAL[j - i] : 0;
+    k.phi[i] = (j + 16 - i <= 13) ? CP_BAL[j + 16 - i] : 0;
+  }
+  return k;
+}
+#else
+inline cctx cctx_load() {
+  cctx k;
+  for (int i = 0; i < 14; i++)
+    for (int j = 0; j < 16; j++) {
+      k.np[i].v[j] = (j >= i && j - i <= 13) ? CNP_BAL[j - i] : 0;
+      k.plo[i].v[j] = (j >= i && j - i <= 13) ? CP_BAL[j - i] : 0;
+      k.phi[i].v[j] = (j + 16 - i <= 13) ? CP_BAL[j + 16 - i] : 0;
+    }
+  return k;
+}
+#endif
 
 // Montgomery product a b R^-1 (mod p): the five steps of the file comment.
-TBC_FN c32 cmul(c32 a, c32 b) {
+TBC_FN c32 cmul(c32 a, c32 b, const cctx& K) {
   // 1. T = a b: lane j accumulates column j (tlo) and column j + 16 (thi)
   c64 tlo = c64(0), thi = c64(0);
 #define TBC_S1(i)                                  \
@@ -310,7 +346,7 @@ TBC_FN c32 cmul(c32 a, c32 b) {
   }
   // 3. Q_j = sum_{i <= j} E_{j-i} N'_i  (j < 14), then its digits q (mod R)
   c64 Q = c64(0);
-#define TBC_S3(i) Q += mulw(keep_ge(i, ror<i>(E)), CNP_BAL[i]);
+#define TBC_S3(i) Q += mulw(bcast<i>(E), K.np[i]);
   TBC_REP14(TBC_S3)
 #undef TBC_S3
   c32 q;
@@ -322,12 +358,11 @@ TBC_FN c32 cmul(c32 a, c32 b) {
     q = keep_lt(14, l + shr<1>(m) + shr<2>(h));
   }
   // 4. W = T + q p (columns, into tlo / thi)
-#define TBC_S4(t)                                  \
-  {                                                \
-    const c32 qv = ror<t>(q);                      \
-    const c32 qlo = keep_ge(t, qv);                \
-    tlo += mulw(qlo, CP_BAL[t]);                   \
-    thi += mulw(qv - qlo, CP_BAL[t]);              \
+#define TBC_S4(i)                    \
+  {                                  \
+    const c32 qi = bcast<i>(q);      \
+    tlo += mulw(qi, K.plo[i]);       \
+    thi += mulw(qi, K.phi[i]);       \
   }
   TBC_REP14(TBC_S4)
 #undef TBC_S4
@@ -350,37 +385,37 @@ TBC_FN c32 cmul(c32 a, c32 b) {
   return keep_lt(14, sel_lt(13, dl, top) + shr<1>(dc));
 }
 
-TBC_FN c32 csqr(c32 a) { return cmul(a, a); }
+TBC_FN c32 csqr(c32 a, const cctx& K) { return cmul(a, a, K); }
 
 // N independent products interleaved (one instruction stream, N chains: the
 // row's latency-bound product issues N x the work in about the same time)
 template <int N>
-TBC_FN void cmul_n(c32 (&r)[N], const c32 (&a)[N], const c32 (&b)[N]) {
-  TB_UNROLL for (int k = 0; k < N; k++) r[k] = cmul(a[k], b[k]);
+TBC_FN void cmul_n(c32 (&r)[N], const c32 (&a)[N], const c32 (&b)[N], const cctx& K) {
+  TB_UNROLL for (int k = 0; k < N; k++) r[k] = cmul(a[k], b[k], K);
 }
 
 // a^e for the fixed exponents of tb_fp.h fp_pow_win (sliding window w = 4:
 // sched[k] = squarings << 4 | (table index < 8 ? multiply by a^(2i+1) : none)),
 // for N bases at once (interleaved chains).
 template <int N>
-TBC_FN void cpow_win_n(c32 (&r)[N], const c32 (&a)[N], uint32_t first, const uint16_t* sched, int nstep) {
+TBC_FN void cpow_win_n(c32 (&r)[N], const c32 (&a)[N], uint32_t first, const uint16_t* sched, int nstep, const cctx& K) {
   c32 tab[8][N], a2[N];
   TB_UNROLL for (int k = 0; k < N; k++) tab[0][k] = a[k];
-  cmul_n<N>(a2, a, a);
-  TB_UNROLL for (int i = 1; i < 8; i++) cmul_n<N>(tab[i], tab[i - 1], a2);
+  cmul_n<N>(a2, a, a, K);
+  TB_UNROLL for (int i = 1; i < 8; i++) cmul_n<N>(tab[i], tab[i - 1], a2, K);
   TB_UNROLL for (int k = 0; k < N; k++) r[k] = tab[0][k];
   TB_UNROLL for (int i = 1; i < 8; i++)
     if (first == (uint32_t)i) TB_UNROLL for (int k = 0; k < N; k++) r[k] = tab[i][k];
   TB_NOUNROLL for (int s = 0; s < nstep; s++) {
     const uint32_t e = sched[s];
-    TB_NOUNROLL for (uint32_t j = 0; j < (e >> 4); j++) cmul_n<N>(r, r, r);
+    TB_NOUNROLL for (uint32_t j = 0; j < (e >> 4); j++) cmul_n<N>(r, r, r, K);
     const uint32_t t = e & 15u;
     if (t < 8u) {
       c32 m[N];
       TB_UNROLL for (int k = 0; k < N; k++) m[k] = tab[0][k];
       TB_UNROLL for (int i = 1; i < 8; i++)
         if (t == (uint32_t)i) TB_UNROLL for (int k = 0; k < N; k++) m[k] = tab[i][k];
-      cmul_n<N>(r, r, m);
+      cmul_n<N>(r, r, m, K);
     }
   }
 }

@@ -251,6 +251,15 @@ void launch_set_pk(hipStream_t s, uint32_t n, uint32_t n_entries, const uint32_t
 extern "C" __global__ void k_set_hash_wave(const uint8_t* __restrict__ msgs, const uint32_t* __restrict__ msg_off,
                                            const uint8_t* __restrict__ dst, uint32_t dlen, uint32_t n, g2a* __restrict__ Q,
                                            uint8_t* __restrict__ skip);  // k_hwave.hip
+extern "C" __global__ void k_set_hash_coop(const uint8_t* __restrict__ msgs, const uint32_t* __restrict__ msg_off,
+                                           const uint8_t* __restrict__ dst, uint32_t dlen, uint32_t n, g2a* __restrict__ Q,
+                                           uint8_t* __restrict__ skip);  // k_hwave.hip (lane-cooperative, 256 threads)
+// small batches hash with the lane-cooperative kernel; TBLS_HASH_COOP=0 selects
+// the one-wave cofactor program (k_set_hash_wave) for A/B
+static bool hash_coop() {
+  static const bool v = !(getenv("TBLS_HASH_COOP") && getenv("TBLS_HASH_COOP")[0] == '0');
+  return v;
+}
 
 int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* partial_out, ws_layout& L,
                    const uint8_t* dst, uint32_t dlen, hipEvent_t* ev = nullptr, bool serial_req = false,
@@ -297,7 +306,9 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
   }
   auto launch_hash = [&]() -> int {
     TB_EV(6, sh);
-    if (n && n <= TB_HASH_WAVE_MAX)  // one workgroup per set: the cofactor clearing lane-parallel
+    if (n && n <= TB_HASH_WAVE_MAX && hash_coop())  // one 256-thread workgroup per set: coop SSWU chains and cofactor program
+      hipLaunchKernelGGL(k_set_hash_coop, dim3(n), dim3(256), 0, sh, b.msgs, b.msg_off, dst, dlen, n, Q, skip);
+    else if (n && n <= TB_HASH_WAVE_MAX)  // one workgroup per set: the cofactor clearing lane-parallel
       hipLaunchKernelGGL(k_set_hash_wave, dim3(n), dim3(128), 0, sh, b.msgs, b.msg_off, dst, dlen, n, Q, skip);
     else if (n)
       hipLaunchKernelGGL(k_set_hash, g, blk, 0, sh, b.msgs, b.msg_off, dst, dlen, n, Q, skip);

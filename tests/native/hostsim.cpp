@@ -62,7 +62,7 @@ extern "C" int tbls_hostsim_coop_mul_digits(const int32_t* a, const int32_t* b, 
       x.v[j] = a[16 * k + j];
       y.v[j] = b[16 * k + j];
     }
-    const tb::coop::c32 r = tb::coop::cmul(x, y);
+    const tb::coop::c32 r = tb::coop::cmul(x, y, tb::coop::cctx_load());
     for (int j = 0; j < 16; j++) out[16 * k + j] = r.v[j];
   }
   return 0;
@@ -72,7 +72,7 @@ extern "C" int tbls_hostsim_coop_mul_digits(const int32_t* a, const int32_t* b, 
 extern "C" int tbls_hostsim_coop_mul_fp(const uint32_t* a, const uint32_t* b, uint32_t* out, size_t n) {
   for (size_t k = 0; k < n; k++) {
     const tb::coop::c32 x = tb::coop::cfrom_words(a + 12 * k), y = tb::coop::cfrom_words(b + 12 * k);
-    const tb::coop::c32 r = tb::coop::cmul(x, y);
+    const tb::coop::c32 r = tb::coop::cmul(x, y, tb::coop::cctx_load());
     const tb::fp f = tb::coop::cdigits_to_fp(r.v);
     for (int j = 0; j < 12; j++) out[12 * k + j] = f.l[j];
   }
@@ -93,7 +93,7 @@ extern "C" int tbls_hostsim_coop_sqrt_cand(const uint32_t* a, uint32_t* out, siz
   for (size_t k = 0; k + 1 < n + 1; k += 2) {
     const size_t k1 = k + 1 < n ? k + 1 : k;
     tb::coop::c32 x[2] = {tb::coop::cfrom_words(a + 12 * k), tb::coop::cfrom_words(a + 12 * k1)}, r[2];
-    tb::coop::cpow_win_n<2>(r, x, tb::EXPW_SQRT_FIRST, tb::EXPW_SQRT, tb::EXPW_SQRT_N);
+    tb::coop::cpow_win_n<2>(r, x, tb::EXPW_SQRT_FIRST, tb::EXPW_SQRT, tb::EXPW_SQRT_N, tb::coop::cctx_load());
     const tb::fp f0 = tb::coop::cdigits_to_fp(r[0].v), f1 = tb::coop::cdigits_to_fp(r[1].v);
     for (int j = 0; j < 12; j++) {
       out[12 * k + j] = f0.l[j];
@@ -108,7 +108,7 @@ extern "C" int tbls_hostsim_coop_reduce(const int64_t* x, int32_t* out, size_t n
   for (size_t k = 0; k < n; k++) {
     tb::coop::c64 v;
     for (int j = 0; j < 16; j++) v.v[j] = x[16 * k + j];
-    const tb::coop::c32 r = tb::coop::creduce64(v);
+    const tb::coop::c32 r = tb::coop::creduce64(v, tb::coop::cctx_load().plo[0]);
     for (int j = 0; j < 16; j++) out[16 * k + j] = r.v[j];
   }
   return 0;

@@ -34,6 +34,7 @@ __device__ coop::c32 coop_row_from_fp(const fp& v, uint32_t (*lds)[12]) {
 extern "C" __global__ void __launch_bounds__(64) k_test_coop_mul(const uint8_t* in, uint8_t* out, uint32_t n) {
   __shared__ uint32_t W[4][12];
   __shared__ int32_t D[4][16];
+  const coop::cctx K = coop::cctx_load();
   const uint32_t rec = blockIdx.x * 4 + (threadIdx.x >> 4);
   const bool live = rec < n;
   const uint8_t* r = in + (size_t)(live ? rec : 0) * TB_TEST_IN;
@@ -43,7 +44,7 @@ extern "C" __global__ void __launch_bounds__(64) k_test_coop_mul(const uint8_t* 
     b = tio_fp(r + 48);
   }
   const coop::c32 x = coop_row_from_fp(a, W), y = coop_row_from_fp(b, W);
-  const fp z = coop_row_to_fp(coop::cmul(x, y), D);
+  const fp z = coop_row_to_fp(coop::cmul(x, y, K), D);
   if (live && (threadIdx.x & 15) == 0) tio_put_fp(out + (size_t)rec * TB_TEST_OUT, z);
 }
 
@@ -58,16 +59,17 @@ extern "C" __global__ void __launch_bounds__(64) k_test_coop_timing(const uint8_
     a = tio_fp(in);
     b = tio_fp(in + 48);
   }
+  const coop::cctx K = coop::cctx_load();
   coop::c32 x = coop_row_from_fp(a, W), y = coop_row_from_fp(b, W);
   const coop::c32 x0 = x, y0 = y;
   const long long t0 = clock64();
-  TB_NOUNROLL for (int k = 0; k < 64; k++) x = coop::cmul(x, y0);
+  TB_NOUNROLL for (int k = 0; k < 64; k++) x = coop::cmul(x, y0, K);
   __syncthreads();
   const long long t1 = clock64();
   coop::c32 u = x0, v = y0;
   TB_NOUNROLL for (int k = 0; k < 64; k++) {
-    u = coop::cmul(u, y0);
-    v = coop::cmul(v, x0);
+    u = coop::cmul(u, y0, K);
+    v = coop::cmul(v, x0, K);
   }
   __syncthreads();
   const long long t2 = clock64();
@@ -94,11 +96,14 @@ extern "C" __global__ void __launch_bounds__(64) k_test_coop_timing(const uint8_
 extern "C" __global__ void __launch_bounds__(CFE_THREADS) k_test_final_exp_coop(const uint8_t* in, uint8_t* out) {
   __shared__ cfe_lds L;
   cfe::init(L);
+  cfe_regs R;
+  cfe::regs_load(R, L);
+  const coop::cctx& K = R.K;
   if (threadIdx.x == 0) fp12_to_coords(L.tmp, tio_fp12(in + (size_t)blockIdx.x * TB_TEST_IN));
   __syncthreads();
   cfe::load_coords(L.F, L.tmp);
   const long long t0 = clock64();
-  cfe::final_exp(L);
+  cfe::final_exp(L, R);
   const long long t1 = clock64();
   cfe::store_coords(L.F, L);
   if (threadIdx.x == 0) {
@@ -116,6 +121,9 @@ extern "C" __global__ void __launch_bounds__(256) k_test_cfe_ops(const uint8_t* 
   __shared__ cfe_lds L;
   const uint8_t* r = in + (size_t)blockIdx.x * TB_TEST_IN;
   cfe::init(L);
+  cfe_regs R;
+  cfe::regs_load(R, L);
+  const coop::cctx& K = R.K;
   const uint32_t op = *reinterpret_cast<const uint32_t*>(r + 1152);
   if (threadIdx.x == 0) fp12_to_coords(L.tmp, tio_fp12(r));
   __syncthreads();
@@ -123,16 +131,16 @@ extern "C" __global__ void __launch_bounds__(256) k_test_cfe_ops(const uint8_t* 
   if (threadIdx.x == 0) fp12_to_coords(L.tmp, tio_fp12(r + 576));
   __syncthreads();
   cfe::load_coords(L.X, L.tmp);
-  if (op == 0) cfe::mul(L.T, L.F, L.X, L);
-  else if (op == 1) cfe::cyc_sqr(L.T, L.F, L);
-  else if (op == 2) cfe::frob(L.T, L.F, L);
+  if (op == 0) cfe::mul(L.T, L.F, L.X, L, R);
+  else if (op == 1) cfe::cyc_sqr(L.T, L.F, L, R);
+  else if (op == 2) cfe::frob(L.T, L.F, L, R);
   else if (op == 3) cfe::conj(L.T, L.F);
   else if (op == 5) {  // the coop Fp12 inversion
-    cfe::inv(L.T, L.F, L);
+    cfe::inv(L.T, L.F, L, R);
   } else if (op == 6) {  // t^x
-    cfe::cyc_exp_x(L.T, L.F, L);
+    cfe::cyc_exp_x(L.T, L.F, L, R);
   } else if (op == 7) {  // full
-    cfe::final_exp(L);
+    cfe::final_exp(L, R);
     cfe::copy(L.T, L.F);
   } else
     cfe::copy(L.T, L.F);
@@ -140,11 +148,11 @@ extern "C" __global__ void __launch_bounds__(256) k_test_cfe_ops(const uint8_t* 
   long long c[4] = {0, 0, 0, 0};
   if (op == 8) {
     c[0] = clock64();
-    for (int k = 0; k < 64; k++) cfe::cyc_sqr(L.A, L.A, L);
+    for (int k = 0; k < 64; k++) cfe::cyc_sqr(L.A, L.A, L, R);
     c[1] = clock64();
-    for (int k = 0; k < 64; k++) cfe::mul(L.B, L.B, L.F, L);
+    for (int k = 0; k < 64; k++) cfe::mul(L.B, L.B, L.F, L, R);
     c[2] = clock64();
-    cfe::inv(L.C, L.F, L);
+    cfe::inv(L.C, L.F, L, R);
     c[3] = clock64();
   }
   cfe::store_coords(L.T, L);
