@@ -15,6 +15,7 @@
 // sums below 2^395 (the generators cap sum |coef| of an operand at 4096).
 #pragma once
 #include "tb_coop.h"
+#include "tb_cpoint.h"
 #include "tb_fp12_wave.h"
 
 namespace tb {
@@ -29,14 +30,11 @@ using coop::cctx;
 __device__ TB_INLINE int row() { return (int)(threadIdx.x >> 4); }
 __device__ TB_INLINE int dig() { return (int)(threadIdx.x & 15u); }
 
-struct c2 {
-  c32 c0, c1;
-};
-
-__device__ TB_INLINE c2 add(const c2& a, const c2& b) { return {a.c0 + b.c0, a.c1 + b.c1}; }
-__device__ TB_INLINE c2 sub(const c2& a, const c2& b) { return {a.c0 - b.c0, a.c1 - b.c1}; }
-__device__ TB_INLINE c2 neg(const c2& a) { return {-a.c0, -a.c1}; }
-__device__ TB_INLINE c2 norm(const c2& a) { return {coop::cnorm(a.c0), coop::cnorm(a.c1)}; }
+using coop::add;
+using coop::c2;
+using coop::neg;
+using coop::norm;
+using coop::sub;
 __device__ TB_INLINE c2 reduce(const c2& a, const cctx& K) {
   return {coop::creduce64((c64)a.c0, K.plo[0]), coop::creduce64((c64)a.c1, K.plo[0])};
 }

@@ -260,6 +260,22 @@ static bool hash_coop() {
   static const bool v = !(getenv("TBLS_HASH_COOP") && getenv("TBLS_HASH_COOP")[0] == '0');
   return v;
 }
+extern "C" __global__ void k_keys_coop(const uint8_t* __restrict__ pks, const uint32_t* __restrict__ pk_off, const g1a* __restrict__ tab_aff,
+                                       const uint8_t* __restrict__ tab_code, const uint32_t* __restrict__ key_idx, uint32_t tab_n,
+                                       const uint64_t* __restrict__ rand, uint32_t n, g1a* __restrict__ P, g1a* __restrict__ P2,
+                                       uint8_t* __restrict__ set_code, uint32_t* __restrict__ n_bad, const g1a* __restrict__ comb);
+extern "C" __global__ void k_sig_check_coop(const uint8_t* __restrict__ sigs, uint32_t n, g2a* __restrict__ sig_aff, uint8_t* __restrict__ sig_use,
+                                            uint8_t* __restrict__ sig_code, uint32_t* __restrict__ n_bad);  // k_kcoop.hip
+// small batches: lane-cooperative key and signature stages (k_kcoop.hip);
+// TBLS_KEYS_COOP=0 / TBLS_SIG_COOP=0 select the one-thread-per-item kernels (A/B)
+static bool keys_coop() {
+  static const bool v = !(getenv("TBLS_KEYS_COOP") && getenv("TBLS_KEYS_COOP")[0] == '0');
+  return v;
+}
+static bool sig_coop() {
+  static const bool v = !(getenv("TBLS_SIG_COOP") && getenv("TBLS_SIG_COOP")[0] == '0');
+  return v;
+}
 
 int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* partial_out, ws_layout& L,
                    const uint8_t* dst, uint32_t dlen, hipEvent_t* ev = nullptr, bool serial_req = false,
@@ -335,6 +351,9 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
     if (pp.msm)
       hipLaunchKernelGGL(k_sig_check, g, blk, 0, ssig, b.sigs, n, (g2a*)(w + L.sig_aff), w + L.sig_use, w + L.sig_code,
                          (uint32_t*)(w + L.n_bad), 0u);
+    else if (n <= TB_HASH_WAVE_MAX && sig_coop())  // the same, 4 sets per wave, lane-cooperative
+      hipLaunchKernelGGL(k_sig_check_coop, dim3((n + 3) / 4), dim3(64), 0, ssig, b.sigs, n, (g2a*)(Q + n), skip + n, w + L.sig_code,
+                         (uint32_t*)(w + L.n_bad));
     else  // the set's signature pair: Q[n + i] = sig_i, skip[n + i] = infinite / invalid
       hipLaunchKernelGGL(k_sig_check, g, blk, 0, ssig, b.sigs, n, Q + n, skip + n, w + L.sig_code, (uint32_t*)(w + L.n_bad), 1u);
   }
@@ -367,13 +386,26 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
   HIPCHK(hipEventRecord(c.e_join[1], sb));
   // --- stream a: public keys, [r] apk (+ -[r] g1 for the signature pairs) -----
   TB_EV(0, sa);
-  if (K) hipLaunchKernelGGL(k_pk_decompress, dim3((K + TB_BLOCK - 1) / TB_BLOCK), blk, 0, sa, b.pks, K, (g1a*)(w + L.pk_aff), w + L.pk_code);
-  TB_EV(1, sa);
-  TB_EV(2, sa);
-  launch_set_pk(sa, n, b.n_keys, b.pk_off, use_tab ? c.tab_aff.as<const g1a>() : (const g1a*)(w + L.pk_aff),
-                use_tab ? c.tab_code.as<const uint8_t>() : (const uint8_t*)(w + L.pk_code), b.rand, P, w + L.set_code,
-                (uint32_t*)(w + L.n_bad), key_idx, use_tab ? c.tab_n : 0u, (uint32_t*)(w + L.mlist), (uint32_t*)(w + L.mcnt),
-                pp.msm ? nullptr : P + n, c.comb.as<const g1a>());
+  if (b.n_keys == n && n && n <= TB_HASH_WAVE_MAX && keys_coop()) {
+    // one kernel: decode + G1 check (wave 0) beside -[r] g1, then [r] pk (wave
+    // 1); its time shows as stage 0.  As many keys as sets: one key per set
+    // in every real batch (a set of several keys beside empty ones still
+    // verifies correctly, on one lane).
+    hipLaunchKernelGGL(k_keys_coop, dim3((n + 3) / 4), dim3(128), 0, sa, use_tab ? nullptr : b.pks, b.pk_off,
+                       use_tab ? c.tab_aff.as<const g1a>() : nullptr, use_tab ? c.tab_code.as<const uint8_t>() : nullptr, key_idx,
+                       use_tab ? c.tab_n : 0u, b.rand, n, P, pp.msm ? nullptr : P + n, w + L.set_code, (uint32_t*)(w + L.n_bad),
+                       c.comb.as<const g1a>());
+    TB_EV(1, sa);
+    TB_EV(2, sa);
+  } else {
+    if (K) hipLaunchKernelGGL(k_pk_decompress, dim3((K + TB_BLOCK - 1) / TB_BLOCK), blk, 0, sa, b.pks, K, (g1a*)(w + L.pk_aff), w + L.pk_code);
+    TB_EV(1, sa);
+    TB_EV(2, sa);
+    launch_set_pk(sa, n, b.n_keys, b.pk_off, use_tab ? c.tab_aff.as<const g1a>() : (const g1a*)(w + L.pk_aff),
+                  use_tab ? c.tab_code.as<const uint8_t>() : (const uint8_t*)(w + L.pk_code), b.rand, P, w + L.set_code,
+                  (uint32_t*)(w + L.n_bad), key_idx, use_tab ? c.tab_n : 0u, (uint32_t*)(w + L.mlist), (uint32_t*)(w + L.mcnt),
+                  pp.msm ? nullptr : P + n, c.comb.as<const g1a>());
+  }
   TB_EV(3, sa);
   HIPCHK(hipEventRecord(c.e_join[0], sa));
   // --- high-priority stream: hash_to_G2 per set -------------------------------

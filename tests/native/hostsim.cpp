@@ -113,3 +113,61 @@ extern "C" int tbls_hostsim_coop_reduce(const int64_t* x, int32_t* out, size_t n
   }
   return 0;
 }
+
+// ---- lane-cooperative point arithmetic (tb_cpoint.h) -----------------------
+#include "../../teku_amd/csrc/tb_cpoint.h"
+
+// G1: in = n x (x1, y1, x2, y2) Montgomery words (12 each); out = n x (X, Y, Z)
+// op 0: dbl(P1)  1: madd(dbl(P1), P2)  2: add(dbl(P1), dbl(P2))  3: [k] P1
+// (mul_u64_aff)  4: [k] dbl(P1) (mul_u64)  5: [k]([k] P1)
+extern "C" int tbls_hostsim_cpoint_g1(int op, const uint32_t* in, uint32_t* out, size_t n, uint64_t k) {
+  using namespace tb::coop;
+  const cctx K = cctx_load();
+  const c32 one = cfrom_words(tb::R1);
+  for (size_t i = 0; i < n; i++) {
+    const uint32_t* w = in + 48 * i;
+    const c32 x1 = cfrom_words(w), y1 = cfrom_words(w + 12), x2 = cfrom_words(w + 24), y2 = cfrom_words(w + 36);
+    const cj1 p1 = {x1, y1, one}, p2 = {x2, y2, one};
+    cj1 r;
+    switch (op) {
+      case 0: r = dbl(p1, K); break;
+      case 1: r = madd(dbl(p1, K), x2, y2, K); break;
+      case 2: r = add(dbl(p1, K), dbl(p2, K), K); break;
+      case 3: r = mul_u64_aff(x1, y1, k, one, K); break;
+      case 4: r = mul_u64(dbl(p1, K), k, K); break;
+      default: r = mul_u64(mul_u64_aff(x1, y1, k, one, K), k, K); break;
+    }
+    const c32* c[3] = {&r.x, &r.y, &r.z};
+    for (int j = 0; j < 3; j++) {
+      const tb::fp f = cdigits_to_fp(c[j]->v);
+      for (int q = 0; q < 12; q++) out[36 * i + 12 * j + q] = f.l[q];
+    }
+  }
+  return 0;
+}
+
+// G2: in = n x (x1, y1, x2, y2) as Fp2 (c0, c1) Montgomery words; out = n x (X, Y, Z)
+// op 0: dbl(P1)  1: madd(dbl(P1), P2)  3: [k] P1 (mul_u64_aff)
+extern "C" int tbls_hostsim_cpoint_g2(int op, const uint32_t* in, uint32_t* out, size_t n, uint64_t k) {
+  using namespace tb::coop;
+  const cctx K = cctx_load();
+  const c2 one = {cfrom_words(tb::R1), c32(0)};
+  for (size_t i = 0; i < n; i++) {
+    const uint32_t* w = in + 96 * i;
+    c2 v[4];
+    for (int j = 0; j < 4; j++) v[j] = {cfrom_words(w + 24 * j), cfrom_words(w + 24 * j + 12)};
+    const cj2 p1 = {v[0], v[1], one};
+    cj2 r;
+    switch (op) {
+      case 0: r = dbl(p1, K); break;
+      case 1: r = madd(dbl(p1, K), v[2], v[3], K); break;
+      default: r = mul_u64_aff(v[0], v[1], k, one, K); break;
+    }
+    const c32* c[6] = {&r.x.c0, &r.x.c1, &r.y.c0, &r.y.c1, &r.z.c0, &r.z.c1};
+    for (int j = 0; j < 6; j++) {
+      const tb::fp f = cdigits_to_fp(c[j]->v);
+      for (int q = 0; q < 12; q++) out[72 * i + 12 * j + q] = f.l[q];
+    }
+  }
+  return 0;
+}

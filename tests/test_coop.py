@@ -159,3 +159,72 @@ def test_coop_reduce(lib):
         assert all(abs(int(v)) <= (1 << 28) + (1 << 12) for v in r[:13])
         assert abs(val(r)) < 1.6 * P
         assert (val(r) - val(a)) % P == 0
+
+
+# ---- point arithmetic (tb_cpoint.h) -----------------------------------------
+def _words(v):
+    return [(v >> (32 * i)) & 0xFFFFFFFF for i in range(12)]
+
+
+def _mont(v):
+    return v * R % P
+
+
+def _unwords(ws):
+    return sum(int(w) << (32 * i) for i, w in enumerate(ws)) * RINV % P
+
+
+def _g1_points(rng, k):
+    return [O.jac_to_affine(O.FP, O.jac_mul(O.FP, O.jac_from_affine(O.FP, O.G1_GEN), rng.randrange(1, O.R))) for _ in range(k)]
+
+
+def _g2_points(rng, k):
+    return [O.jac_to_affine(O.FP2, O.jac_mul(O.FP2, O.jac_from_affine(O.FP2, O.G2_GEN), rng.randrange(1, O.R))) for _ in range(k)]
+
+
+def _eq_jac(F, got, exp_aff):
+    return O.jac_to_affine(F, got) == exp_aff
+
+
+@pytest.mark.parametrize("op", [0, 1, 2, 3, 4, 5])
+def test_cpoint_g1(lib, op):
+    lib.tbls_hostsim_cpoint_g1.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64]
+    rng = random.Random(100 + op)
+    n = 6
+    A, B = _g1_points(rng, n), _g1_points(rng, n)
+    k = O.X_ABS if op == 5 else rng.getrandbits(64) | (1 << 63)
+    inp = np.array([w for a, b in zip(A, B) for v in (a[0], a[1], b[0], b[1]) for w in _words(_mont(v))], dtype=np.uint32)
+    out = np.zeros(36 * n, dtype=np.uint32)
+    lib.tbls_hostsim_cpoint_g1(op, inp.ctypes.data, out.ctypes.data, n, k)
+    F = O.FP
+    for i, (a, b) in enumerate(zip(A, B)):
+        ja, jb = O.jac_from_affine(F, a), O.jac_from_affine(F, b)
+        exp = {
+            0: lambda: O.jac_double(F, ja),
+            1: lambda: O.jac_add(F, O.jac_double(F, ja), jb),
+            2: lambda: O.jac_add(F, O.jac_double(F, ja), O.jac_double(F, jb)),
+            3: lambda: O.jac_mul(F, ja, k),
+            4: lambda: O.jac_mul(F, O.jac_double(F, ja), k),
+            5: lambda: O.jac_mul(F, ja, k * k),
+        }[op]()
+        got = tuple(_unwords(out[36 * i + 12 * j : 36 * i + 12 * j + 12]) for j in range(3))
+        assert _eq_jac(F, got, O.jac_to_affine(F, exp)), (op, i)
+
+
+@pytest.mark.parametrize("op", [0, 1, 3])
+def test_cpoint_g2(lib, op):
+    lib.tbls_hostsim_cpoint_g2.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64]
+    rng = random.Random(200 + op)
+    n = 3
+    A, B = _g2_points(rng, n), _g2_points(rng, n)
+    k = O.X_ABS if op == 3 else 0
+    inp = np.array([w for a, b in zip(A, B) for v in (a[0], a[1], b[0], b[1]) for c in v for w in _words(_mont(c))], dtype=np.uint32)
+    out = np.zeros(72 * n, dtype=np.uint32)
+    lib.tbls_hostsim_cpoint_g2(op, inp.ctypes.data, out.ctypes.data, n, k)
+    F = O.FP2
+    for i, (a, b) in enumerate(zip(A, B)):
+        ja, jb = O.jac_from_affine(F, a), O.jac_from_affine(F, b)
+        exp = {0: lambda: O.jac_double(F, ja), 1: lambda: O.jac_add(F, O.jac_double(F, ja), jb), 3: lambda: O.jac_mul(F, ja, k)}[op]()
+        c = [_unwords(out[72 * i + 12 * j : 72 * i + 12 * j + 12]) for j in range(6)]
+        got = ((c[0], c[1]), (c[2], c[3]), (c[4], c[5]))
+        assert _eq_jac(F, got, O.jac_to_affine(F, exp)), (op, i)
