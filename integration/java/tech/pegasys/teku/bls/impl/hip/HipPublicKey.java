@@ -1,0 +1,114 @@
+/*
+ * PublicKey (impl/PublicKey.java) over the compressed bytes; validity
+ * (!infinity && in G1) computed on the device and memoised, as
+ * BlstPublicKey.java:74-75.  Mirror: teku_amd/bls.py HipPublicKey.
+ */
+package tech.pegasys.teku.bls.impl.hip;
+
+import java.util.Arrays;
+import java.util.List;
+import org.apache.tuweni.bytes.Bytes48;
+import tech.pegasys.teku.bls.impl.BlsException;
+import tech.pegasys.teku.bls.impl.PublicKey;
+
+final class HipPublicKey implements PublicKey {
+  static final byte[] INFINITY = infinity(48);
+
+  private final byte[] bytes;
+  private volatile Boolean valid;
+
+  HipPublicKey(final byte[] compressed, final Integer checkedCode) {
+    this.bytes = compressed.clone();
+    this.valid = checkedCode == null ? null : checkedCode == TekuBlsHip.SUCCESS;
+  }
+
+  static byte[] infinity(final int n) {
+    final byte[] b = new byte[n];
+    b[0] = (byte) 0xc0;
+    return b;
+  }
+
+  /* BlstPublicKey.fromBytes: decode failures throw (BlstPublicKey.java:38-45) */
+  static HipPublicKey fromBytes(final Bytes48 compressed) {
+    final byte[] b = compressed.toArrayUnsafe();
+    final int code = TekuBlsHip.pkValidate(b);
+    if (code == TekuBlsHip.BAD_ENCODING || code == TekuBlsHip.POINT_NOT_ON_CURVE) {
+      throw new BlsException("Deserialization of public key bytes failed: " + compressed);
+    }
+    if (code == TekuBlsHip.DEVICE_ERROR) {
+      throw new BlsException("GPU BLS backend: device error");
+    }
+    return new HipPublicKey(b, code);
+  }
+
+  static HipPublicKey fromPublicKey(final PublicKey pk) {
+    if (pk instanceof HipPublicKey h) {
+      return h;
+    }
+    return fromBytes(pk.toBytesCompressed());
+  }
+
+  static HipPublicKey aggregate(final List<HipPublicKey> keys) {
+    if (keys.isEmpty()) {
+      throw new IllegalArgumentException("empty public key list"); // BlstPublicKey.java:56
+    }
+    final byte[] blob = new byte[48 * keys.size()];
+    for (int i = 0; i < keys.size(); i++) {
+      System.arraycopy(keys.get(i).bytes, 0, blob, 48 * i, 48);
+    }
+    final byte[] out = new byte[48];
+    final int rc = TekuBlsHip.aggregatePks(blob, keys.size(), out);
+    if (rc == TekuBlsHip.BAD_ENCODING || rc == TekuBlsHip.POINT_NOT_ON_CURVE) {
+      throw new BlsException("Deserialization of public key bytes failed");
+    }
+    if (rc != TekuBlsHip.SUCCESS) {
+      throw new BlsException("GPU BLS backend: aggregate failed, code " + rc);
+    }
+    return new HipPublicKey(out, null);
+  }
+
+  byte[] raw() {
+    return bytes;
+  }
+
+  boolean isInfinity() {
+    return Arrays.equals(bytes, INFINITY);
+  }
+
+  @Override
+  public Bytes48 toBytesCompressed() {
+    return Bytes48.wrap(bytes.clone());
+  }
+
+  @Override
+  public void forceValidation() throws IllegalArgumentException {
+    if (!isValid()) {
+      throw new IllegalArgumentException("Invalid PublicKey: " + toBytesCompressed());
+    }
+  }
+
+  @Override
+  public boolean isInGroup() {
+    return isInfinity() || isValid();
+  }
+
+  @Override
+  public boolean isValid() {
+    Boolean v = valid;
+    if (v == null) {
+      v = TekuBlsHip.pkValidate(bytes) == TekuBlsHip.SUCCESS;
+      valid = v;
+    }
+    return v;
+  }
+
+  @Override
+  public int hashCode() {
+    return Arrays.hashCode(bytes);
+  }
+
+  @Override
+  public boolean equals(final Object obj) {
+    return obj instanceof HipPublicKey o && Arrays.equals(o.bytes, bytes);
+  }
+}
