@@ -333,3 +333,143 @@ extern "C" __global__ void __launch_bounds__(64)
     if (code != TB_SUCCESS) atomicAdd(n_bad, 1u);
   }
 }
+
+// ---------------------------------------------------------------------------
+// Multi-key sets (configs 2/3: 488-512 keys per set; BlstPublicKey.aggregate,
+// BlstPublicKey.java:55-71), lane-cooperative: one 256-thread workgroup (16
+// rows) per set of the compacted list.  Row q sums the set's keys q, q + 16,
+// ... with coop mixed additions, the 16 row sums meet in a 4-level LDS tree of
+// coop general additions, and row 0 forms P = [r] apk (coop, Jacobian input)
+// with one lane-0 inversion.  The coop additions have no exceptional-case
+// branches: a sum that meets P == +-Q (a repeated key, or keys cancelling)
+// ends with Z = 0 and stays there through every later addition, so Z = 0 of
+// the aggregate sends the set to lane 0's one-lane body (stage_set_pk: exact,
+// and infinity -> PK_IS_INFINITY).  For a finite aggregate of group points no
+// multiple [k] apk, 2 <= k < 2^64, meets +-apk (tb_ccurve.h), so [r] apk is
+// exact.  Same outputs as k_set_pk_wave.
+// ---------------------------------------------------------------------------
+struct ka_set {
+  int32_t pt[16][3][16];  // row sums (X, Y, Z digits)
+  uint32_t inf[16];
+  int32_t zb[4][16];
+  fp inv;
+  fp out[2];
+  int bad;
+};
+
+__device__ TB_NOINLINE int ka_set_generic(const g1a* pk_aff, const uint8_t* pk_code, uint32_t b, uint32_t e, uint64_t r, g1a& o,
+                                          const uint32_t* key_idx, uint32_t tab_n) {
+  return stage_set_pk(pk_aff, pk_code, b, e, r, o, key_idx, tab_n);
+}
+
+extern "C" __global__ void __launch_bounds__(256)
+    k_set_pk_agg_coop(const uint32_t* __restrict__ pk_off, const g1a* __restrict__ pk_aff, const uint8_t* __restrict__ pk_code,
+                      const uint64_t* __restrict__ rand, const uint32_t* __restrict__ list, const uint32_t* __restrict__ cnt,
+                      g1a* __restrict__ P, uint8_t* __restrict__ set_code, uint32_t* __restrict__ n_bad,
+                      const uint32_t* __restrict__ key_idx, uint32_t tab_n) {
+  __shared__ ka_set S;
+  tb_latency_prio();
+  const int q = crow::row(), d = crow::dig();
+  const coop::cctx K = coop::cctx_load();
+  const c32 one = crow::from_const(R1);
+  const uint32_t total = cnt[0];
+  for (uint32_t w = blockIdx.x; w < total; w += gridDim.x) {
+    const uint32_t i = list[w], b = pk_off[i], e = pk_off[i + 1];
+    if (threadIdx.x == 0) S.bad = TB_SUCCESS;
+    __syncthreads();
+    // ---- row sums (row-uniform control flow: every lane of a row walks the same keys)
+    coop::cj1 acc = {c32(0), c32(0), c32(0)};
+    bool inf = true;
+    for (uint32_t j = b + (uint32_t)q; j < e; j += 16) {
+      uint32_t k;
+      if (!set_key(key_idx, tab_n, j, k)) {
+        S.bad = TB_BAD_ENCODING;
+      } else if (pk_code[k] != TB_SUCCESS) {
+        S.bad = TB_PK_IS_INFINITY;  // BlstPublicKey.java:58-65 (any racing writer stores a failure)
+      } else {
+        const c32 qx = crow::from_fp(pk_aff[k].x), qy = crow::from_fp(pk_aff[k].y);
+        if (inf) {
+          acc = {qx, qy, one};
+          inf = false;
+        } else {
+          acc = coop::madd(acc, qx, qy, K);
+        }
+      }
+    }
+    S.pt[q][0][d] = acc.x;
+    S.pt[q][1][d] = acc.y;
+    S.pt[q][2][d] = acc.z;
+    if (d == 0) S.inf[q] = inf ? 1u : 0u;
+    __syncthreads();
+    // ---- 4-level tree over the rows
+    for (int s = 8; s > 0; s >>= 1) {
+      if (q < s) {
+        const bool pi = S.inf[q] != 0, qi = S.inf[q + s] != 0;
+        if (!qi) {
+          const coop::cj1 o = {S.pt[q + s][0][d], S.pt[q + s][1][d], S.pt[q + s][2][d]};
+          if (!pi) {
+            const coop::cj1 m = {S.pt[q][0][d], S.pt[q][1][d], S.pt[q][2][d]};
+            acc = coop::add(m, o, K);
+          } else {
+            acc = o;
+          }
+        }
+      }
+      __syncthreads();
+      if (q < s && S.inf[q + s] == 0) {
+        S.pt[q][0][d] = acc.x;
+        S.pt[q][1][d] = acc.y;
+        S.pt[q][2][d] = acc.z;
+        if (d == 0) S.inf[q] = 0u;
+      }
+      __syncthreads();
+    }
+    // ---- row 0: the aggregate, [r] apk, affine
+    if (q == 0) {
+      const coop::cj1 apk = {S.pt[0][0][d], S.pt[0][1][d], S.pt[0][2][d]};
+      const c32 zv[1] = {apk.z};
+      const bool zero = S.inf[0] != 0 || crow::zeros_n<1>(zv, S.zb) != 0u;
+      const uint64_t rnd = rand[i];
+      int code = S.bad;
+      if (code == TB_SUCCESS && zero) {
+        // infinity or an exceptional addition: the exact one-lane body
+        if (d == 0) {
+          g1a o;
+          code = ka_set_generic(pk_aff, pk_code, b, e, rnd, o, key_idx, tab_n);
+          S.out[0] = o.x;
+          S.out[1] = o.y;
+        }
+      } else if (code == TB_SUCCESS && rnd == 0) {
+        code = TB_PK_IS_INFINITY;  // [0] apk (stage_set_pk_finish)
+      } else if (code == TB_SUCCESS) {
+        const coop::cj1 t = coop::mul_u64(apk, rnd, K);
+        const c32 v1[1] = {t.z};
+        crow::to_fp_n<1>(v1, S.zb, &S.inv);
+        if (d == 0) S.inv = fp_inv(S.inv);
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        const c32 i1 = crow::from_fp(S.inv);
+        const c32 i2 = coop::csqr(i1, K);
+        c32 a3[2] = {t.x, i2}, b3[2] = {i2, i1}, i3[2];
+        coop::cmul_n<2>(i3, a3, b3, K);  // X / Z^2, 1 / Z^3
+        const c32 y = coop::cmul(t.y, i3[1], K);
+        const c32 v2[2] = {i3[0], y};
+        crow::to_fp_n<2>(v2, S.zb, S.out);
+      }
+      if (d == 0) {  // lane 0's code is the set's in every branch
+        g1a o;
+        o.x = fp_zero();
+        o.y = fp_zero();
+        if (code == TB_SUCCESS) {
+          o.x = S.out[0];
+          o.y = S.out[1];
+        } else {
+          set_code[i] = (uint8_t)code;
+          atomicAdd(n_bad, 1u);
+        }
+        P[i] = o;
+      }
+    }
+    __syncthreads();
+  }
+}

@@ -30,8 +30,10 @@
 //   k_kzg_quotient (+ k_kzg_quotient_domain), k_kzg_lincomb_terms,
 //   k_kzg_lincomb_reduce: g1_lincomb over the bit-reversed Lagrange points.
 #include "tb_kzg_decl.h"
+#include "tb_ccurve.h"
 
 using namespace tb;
+using coop::c32;
 
 #define KZG_N 4096u
 #define KZG_BLOB_BYTES (32u * KZG_N)
@@ -391,6 +393,220 @@ extern "C" __global__ void __launch_bounds__(TB_BLOCK) k_kzg_terms(const g1a* __
   fr s = fr_pow_u32(rr, i);
   if (k >= 2u * n) s = fr_mul(s, z[i]);
   T[k] = inf[pi] ? jac_inf<fp>() : g1_mul_fr(pts[pi], s);
+}
+
+// ---------------------------------------------------------------------------
+// Lane-cooperative forms for the small host-API batches (1-6 blobs, the
+// per-block shape): one 16-lane row per point / term (tb_coop.h), where the
+// one-lane kernels above leave the chip idle and pay ~7,000 cycles per
+// dependent Fp product.
+// ---------------------------------------------------------------------------
+#define KZ_PENDING (-1)
+
+// hash_to_bls_field of host-computed challenge digests (tb_sha256_host.h):
+// z_i = int(digest_i) mod r, Montgomery
+extern "C" __global__ void __launch_bounds__(TB_BLOCK) k_kzg_z_from_digest(const uint8_t* __restrict__ dig, uint32_t n, fr* __restrict__ z) {
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= n) return;
+  uint32_t st[8];
+  TB_UNROLL for (int i = 0; i < 8; i++) {
+    const uint8_t* q = dig + 32u * (size_t)b + 4 * i;
+    st[i] = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | q[3];
+  }
+  z[b] = fr_from_digest(fr_plain_from_bewords(st));
+}
+
+struct kp_row {
+  int32_t zb[4][16];
+  fp x, y;
+  fp out[2];
+  int code;
+  uint32_t want, inf;
+};
+
+// k_kzg_points on one row per point (4 per 64-thread workgroup): the header
+// and x on lane 0 (g1_decompress), the square root and the G1 subgroup check
+// (tb_ccurve.h g1_in_group) on the row.  Same out / inf / code.
+extern "C" __global__ void __launch_bounds__(64) k_kzg_points_coop(const uint8_t* __restrict__ bytes, uint32_t m, g1a* __restrict__ out,
+                                                                   uint8_t* __restrict__ inf, uint8_t* __restrict__ code) {
+  __shared__ kp_row S[4];
+  tb_latency_prio();
+  const int r = (threadIdx.x >> 4) & 3, d = crow::dig();
+  const uint32_t i = blockIdx.x * 4 + r;
+  const bool act = i < m;
+  kp_row& M = S[r];
+  const coop::cctx K = coop::cctx_load();
+  if (d == 0) {
+    int c = TB_BAD_ENCODING;
+    fp x = fp_zero();
+    uint32_t want = 0, isinf = 0;
+    if (act) {
+      const uint8_t* b = bytes + 48u * (size_t)i;
+      const uint8_t b0 = b[0];
+      want = (b0 & 0x20) ? 1u : 0u;
+      if (!(b0 & 0x80)) {
+        c = TB_BAD_ENCODING;
+      } else if (b0 & 0x40) {
+        uint32_t acc = b0 & 0x3f;
+        for (int k = 1; k < 48; k++) acc |= b[k];
+        c = acc ? TB_BAD_ENCODING : TB_SUCCESS;
+        isinf = acc ? 0u : 1u;
+      } else {
+        fp v = fp_plain_from_be(b);
+        v.l[11] &= 0x1fffffffu;
+        if (!fp_plain_lt_p(v)) {
+          c = TB_BAD_ENCODING;
+        } else {
+          x = fp_to_mont(v);
+          c = KZ_PENDING;
+        }
+      }
+    }
+    M.x = x;
+    M.y = fp_zero();
+    M.code = c;
+    M.want = want;
+    M.inf = isinf;
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  {
+    const c32 x = crow::from_fp(M.x);
+    const c32 rhs = coop::cnorm(coop::cmul(coop::csqr(x, K), x, K) + crow::from_const(B_G1));
+    c32 a1[1] = {rhs}, y1[1];
+    coop::cpow_win_n<1>(y1, a1, EXPW_SQRT_FIRST, EXPW_SQRT, EXPW_SQRT_N, K);
+    const c32 v[2] = {coop::csqr(y1[0], K) - rhs, y1[0]};
+    crow::to_fp_n<2>(v, M.zb, M.out);
+  }
+  if (d == 0 && M.code == KZ_PENDING) {
+    if (!fp_is_zero(M.out[0])) {
+      M.code = TB_POINT_NOT_ON_CURVE;
+    } else {
+      const fp y = M.out[1];
+      M.y = fp_cneg(y, fp_sign_zcash(y) != (M.want != 0));
+      if (fp_is_zero(M.x)) M.code = TB_POINT_NOT_IN_GROUP;
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  // G1 check (rows without a pending point run on their values, ignored)
+  const bool ok = crow::g1_in_group(crow::from_fp(M.x), crow::from_fp(M.y), M.zb, K);
+  if (d == 0 && act) {
+    int c = M.code;
+    if (c == KZ_PENDING) c = ok ? TB_SUCCESS : TB_POINT_NOT_IN_GROUP;
+    g1a a;
+    a.x = M.x;
+    a.y = M.y;
+    out[i] = a;
+    inf[i] = (c == TB_SUCCESS && M.inf) ? 1 : 0;
+    code[i] = (uint8_t)c;
+  }
+}
+
+struct kt_row {
+  int32_t zb[4][16];
+  fp px, py, qx, qy;
+  fp out[3];
+  fr s;
+  uint32_t a[4], b[4];
+  uint32_t skip, pi;
+};
+
+// k_kzg_terms on one row per term (one 16-lane workgroup each, so no two
+// terms share a wave's control flow): lane 0 forms the scalar and the GLV
+// split, the row runs the joint 128-bit double-and-add with the coop
+// formulas (addend P, phi(-P) affine or their sum, all as general
+// additions after the selection) and writes the Jacobian term.  The coop
+// additions have no exceptional-case branches: an accumulator meeting +-the
+// addend ends with Z = 0 (sticky), and then lane 0 recomputes the term with the
+// exact one-lane g1_mul_fr (for the hash-derived scalars here this does not
+// happen in practice; the branch keeps the result exact regardless).
+extern "C" __global__ void __launch_bounds__(16) k_kzg_terms_coop(const g1a* __restrict__ pts, const uint8_t* __restrict__ inf,
+                                                                  const fr* __restrict__ z, const fr* __restrict__ y,
+                                                                  const fr* __restrict__ r, uint32_t n, g1j* __restrict__ T) {
+  __shared__ kt_row M;
+  tb_latency_prio();
+  const int d = crow::dig();
+  const uint32_t k = blockIdx.x;
+  if (k > 3u * n) return;
+  const coop::cctx K = coop::cctx_load();
+  if (d == 0) {
+    const fr rr = n > 1 ? r[0] : fr_one();
+    fr s;
+    g1a P;
+    uint32_t skip = 0, pi = 0;
+    if (k == 3u * n) {
+      fr acc = fr_zero(), rp = fr_one();
+      for (uint32_t i = 0; i < n; i++) {
+        acc = fr_add(acc, fr_mul(rp, y[i]));
+        rp = fr_mul(rp, rr);
+      }
+      s = acc;
+      P.x = fp_from_const(G1_X);
+      P.y = fp_from_const(G1_NEG_Y);
+      pi = 0xffffffffu;
+    } else {
+      const uint32_t i = k < n ? k : (k < 2u * n ? k - n : k - 2u * n);
+      pi = k >= n && k < 2u * n ? i : n + i;  // pts: commitments [0, n), proofs [n, 2n)
+      s = fr_pow_u32(rr, i);
+      if (k >= 2u * n) s = fr_mul(s, z[i]);
+      P = pts[pi];
+      skip = inf[pi] ? 1u : 0u;
+    }
+    uint32_t a[4], b[4];
+    glv_split(fr_from_mont(s), a, b);
+    TB_UNROLL for (int q = 0; q < 4; q++) {
+      M.a[q] = a[q];
+      M.b[q] = b[q];
+    }
+    M.s = s;
+    M.px = P.x;
+    M.py = P.y;
+    M.qx = fp_mul(P.x, fp_from_const(BETA));
+    M.qy = fp_neg(P.y);
+    M.skip = skip;
+    M.pi = pi;
+  }
+  __syncthreads();
+  if (M.skip) {  // the point at infinity
+    if (d == 0) T[k] = jac_inf<fp>();
+    return;
+  }
+  const c32 one = crow::from_const(R1);
+  const coop::cj1 Pj = {crow::from_fp(M.px), crow::from_fp(M.py), one};
+  const coop::cj1 Qj = {crow::from_fp(M.qx), crow::from_fp(M.qy), one};
+  const coop::cj1 Sj = coop::madd(Pj, Qj.x, Qj.y, K);  // P + [mu] P: never exceptional (1 +- mu != 0 mod r)
+  coop::cj1 acc = Pj;
+  bool ainf = true;
+  TB_NOUNROLL for (int i = 127; i >= 0; --i) {
+    if (!ainf) acc = coop::dbl(acc, K);
+    const bool ba = (M.a[i >> 5] >> (i & 31)) & 1u, bb = (M.b[i >> 5] >> (i & 31)) & 1u;
+    if (ba || bb) {
+      const coop::cj1 t = {ba ? (bb ? Sj.x : Pj.x) : Qj.x, ba ? (bb ? Sj.y : Pj.y) : Qj.y, ba ? (bb ? Sj.z : Pj.z) : Qj.z};
+      acc = ainf ? t : coop::add(acc, t, K);
+      ainf = false;
+    }
+  }
+  if (ainf) {  // scalar 0
+    if (d == 0) T[k] = jac_inf<fp>();
+    return;
+  }
+  const c32 v[3] = {acc.x, acc.y, acc.z};
+  crow::to_fp_n<3>(v, M.zb, M.out);
+  if (d == 0) {
+    if (fp_is_zero(M.out[2])) {  // an exceptional addition: the exact one-lane form
+      g1a P;
+      P.x = M.px;
+      P.y = M.py;
+      T[k] = g1_mul_fr(P, M.s);
+    } else {
+      g1j o;
+      o.x = M.out[0];
+      o.y = M.out[1];
+      o.z = M.out[2];
+      T[k] = o;
+    }
+  }
 }
 
 // A = sum T[0, n), B = sum T[n, 3n], as the two pairs of the check

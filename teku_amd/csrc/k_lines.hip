@@ -300,3 +300,78 @@ extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_MIN_WAVES)
                   uint32_t n_extra, fp12* __restrict__ f) {
   miller_acc_body<2, TB_SPREAD_EXTRA != 0>(lines, skip, code_a, code_b, n, xlines, xskip, n_extra, f);
 }
+
+// ---------------------------------------------------------------------------
+// Segmented accumulator.  The 68 steps of the loop split into nseg runs of
+// consecutive steps; thread (j, g) accumulates segment j's steps for the
+// `per` pairs of group g, starting from f = 1 (its first step's squaring is
+// skipped and its first line is taken as f), and writes conj(f) to
+// f_out[j * seg_stride + g_base + g].  The group's Miller value is
+//   f = prod_j f_j^(2^D_j),   D_j = doubling steps after segment j,
+// and squaring is a homomorphism, so the batch takes the product over groups
+// per segment first and pays the squarings once (Horner over the nseg
+// segment products, k_fp12_seg_combine_coop).  This decouples the squaring
+// share from occupancy: at 131,072 pairs, 8 pairs x 4 segments per thread keep
+// 1024 accumulator waves with one f^2 per 8 line products (k_miller_acc2: one
+// per 2), and at 32,768 pairs (config 4) 2 pairs x 4 segments fill the GPU
+// with a quarter of the loop per thread.
+// ---------------------------------------------------------------------------
+namespace {
+struct step_mask {
+  uint64_t lo, hi;
+};
+// bit s: step s is a doubling step (squaring of f), else an addition step
+constexpr step_mask miller_dbl_steps() {
+  step_mask m{0, 0};
+  int s = 0;
+  for (int b = 62; b >= 0; --b) {
+    if (s < 64)
+      m.lo |= 1ull << s;
+    else
+      m.hi |= 1ull << (s - 64);
+    s++;
+    if ((0xd201000000010000ull >> b) & 1) s++;
+  }
+  return m;
+}
+constexpr step_mask DBL_STEPS = miller_dbl_steps();
+
+__device__ TB_INLINE bool step_is_dbl(int s) { return ((s < 64 ? (DBL_STEPS.lo >> s) : (DBL_STEPS.hi >> (s - 64))) & 1ull) != 0; }
+
+// the line (A + B v) + (C v) w as an Fp12
+__device__ TB_INLINE fp12 line_fp12(const line3& l) { return {{l.a, l.b, fp2_zero()}, {fp2_zero(), l.c, fp2_zero()}}; }
+}  // namespace
+
+extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_MIN_WAVES)
+    k_miller_accs(const uint4* __restrict__ lines, const uint8_t* __restrict__ skip, const uint8_t* __restrict__ code_a,
+                  const uint8_t* __restrict__ code_b, uint32_t n, uint32_t per, uint32_t nseg, uint32_t g_pad, fp12* __restrict__ f_out,
+                  uint32_t seg_stride) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t j = t / g_pad, g = t % g_pad;
+  const uint32_t G = (n + per - 1) / per;
+  if (j >= nseg || g >= G) return;
+  const int s_lo = (int)(TB_LINE_STEPS * j / nseg), s_hi = (int)(TB_LINE_STEPS * (j + 1) / nseg);
+  const uint32_t i0 = per * g;
+  uint32_t usem = 0;
+  for (uint32_t k = 0; k < per; k++) {
+    const uint32_t i = i0 + k;
+    if (i < n && skip[i] == 0 && code_a[i] == 0 && code_b[i] == 0) usem |= 1u << k;
+  }
+  fp12 f = fp12_one();
+  bool fresh = true;  // f == 1
+  TB_NOUNROLL for (int s = s_lo; s < s_hi; s++) {
+    if (!fresh && step_is_dbl(s)) f = fp12_sqr_i(f);
+    TB_NOUNROLL for (uint32_t k = 0; k < per; k++) {
+      if ((usem >> k) & 1u) {
+        const line3 l = line_load(lines, n, i0 + k, s);
+        if (fresh) {
+          f = line_fp12(l);
+          fresh = false;
+        } else {
+          f = fp12_mul_by_line_i(f, l.a, l.b, l.c);
+        }
+      }
+    }
+  }
+  f_out[(size_t)j * seg_stride + g] = fp12_conj(f);
+}

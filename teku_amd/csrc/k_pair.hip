@@ -45,6 +45,52 @@ extern "C" __global__ void __launch_bounds__(64)
   w_store(out + blockIdx.x, L.A);
 }
 
+// The same over nseg segments at once (grid y = segment): segment y is
+// in[y * in_stride ..), n values (the last segment n_last: it also holds the
+// bit-sum pairs' Miller values), output out[y * out_stride + block].
+extern "C" __global__ void __launch_bounds__(64)
+    k_fp12_prod_wave_seg(const fp12* __restrict__ in, uint32_t n, uint32_t n_last, uint32_t nseg, uint32_t in_stride, uint32_t chunk,
+                         fp12* __restrict__ out, uint32_t out_stride) {
+  __shared__ prod_lds L;
+  tb_latency_prio();
+  const uint32_t y = blockIdx.y;
+  const uint32_t cnt = y + 1 == nseg ? n_last : n;
+  const fp12* src = in + (size_t)y * in_stride;
+  const uint32_t b = blockIdx.x * chunk;
+  uint32_t e = b + chunk;
+  if (e > cnt) e = cnt;
+  if (b >= e) return;
+  w12_tabs_load(L.s);
+  w_load(L.A, src + b);
+  for (uint32_t i = b + 1; i < e; i++) {
+    w_load(L.X, src + i);
+    w_mul(L.A, L.A, L.X, L.s);
+  }
+  w_store(out + (size_t)y * out_stride + blockIdx.x, L.A);
+}
+
+// Horner over the segment products of the segmented accumulator (k_lines.hip
+// k_miller_accs): R = v_0, then R = R^(2^d_j) v_j for j = 1 .. nseg - 1 (d_j =
+// doubling steps of segment j, byte j - 1 of dpack); one 256-thread coop
+// workgroup (tb_cfe.h products, general squaring as mul(x, x)).
+extern "C" __global__ void __launch_bounds__(CFE_THREADS)
+    k_fp12_seg_combine_coop(const fp12* __restrict__ vals, uint32_t nseg, uint32_t dpack, fp12* __restrict__ out) {
+  __shared__ cfe_lds L;
+  tb_latency_prio();
+  cfe::init(L);
+  cfe_regs R;
+  cfe::regs_load(R, L);
+  cfe::load_coords(L.F, reinterpret_cast<const fp*>(vals));
+  for (uint32_t j = 1; j < nseg; j++) {
+    const uint32_t d = (dpack >> (8 * (j - 1))) & 255u;
+    for (uint32_t k = 0; k < d; k++) cfe::mul(L.F, L.F, L.F, L, R);
+    cfe::load_coords(L.X, reinterpret_cast<const fp*>(vals + j));
+    cfe::mul(L.F, L.F, L.X, L, R);
+  }
+  cfe::store_coords(L.F, L);
+  if (threadIdx.x < 12) reinterpret_cast<fp*>(out)[threadIdx.x] = L.tmp[threadIdx.x];
+}
+
 // result[0] = 1 iff no set is invalid and final_exp(prod_{i<g} f_i) == 1
 // (one 64-lane wave; g = number of per-GPU partials)
 extern "C" __global__ void __launch_bounds__(64) k_final_verify_wave(const fp12* __restrict__ f, uint32_t g,

@@ -18,6 +18,8 @@
 #include "../../include/tekukzg.h"
 #include "tb_kzg_decl.h"
 #include "tb_host.h"
+#include "tb_sha256_host.h"
+#include <thread>
 
 using namespace tb;
 
@@ -93,7 +95,7 @@ struct kzg_state {
   uint8_t* lag_inf = nullptr;
   fr* roots = nullptr;
   g2a* g2 = nullptr;  // G2 monomial points; [tau]_2 = g2[1]
-  growbuf ws, stage{nullptr, 0, true};
+  growbuf ws, stage{nullptr, 0, true}, dstage{nullptr, 0, true};  // dstage: host challenge digests
   float stage_ms[6] = {};
   // the last verify's device transcript (tkzg_last_transcript)
   const fr *last_z = nullptr, *last_y = nullptr, *last_r = nullptr;
@@ -111,7 +113,7 @@ constexpr size_t PAIR_WS_BYTES = 2 * sizeof(g1a) + 2 * sizeof(g2a) + 16 + 16 + 2
 
 // worst-case workspace for a verify of n blobs (besides the inputs)
 size_t verify_ws_bytes(size_t n) {
-  return align16(2 * n * sizeof(g1a)) + align16(2 * n) + align16(2 * n) + 2 * align16(n * sizeof(fr)) + align16(n) +
+  return align16(2 * n * sizeof(g1a)) + align16(2 * n) + align16(2 * n) + 2 * align16(n * sizeof(fr)) + align16(n) + align16(32 * n) +
          align16(32 + 160 * n) + align16(sizeof(fr)) + align16((3 * n + 1) * sizeof(g1j)) + align16(sizeof(int)) + 64 + PAIR_WS_BYTES;
 }
 
@@ -146,12 +148,40 @@ void launch_pairing(kzg_state& g, const g1j* T, uint32_t n, const pair_ws& p, in
 
 // The verification on device-resident inputs: ok_host <- verdict, or BADARGS
 // from the per-blob / per-point codes.  single: verify_kzg_proof_impl (n == 1).
+// Small batches (n <= TKZG_COOP_MAX, default 1024; 0 disables) decode the points and form the
+// terms on lane-cooperative rows (k_kzg_points_coop, k_kzg_terms_coop).
+static bool kzg_coop(size_t n) {
+  static const long v = getenv("TKZG_COOP_MAX") ? atol(getenv("TKZG_COOP_MAX")) : 1024;
+  return (long)n <= v;
+}
+void launch_points(const uint8_t* d_com, const uint8_t* d_proof, uint32_t un, g1a* pts, uint8_t* pinf, uint8_t* codes, hipStream_t sp) {
+  if (kzg_coop(un)) {
+    hipLaunchKernelGGL(k_kzg_points_coop, dim3(blocks(un, 4)), dim3(64), 0, sp, d_com, un, pts, pinf, codes);
+    hipLaunchKernelGGL(k_kzg_points_coop, dim3(blocks(un, 4)), dim3(64), 0, sp, d_proof, un, pts + un, pinf + un, codes + un);
+  } else {
+    hipLaunchKernelGGL(k_kzg_points, dim3(blocks(un, TB_BLOCK)), dim3(TB_BLOCK), 0, sp, d_com, un, pts, pinf, codes);
+    hipLaunchKernelGGL(k_kzg_points, dim3(blocks(un, TB_BLOCK)), dim3(TB_BLOCK), 0, sp, d_proof, un, pts + un, pinf + un, codes + un);
+  }
+}
+
+// compute_challenge digests of n host blobs (tb_sha256_host.h), blobs on
+// separate threads beyond the first
+void host_digests(const uint8_t* blobs, const uint8_t* com, size_t n, uint8_t* out) {
+  std::vector<std::thread> th;
+  for (size_t i = 1; i < n; i++) th.emplace_back([=]() { tbh::kzg_challenge_digest(blobs + i * BLOB, BLOB, com + 48 * i, out + 32 * i); });
+  if (n) tbh::kzg_challenge_digest(blobs, BLOB, com, out);
+  for (auto& t : th) t.join();
+}
+
+// h_blobs / h_com (optional): the same inputs in host memory -- the
+// challenges are then hashed here while the device decodes the points.
 int verify_dev(kzg_state& g, const uint8_t* d_blobs, const uint8_t* d_com, const uint8_t* d_proof, size_t n, hipStream_t s,
-               uint8_t* ws, int* ok_host, bool timed) {
+               uint8_t* ws, int* ok_host, bool timed, const uint8_t* h_blobs = nullptr, const uint8_t* h_com = nullptr) {
   carve c{ws};
   g1a* pts = c.take<g1a>(2 * n);
   uint8_t* pinf = c.take<uint8_t>(2 * n);
   uint8_t* codes = c.take<uint8_t>(3 * n);  // points (2n) then blobs (n)
+  uint8_t* dig = c.take<uint8_t>(32 * n);
   fr* z = c.take<fr>(n);
   fr* y = c.take<fr>(n);
   uint8_t* rec = c.take<uint8_t>(32 + 160 * n);
@@ -166,17 +196,22 @@ int verify_dev(kzg_state& g, const uint8_t* d_blobs, const uint8_t* d_com, const
   if (!timed) {
     KCHK(hipEventRecord(g.fork, s));
     KCHK(hipStreamWaitEvent(sp, g.fork, 0));
-    hipLaunchKernelGGL(k_kzg_points, dim3(blocks(n, TB_BLOCK)), dim3(TB_BLOCK), 0, sp, d_com, un, pts, pinf, codes);
-    hipLaunchKernelGGL(k_kzg_points, dim3(blocks(n, TB_BLOCK)), dim3(TB_BLOCK), 0, sp, d_proof, un, pts + n, pinf + n, codes + n);
+    launch_points(d_com, d_proof, un, pts, pinf, codes, sp);
     KCHK(hipEventRecord(g.join, sp));
   }
-  hipLaunchKernelGGL(k_kzg_challenge, dim3(blocks(n, TB_BLOCK)), dim3(TB_BLOCK), 0, s, d_blobs, d_com, un, z);
+  if (h_blobs) {  // the host hashes while the device decodes
+    if (g.dstage.ensure(32 * n)) return fail(TKZG_MALLOC, "pinned staging allocation failed");
+    host_digests(h_blobs, h_com, n, g.dstage.b());
+    KCHK(hipMemcpyAsync(dig, g.dstage.b(), 32 * n, hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(k_kzg_z_from_digest, dim3(blocks(n, TB_BLOCK)), dim3(TB_BLOCK), 0, s, (const uint8_t*)dig, un, z);
+  } else {
+    hipLaunchKernelGGL(k_kzg_challenge, dim3(blocks(n, TB_BLOCK)), dim3(TB_BLOCK), 0, s, d_blobs, d_com, un, z);
+  }
   if (timed) KCHK(hipEventRecord(g.ev[1], s));
   hipLaunchKernelGGL(k_kzg_eval, dim3(un), dim3(256), 0, s, d_blobs, un, z, g.roots, (fr*)nullptr, y, codes + 2 * n);
   if (timed) {
     KCHK(hipEventRecord(g.ev[2], s));
-    hipLaunchKernelGGL(k_kzg_points, dim3(blocks(n, TB_BLOCK)), dim3(TB_BLOCK), 0, s, d_com, un, pts, pinf, codes);
-    hipLaunchKernelGGL(k_kzg_points, dim3(blocks(n, TB_BLOCK)), dim3(TB_BLOCK), 0, s, d_proof, un, pts + n, pinf + n, codes + n);
+    launch_points(d_com, d_proof, un, pts, pinf, codes, s);
     KCHK(hipEventRecord(g.ev[3], s));
   }
   if (n > 1) {
@@ -187,7 +222,10 @@ int verify_dev(kzg_state& g, const uint8_t* d_blobs, const uint8_t* d_com, const
   }
   if (timed) KCHK(hipEventRecord(g.ev[4], s));
   if (!timed) KCHK(hipStreamWaitEvent(s, g.join, 0));
-  hipLaunchKernelGGL(k_kzg_terms, dim3(blocks(3 * n + 1, TB_BLOCK)), dim3(TB_BLOCK), 0, s, pts, pinf, z, y, r, un, T);
+  if (kzg_coop(n))
+    hipLaunchKernelGGL(k_kzg_terms_coop, dim3(3 * un + 1), dim3(16), 0, s, pts, pinf, z, y, r, un, T);
+  else
+    hipLaunchKernelGGL(k_kzg_terms, dim3(blocks(3 * n + 1, TB_BLOCK)), dim3(TB_BLOCK), 0, s, pts, pinf, z, y, r, un, T);
   if (timed) KCHK(hipEventRecord(g.ev[5], s));
   launch_pairing(g, T, un, pw, ok, s);
   if (timed) KCHK(hipEventRecord(g.ev[6], s));
@@ -225,9 +263,11 @@ int verify_host(kzg_state& g, const uint8_t* blobs, const uint8_t* com, const ui
   memcpy(h + align16(n * BLOB) + align16(48 * n), proof, 48 * n);
   KCHK(hipMemcpyAsync(g.ws.p, h, in_bytes, hipMemcpyHostToDevice, g.s));
   uint8_t* d = g.ws.b();
-  // the stage is reused for the verdict only after this copy completed
-  KCHK(hipStreamSynchronize(g.s));
-  return verify_dev(g, d, d + align16(n * BLOB), d + align16(n * BLOB) + align16(48 * n), n, g.s, d + in_bytes, ok, false);
+  // small batches: the Fiat-Shamir challenges on the host (TKZG_HOST_CHALLENGE_MAX, default 16; 0: on the device)
+  static const long hmax = getenv("TKZG_HOST_CHALLENGE_MAX") ? atol(getenv("TKZG_HOST_CHALLENGE_MAX")) : 16;
+  const bool host_ch = (long)n <= hmax;
+  return verify_dev(g, d, d + align16(n * BLOB), d + align16(n * BLOB) + align16(48 * n), n, g.s, d + in_bytes, ok, false,
+                    host_ch ? blobs : nullptr, host_ch ? com : nullptr);
 }
 
 // g1_lincomb over the Lagrange points of n_blobs scalar vectors (device), out: 48 B each (device)
@@ -515,9 +555,15 @@ extern "C" int tkzg_verify_kzg_proof(int* ok, const uint8_t commitment[48], cons
     memcpy(h + 96, z_b, 32);
     memcpy(h + 128, y_b, 32);
     KCHK(hipMemcpyAsync(d_in, h, 160, hipMemcpyHostToDevice, g.s));
-    hipLaunchKernelGGL(k_kzg_points, dim3(1), dim3(TB_BLOCK), 0, g.s, d_in, 2u, pts, pinf, codes);
+    if (kzg_coop(1))
+      hipLaunchKernelGGL(k_kzg_points_coop, dim3(1), dim3(64), 0, g.s, d_in, 2u, pts, pinf, codes);
+    else
+      hipLaunchKernelGGL(k_kzg_points, dim3(1), dim3(TB_BLOCK), 0, g.s, d_in, 2u, pts, pinf, codes);
     hipLaunchKernelGGL(k_kzg_scalars_in, dim3(1), dim3(TB_BLOCK), 0, g.s, d_in + 96, 2u, zy, codes + 2);
-    hipLaunchKernelGGL(k_kzg_terms, dim3(1), dim3(TB_BLOCK), 0, g.s, pts, pinf, zy, zy + 1, zy, 1u, T);
+    if (kzg_coop(1))
+      hipLaunchKernelGGL(k_kzg_terms_coop, dim3(4), dim3(16), 0, g.s, pts, pinf, zy, zy + 1, zy, 1u, T);
+    else
+      hipLaunchKernelGGL(k_kzg_terms, dim3(1), dim3(TB_BLOCK), 0, g.s, pts, pinf, zy, zy + 1, zy, 1u, T);
     launch_pairing(g, T, 1u, pw, d_ok, g.s);
     KCHK(hipGetLastError());
     KCHK(hipStreamSynchronize(g.s));

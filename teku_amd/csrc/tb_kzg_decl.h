@@ -20,4 +20,7 @@ __global__ void k_kzg_quotient(const tb::fr* poly, const tb::fr* z, const tb::fr
 __global__ void k_kzg_quotient_domain(const tb::fr* poly, const tb::fr* z, const tb::fr* y, const tb::fr* roots, tb::fr* q);
 __global__ void k_kzg_lincomb_terms(const tb::fr* sc, const tb::g1a* lag, const uint8_t* lag_inf, uint32_t n_blobs, tb::g1j* T);
 __global__ void k_kzg_lincomb_reduce(const tb::g1j* T, uint8_t* out);
+__global__ void k_kzg_z_from_digest(const uint8_t* dig, uint32_t n, tb::fr* z);
+__global__ void k_kzg_points_coop(const uint8_t* bytes, uint32_t m, tb::g1a* out, uint8_t* inf, uint8_t* code);
+__global__ void k_kzg_terms_coop(const tb::g1a* pts, const uint8_t* inf, const tb::fr* z, const tb::fr* y, const tb::fr* r, uint32_t n, tb::g1j* T);
 }

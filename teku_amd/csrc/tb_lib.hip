@@ -155,8 +155,63 @@ static uint32_t miller_wave_max() {
 #ifndef TB_SPREAD_EXTRA
 #define TB_SPREAD_EXTRA 0
 #endif
+// Segmented accumulator (k_lines.hip k_miller_accs): `per` pairs per thread,
+// the loop's 68 steps in `nseg` segments.  Chosen to minimize the modelled
+// accumulator time: per-thread latency (68 / nseg) (12 + 13 per) Fp2
+// products (one f^2, per sparse line products per step) times the wave rounds
+// (TB_ACC_FULL threads = one 64-lane wave per SIMD fill the GPU once); ties go
+// to fewer segments (smaller product tree).  TBLS_ACC_PER / TBLS_ACC_SEG
+// override (A/B); TBLS_ACC_SEG=0 selects the unsegmented k_miller_acc1/2.
+#define TB_ACC_FULL 65536u
+static int acc_env(const char* name) {
+  const char* v = getenv(name);
+  return v ? atoi(v) : -1;
+}
+static void acc_plan(uint32_t n_main, uint32_t& per, uint32_t& nseg) {
+  static const int e_per = acc_env("TBLS_ACC_PER"), e_seg = acc_env("TBLS_ACC_SEG");
+  if (e_seg == 0) {  // the unsegmented kernels
+    per = n_main >= TB_MILLER_PER2_MIN ? 2u : 1u;
+    nseg = 1;
+    return;
+  }
+  double best = 0;
+  per = 1;
+  nseg = 1;
+  for (uint32_t p : {1u, 2u, 4u, 8u}) {
+    if (e_per > 0 && (int)p != e_per) continue;
+    for (uint32_t sg : {1u, 2u, 4u}) {
+      if (e_seg > 0 && (int)sg != e_seg) continue;
+      const double threads = (double)sg * ((n_main + p - 1) / p);
+      const double rounds = std::max(1.0, std::ceil(threads / TB_ACC_FULL));
+      const double cost = rounds * (68.0 / sg) * (12.0 + 13.0 * p);
+      if (best == 0 || cost < best * 0.999) {
+        best = cost;
+        per = p;
+        nseg = sg;
+      }
+    }
+  }
+}
+// Horner exponents of the segment products: byte j - 1 = doubling steps in
+// segment j (j >= 1) of the 68-step loop split as k_miller_accs splits it
+static uint32_t seg_dpack(uint32_t nseg) {
+  int dbl[68];
+  int s = 0;
+  for (int b = 62; b >= 0; --b) {
+    dbl[s++] = 1;
+    if ((X_ABS >> b) & 1) dbl[s++] = 0;
+  }
+  uint32_t pack = 0;
+  for (uint32_t j = 1; j < nseg; j++) {
+    uint32_t d = 0;
+    for (uint32_t t = 68 * j / nseg; t < 68 * (j + 1) / nseg; t++) d += (uint32_t)dbl[t];
+    pack |= d << (8 * (j - 1));
+  }
+  return pack;
+}
+
 struct pair_plan {
-  uint32_t n, n_extra, n_pairs, n_main, n_spread, n_xwave, per;
+  uint32_t n, n_extra, n_pairs, n_main, n_spread, n_xwave, per, nseg;
   bool msm, wave, split;
   explicit pair_plan(uint32_t n_) : n(n_) {
     msm = n >= TB_MSM_MIN;
@@ -167,22 +222,32 @@ struct pair_plan {
     n_spread = split && msm && TB_SPREAD_EXTRA ? n_extra : 0u;  // pairs spread line by line
     n_xwave = split && msm && !TB_SPREAD_EXTRA ? n_extra : 0u;  // pairs on their own waves
     n_main = n_pairs - n_spread - n_xwave;                       // pairs owned by accumulator threads
-    per = wave ? 1u : split ? (n_main >= TB_MILLER_PER2_MIN ? 2u : 1u) : (n_pairs <= TB_MILLER1_MAX ? 1u : 2u);
+    nseg = 1;
+    if (wave)
+      per = 1;
+    else if (split)
+      acc_plan(n_main, per, nseg);
+    else
+      per = n_pairs <= TB_MILLER1_MAX ? 1u : 2u;
+    if (n_spread) nseg = 1;  // the spread extra lines need whole loops per thread
   }
-  uint32_t n_f_main() const { return (n_main + per - 1) / per; }
-  uint32_t n_f() const { return n_f_main() + n_xwave; }  // Miller values: accumulators, then the wave pairs'
+  bool seg() const { return split && (nseg > 1 || per > 2); }  // k_miller_accs
+  uint32_t n_groups() const { return (n_main + per - 1) / per; }
+  uint32_t n_f_main() const { return nseg * n_groups(); }
+  uint32_t n_f() const { return n_f_main() + n_xwave; }  // Miller values: accumulators (segment-major), then the wave pairs'
   uint32_t line_pairs() const { return split ? std::min(n_main, TB_LINE_CHUNK) : 0u; }
 };
 
 struct ws_layout {
-  size_t pk_aff, pk_code, P, Q, skip, set_code, sig_code, f, fpart, fpart2, n_bad, result;
+  size_t pk_aff, pk_code, P, Q, skip, set_code, sig_code, f, fpart, fpart2, segv, n_bad, result;
   size_t sig_aff, sig_use, msm_cnt, msm_off, msm_cur, msm_idx, msm_part, msm_sum, mlist, mcnt, lines, xlines, total;
   uint32_t nb_f;
   ws_layout() : total(0) {}
   ws_layout(const pair_plan& pp, uint32_t K) {
     const uint32_t n = pp.n, np = pp.n_pairs, nf = pp.n_f();
     const bool msm = pp.msm;
-    nb_f = (nf + TB_PROD_CHUNK - 1) / TB_PROD_CHUNK;  // first product level
+    // first product level; segmented: nseg rows of the last segment's width
+    nb_f = (nf + TB_PROD_CHUNK - 1) / TB_PROD_CHUNK + pp.nseg * ((pp.n_groups() + pp.n_xwave + TB_PROD_CHUNK - 1) / TB_PROD_CHUNK);
     size_t o = 0;
     pk_aff = o;   o = align_up(o + (size_t)K * sizeof(g1a));
     pk_code = o;  o = align_up(o + K);
@@ -206,7 +271,8 @@ struct ws_layout {
     xlines = o;   o = align_up(o + (size_t)pp.n_spread * TB_LINE_BYTES_PER_PAIR);
     f = o;        o = align_up(o + (size_t)(nf ? nf : 1) * sizeof(fp12));
     fpart = o;    o = align_up(o + (size_t)nb_f * sizeof(fp12));
-    fpart2 = o;   o = align_up(o + (size_t)((nb_f + TB_PROD_CHUNK - 1) / TB_PROD_CHUNK) * sizeof(fp12));
+    fpart2 = o;   o = align_up(o + (size_t)((nb_f + TB_PROD_CHUNK - 1) / TB_PROD_CHUNK + pp.nseg) * sizeof(fp12));
+    segv = o;     o = align_up(o + (size_t)pp.nseg * sizeof(fp12));
     n_bad = o;    o = align_up(o + 4);
     result = o;   o = align_up(o + 4);
     total = o;
@@ -244,8 +310,15 @@ void launch_set_pk(hipStream_t s, uint32_t n, uint32_t n_entries, const uint32_t
   if (!multi) return;
   (void)hipMemsetAsync(mcnt, 0, 4, s);
   hipLaunchKernelGGL(k_multi_list, g, blk, 0, s, pk_off, n, mlist, mcnt);
-  hipLaunchKernelGGL(k_set_pk_wave, dim3(std::min<uint32_t>(n, 4096u)), dim3(64), 0, s, pk_off, aff, code, rand,
-                     (const uint32_t*)mlist, (const uint32_t*)mcnt, P, set_code, n_bad, key_idx, tab_n);
+  // lane-cooperative aggregation (16 rows per set, k_kcoop.hip); TBLS_AGG_COOP=0
+  // selects the one-wave-per-set kernel (A/B)
+  static const bool agg_coop = !(getenv("TBLS_AGG_COOP") && getenv("TBLS_AGG_COOP")[0] == '0');
+  if (agg_coop)
+    hipLaunchKernelGGL(k_set_pk_agg_coop, dim3(std::min<uint32_t>(n, 4096u)), dim3(256), 0, s, pk_off, aff, code, rand,
+                       (const uint32_t*)mlist, (const uint32_t*)mcnt, P, set_code, n_bad, key_idx, tab_n);
+  else
+    hipLaunchKernelGGL(k_set_pk_wave, dim3(std::min<uint32_t>(n, 4096u)), dim3(64), 0, s, pk_off, aff, code, rand,
+                       (const uint32_t*)mlist, (const uint32_t*)mcnt, P, set_code, n_bad, key_idx, tab_n);
 }
 
 extern "C" __global__ void k_set_hash_wave(const uint8_t* __restrict__ msgs, const uint32_t* __restrict__ msg_off,
@@ -448,9 +521,15 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
           HIPCHK(hipStreamWaitEvent(s, c.e_join[1], 0));
           joined = true;
         }
-        hipLaunchKernelGGL(pp.per == 2 ? k_miller_acc2 : k_miller_acc1, dim3((mt + TB_BLOCK - 1) / TB_BLOCK), blk, 0, s,
-                           (const uint4*)lines, (const uint8_t*)skip + lo, ca + lo, cb + lo, m, (const uint4*)(w + L.xlines),
-                           (const uint8_t*)skip + pp.n_main, ex, f + lo / pp.per);
+        if (pp.seg()) {  // segment-major values: segment j of group g at f[j * n_groups + g]
+          const uint32_t g_pad = (mt + TB_BLOCK - 1) / TB_BLOCK * TB_BLOCK;
+          hipLaunchKernelGGL(k_miller_accs, dim3(pp.nseg * g_pad / TB_BLOCK), blk, 0, s, (const uint4*)lines, (const uint8_t*)skip + lo,
+                             ca + lo, cb + lo, m, pp.per, pp.nseg, g_pad, f + lo / pp.per, pp.n_groups());
+        } else {
+          hipLaunchKernelGGL(pp.per == 2 ? k_miller_acc2 : k_miller_acc1, dim3((mt + TB_BLOCK - 1) / TB_BLOCK), blk, 0, s,
+                             (const uint4*)lines, (const uint8_t*)skip + lo, ca + lo, cb + lo, m, (const uint4*)(w + L.xlines),
+                             (const uint8_t*)skip + pp.n_main, ex, f + lo / pp.per);
+        }
       }
     } else
       hipLaunchKernelGGL(pp.per == 1 ? k_miller1 : k_miller2, dim3((nf + TB_BLOCK - 1) / TB_BLOCK), blk, 0, s, (const g1a*)P,
@@ -468,6 +547,27 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
     const fp12* src = (const fp12*)(w + L.f);
     uint32_t cnt = nf ? nf : 1;
     int lvl = 0;
+    if (pp.seg() && pp.nseg > 1) {
+      // per segment (grid y), the bit-sum pairs' values with the last, to the
+      // nseg segment products, then the Horner combine into the partial
+      uint32_t cn = pp.n_groups(), cl = pp.n_groups() + pp.n_xwave, stride = pp.n_groups();
+      for (;;) {
+        const uint32_t no = (cn + TB_PROD_CHUNK - 1) / TB_PROD_CHUNK, nl = (cl + TB_PROD_CHUNK - 1) / TB_PROD_CHUNK;
+        const bool fin = nl == 1;
+        fp12* dstp = (fp12*)(w + (fin ? L.segv : ((lvl & 1) ? L.fpart2 : L.fpart)));
+        const uint32_t ostride = fin ? 1u : nl;
+        hipLaunchKernelGGL(k_fp12_prod_wave_seg, dim3(nl, pp.nseg), dim3(64), 0, s, src, cn, cl, pp.nseg, stride, TB_PROD_CHUNK, dstp,
+                           ostride);
+        if (fin) break;
+        src = dstp;
+        cn = no;
+        cl = nl;
+        stride = nl;
+        lvl++;
+      }
+      hipLaunchKernelGGL(k_fp12_seg_combine_coop, dim3(1), dim3(TB_CFE_THREADS), 0, s, (const fp12*)(w + L.segv), pp.nseg,
+                         seg_dpack(pp.nseg), (fp12*)partial_out);
+    } else
     for (;;) {
       const uint32_t nout = (cnt + TB_PROD_CHUNK - 1) / TB_PROD_CHUNK;
       fp12* dstp = nout == 1 ? (fp12*)partial_out : (fp12*)(w + ((lvl & 1) ? L.fpart2 : L.fpart));

@@ -171,3 +171,25 @@ extern "C" int tbls_hostsim_cpoint_g2(int op, const uint32_t* in, uint32_t* out,
   }
   return 0;
 }
+
+// host SHA-256 of the KZG challenges (tb_sha256_host.h): portable and SHA-NI
+// rounds (ni = 1 uses the extension when the CPU has it)
+#include "../../teku_amd/csrc/tb_sha256_host.h"
+extern "C" int tbls_hostsim_sha256(const uint8_t* p, size_t len, int ni, uint8_t* out) {
+  tbh::sha_force_portable() = !ni;
+  tbh::sha256 h;
+  size_t o = 0, step = 1;
+  while (o < len) {  // uneven update sizes exercise the buffer
+    const size_t k = (len - o) < step ? (len - o) : step;
+    h.update(p + o, k);
+    o += k;
+    step = step * 3 + 1;
+  }
+  h.final(out);
+  tbh::sha_force_portable() = false;
+  return tbh::sha_have_ni() ? 1 : 0;
+}
+extern "C" int tbls_hostsim_kzg_digest(const uint8_t* blob, size_t blob_len, const uint8_t* com, uint8_t* out) {
+  tbh::kzg_challenge_digest(blob, blob_len, com, out);
+  return 0;
+}

@@ -219,3 +219,37 @@ def test_config5_131k_shard(S):
             # the oracle's verdict on the tampered set alone decides the batch
             assert C.verify_each([[p[j]]], [m[j]], [s[j]])[0] is False, (name, j)
             assert got is False, (name, j)
+
+
+def test_multi_key_exceptional_sums(S):
+    """Multi-key sets whose aggregation meets P == +-Q (k_set_pk_agg_coop's
+    one-lane fallback): a repeated key in one coop row (keys 0 and 16), a key
+    beside its negation in one row, keys cancelling to infinity
+    (PK_IS_INFINITY -> the set fails), and a repeated key across rows.  Verdicts
+    of the randomized batch and of fastAggregateVerify per set vs the C oracle."""
+    R = S.R_ORDER
+    base = [S.interop_sk(60000 + i) for i in range(40)]
+    sets_sk = []
+    sets_sk.append(list(base))                                  # plain
+    s1 = list(base); s1[16] = s1[0]; sets_sk.append(s1)          # repeated key, same row
+    s2 = list(base); s2[17] = R - s2[1]; sets_sk.append(s2)      # key and its negation, same row
+    s3 = []
+    for k in base[:20]:
+        s3 += [k, R - k]
+    sets_sk.append(s3)                                          # aggregate = infinity
+    s4 = list(base); s4[1] = s4[0]; sets_sk.append(s4)           # repeated key, different rows
+    s5 = list(base[:18]); s5[2] = s5[17]; sets_sk.append(s5)     # short set, keys 2 == 17 (rows 2 and 1)
+    msgs = [S.bench_message(77, s) for s in range(len(sets_sk))]
+    keys = [S.pubkeys(sk) for sk in sets_sk]
+    agg = [sum(sk) % R for sk in sets_sk]
+    sig = S.sign_blob([a if a else 1 for a in agg], msgs)
+    sigs = [sig[96 * s : 96 * s + 96] for s in range(len(sets_sk))]
+    sigs[3] = S.INFINITY_G2  # the infinity aggregate's "signature"
+    got = S.SetArray.from_lists(keys, msgs, sigs).fast_aggregate_verify_many()
+    exp = C.verify_each(keys, msgs, sigs, threads=THREADS)
+    assert got == exp == [True, True, True, False, True, True]
+    valid = [s for s in range(len(sets_sk)) if s != 3]
+    r = S.random_multipliers(len(valid))
+    kv, mv, sv = [keys[s] for s in valid], [msgs[s] for s in valid], [sigs[s] for s in valid]
+    assert S.SetArray.from_lists(kv, mv, sv).batch_verify(r) is True
+    assert S.SetArray.from_lists(keys, msgs, sigs).batch_verify(S.random_multipliers(len(keys))) is False

@@ -69,3 +69,29 @@ def test_without_device_or_setup_fails_loudly():
         c = kzg.CKZG4844()
         with pytest.raises(kzg.KZGException):
             c.load_trusted_setup(SETUP)
+
+
+def test_host_sha256_challenge_digest():
+    """tb_sha256_host.h (the host-side Fiat-Shamir challenge hash of small
+    host-API batches, tb_kzg.hip verify_host): SHA-NI and portable rounds vs
+    hashlib at block-boundary lengths, and compute_challenge's transcript
+    layout (FSBLOBVERIFY_V1_ || 4096 as 16 bytes BE || blob || commitment)."""
+    import hashlib
+
+    import __graft_entry__ as ge
+
+    L = ctypes.CDLL(ge.build_hostsim())
+    L.tbls_hostsim_sha256.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_char_p]
+    L.tbls_hostsim_kzg_digest.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_char_p]
+    rnd = __import__("random").Random(7)
+    for n in (0, 1, 55, 56, 63, 64, 65, 119, 120, 127, 128, 1000, 131152):
+        d = bytes(rnd.getrandbits(8) for _ in range(n))
+        for ni in (0, 1):
+            out = ctypes.create_string_buffer(32)
+            L.tbls_hostsim_sha256(d, len(d), ni, out)
+            assert out.raw == hashlib.sha256(d).digest(), (n, ni)
+    blob = bytes(rnd.getrandbits(8) for _ in range(131072))
+    com = bytes(rnd.getrandbits(8) for _ in range(48))
+    out = ctypes.create_string_buffer(32)
+    L.tbls_hostsim_kzg_digest(blob, len(blob), com, out)
+    assert out.raw == hashlib.sha256(b"FSBLOBVERIFY_V1_" + (4096).to_bytes(16, "big") + blob + com).digest()
