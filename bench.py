@@ -72,8 +72,38 @@ def peak_mac_per_s(device):
     return MAD_RATE_PER_CU_CLK * torch.cuda.get_device_properties(device).multi_processor_count * CLOCK_HZ
 
 
+def acc_plan(S):
+    """(per, nseg, split) of the library's Miller-accumulator plan at S sets (tbls_acc_plan)."""
+    per, nseg, split = ctypes.c_uint32(0), ctypes.c_uint32(0), ctypes.c_int(0)
+    native.check(native.lib().tbls_acc_plan(S, ctypes.byref(per), ctypes.byref(nseg), ctypes.byref(split)), "acc_plan")
+    return per.value, nseg.value, split.value
+
+
+def plan_counts(S):
+    """M_PER_UNIT with the Miller work of the plan the library runs at S sets:
+    the segmented accumulator (k_miller_accs) shares one f^2 among `per` pairs
+    (tools/count_muls.py miller_seg_PxS), the unsegmented k_miller_acc2 among 2."""
+    per, nseg, split = acc_plan(S)
+    mc = dict(M_PER_UNIT)
+    key = f"miller_seg_{per}x{nseg}"
+    seg = split and (nseg > 1 or per > 2)
+    if seg and key in mc:
+        d = mc[key] - mc["miller"]
+        mc["miller"] = mc[key]
+        mc["per_set_total"] = mc["per_set_total"] + mc.get("pairs_per_set", 1.0) * d
+        mads = dict(mc.get("mads_per_unit", {}))
+        if "miller" in mads:  # the accumulator's products are lazy Fp2 products (3 M, 980 v_mad_u64_u32 each)
+            mads["miller"] = round(mads["miller"] + d / 3 * mc.get("mads_per_fp2_mul", 980))
+        mc["mads_per_unit"] = mads
+    kern = dict(STAGE_KERNEL)
+    if seg:
+        kern["miller"] = "k_miller_lines + k_miller_accs"
+    return mc, kern, {"per": per, "nseg": nseg, "kernel": "k_miller_accs" if seg else "k_miller_acc1/2"}
+
+
 def roofline_entry(stage_ms, S, device, ms_per_step):
     peak = peak_mac_per_s(device)
+    M_PER_UNIT, STAGE_KERNEL, plan = plan_counts(S)
     mads = M_PER_UNIT.get("mads_per_unit", {})
     per_stage = {}
     pairs = M_PER_UNIT.get("pairs_per_set", 1.0)  # set pairs + the signature side's bucket pairs
@@ -108,6 +138,7 @@ def roofline_entry(stage_ms, S, device, ms_per_step):
         "issue_frac": (mads[name] * units[name] / (stage_ms[dom] * 1e-3)) / peak if name in mads else None,
         "stage_frac": {k: v / peak for k, v in per_stage.items()},
         "pipeline_frac": (per_set * MAC_PER_M * S / (ms_per_step * 1e-3)) / peak if per_set else None,
+        "acc_plan": plan,
     }
 
 

@@ -208,6 +208,13 @@ int tbls_dev_batch_partial_timed(int device, const tbls_dev_batch* b, void* stre
  * so stage_ms[7] are exclusive kernel times (the roofline's denominators). */
 int tbls_dev_batch_stage_profile(int device, const tbls_dev_batch* b, void* stream, void* partial_out, float* stage_ms);
 
+/* The Miller-accumulator plan the library uses for a batch of n sets of one
+ * key (introspection for benchmarks and tuning; no device work): *per = pairs
+ * per accumulator thread, *nseg = loop segments per pair (1: unsegmented),
+ * *split = 1 when the split line / accumulator kernels run (0: one-workgroup
+ * wave Miller loops for small batches).  Always TBLS_SUCCESS. */
+int tbls_acc_plan(uint32_t n, uint32_t* per, uint32_t* nseg, int* split);
+
 /* Multiply g partial records (device memory, contiguous) and run the final
  * exponentiation: *ok = 1 iff no invalid set and the product is 1. */
 int tbls_dev_final_verify(int device, const void* partials, uint32_t g, void* stream, int* ok);

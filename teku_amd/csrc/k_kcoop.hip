@@ -351,9 +351,9 @@ extern "C" __global__ void __launch_bounds__(64)
 struct ka_set {
   int32_t pt[16][3][16];  // row sums (X, Y, Z digits)
   uint32_t inf[16];
-  int32_t zb[4][16];
-  fp inv;
-  fp out[2];
+  int32_t zb[2][4][16];   // row 0 ([r] apk) and row 4 (-[r] g1)
+  fp inv[2];
+  fp out[2][2];
   int bad;
 };
 
@@ -366,7 +366,7 @@ extern "C" __global__ void __launch_bounds__(256)
     k_set_pk_agg_coop(const uint32_t* __restrict__ pk_off, const g1a* __restrict__ pk_aff, const uint8_t* __restrict__ pk_code,
                       const uint64_t* __restrict__ rand, const uint32_t* __restrict__ list, const uint32_t* __restrict__ cnt,
                       g1a* __restrict__ P, uint8_t* __restrict__ set_code, uint32_t* __restrict__ n_bad,
-                      const uint32_t* __restrict__ key_idx, uint32_t tab_n) {
+                      const uint32_t* __restrict__ key_idx, uint32_t tab_n, g1a* __restrict__ P2, const g1a* __restrict__ comb) {
   __shared__ ka_set S;
   tb_latency_prio();
   const int q = crow::row(), d = crow::dig();
@@ -424,11 +424,50 @@ extern "C" __global__ void __launch_bounds__(256)
       }
       __syncthreads();
     }
-    // ---- row 0: the aggregate, [r] apk, affine
+    // ---- row 0: the aggregate, [r] apk, affine; row 4 (wave 1, beside it):
+    // the set's signature-pair point -[r] g1 from the comb (P2, when given)
+    if (q == 4 && P2) {
+      const uint64_t rnd = rand[i];
+      coop::cj1 cacc = {one, one, c32(0)};
+      bool cinf = true;
+      for (int k = 0; k < 8; k++) {  // one mixed addition per nonzero byte of r (neg_r_g1)
+        const uint32_t dg = (uint32_t)(rnd >> (8 * k)) & 255u;
+        if (dg) {
+          const g1a* cq = comb + k * 256 + dg;
+          const c32 qx = crow::from_fp(cq->x), qy = crow::from_fp(cq->y);
+          if (cinf) {
+            cacc = {qx, qy, one};
+            cinf = false;
+          } else {
+            cacc = coop::madd(cacc, qx, qy, K);
+          }
+        }
+      }
+      if (!cinf) {
+        const c32 v1[1] = {cacc.z};
+        crow::to_fp_n<1>(v1, S.zb[1], &S.inv[1]);
+        if (d == 0) S.inv[1] = fp_inv(S.inv[1]);
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        const c32 i1 = crow::from_fp(S.inv[1]);
+        const c32 i2 = coop::csqr(i1, K);
+        c32 a3[2] = {cacc.x, i2}, b3[2] = {i2, i1}, i3[2];
+        coop::cmul_n<2>(i3, a3, b3, K);
+        const c32 y = coop::cmul(cacc.y, i3[1], K);
+        const c32 v2[2] = {i3[0], y};
+        crow::to_fp_n<2>(v2, S.zb[1], S.out[1]);
+      }
+      if (d == 0) {
+        g1a o;
+        o.x = cinf ? fp_zero() : S.out[1][0];
+        o.y = fp_neg(cinf ? fp_zero() : S.out[1][1]);
+        P2[i] = o;
+      }
+    }
     if (q == 0) {
       const coop::cj1 apk = {S.pt[0][0][d], S.pt[0][1][d], S.pt[0][2][d]};
       const c32 zv[1] = {apk.z};
-      const bool zero = S.inf[0] != 0 || crow::zeros_n<1>(zv, S.zb) != 0u;
+      const bool zero = S.inf[0] != 0 || crow::zeros_n<1>(zv, S.zb[0]) != 0u;
       const uint64_t rnd = rand[i];
       int code = S.bad;
       if (code == TB_SUCCESS && zero) {
@@ -436,33 +475,33 @@ extern "C" __global__ void __launch_bounds__(256)
         if (d == 0) {
           g1a o;
           code = ka_set_generic(pk_aff, pk_code, b, e, rnd, o, key_idx, tab_n);
-          S.out[0] = o.x;
-          S.out[1] = o.y;
+          S.out[0][0] = o.x;
+          S.out[0][1] = o.y;
         }
       } else if (code == TB_SUCCESS && rnd == 0) {
         code = TB_PK_IS_INFINITY;  // [0] apk (stage_set_pk_finish)
       } else if (code == TB_SUCCESS) {
         const coop::cj1 t = coop::mul_u64(apk, rnd, K);
         const c32 v1[1] = {t.z};
-        crow::to_fp_n<1>(v1, S.zb, &S.inv);
-        if (d == 0) S.inv = fp_inv(S.inv);
+        crow::to_fp_n<1>(v1, S.zb[0], &S.inv[0]);
+        if (d == 0) S.inv[0] = fp_inv(S.inv[0]);
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-        const c32 i1 = crow::from_fp(S.inv);
+        const c32 i1 = crow::from_fp(S.inv[0]);
         const c32 i2 = coop::csqr(i1, K);
         c32 a3[2] = {t.x, i2}, b3[2] = {i2, i1}, i3[2];
         coop::cmul_n<2>(i3, a3, b3, K);  // X / Z^2, 1 / Z^3
         const c32 y = coop::cmul(t.y, i3[1], K);
         const c32 v2[2] = {i3[0], y};
-        crow::to_fp_n<2>(v2, S.zb, S.out);
+        crow::to_fp_n<2>(v2, S.zb[0], S.out[0]);
       }
       if (d == 0) {  // lane 0's code is the set's in every branch
         g1a o;
         o.x = fp_zero();
         o.y = fp_zero();
         if (code == TB_SUCCESS) {
-          o.x = S.out[0];
-          o.y = S.out[1];
+          o.x = S.out[0][0];
+          o.y = S.out[0][1];
         } else {
           set_code[i] = (uint8_t)code;
           atomicAdd(n_bad, 1u);

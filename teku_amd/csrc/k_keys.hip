@@ -8,7 +8,9 @@ using namespace tb;
 // ---------------------------------------------------------------------------
 // public keys
 // ---------------------------------------------------------------------------
-extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_MIN_WAVES)
+// two waves per SIMD (<= 256 registers): at 131,072 keys the 2,048 waves run
+// in one round instead of two
+extern "C" __global__ void __launch_bounds__(TB_BLOCK, 2)
     k_pk_decompress(const uint8_t* __restrict__ pks, uint32_t K, g1a* __restrict__ pk_aff, uint8_t* __restrict__ pk_code) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= K) return;
@@ -16,6 +18,29 @@ extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_MIN_WAVES)
   int code = stage_pk(pks + (size_t)i * 48, a);
   pk_aff[i] = a;
   pk_code[i] = (uint8_t)code;
+}
+
+// Two keys per thread: both square roots interleaved (g1_decompress2), then
+// each key's G1 check; same outputs as k_pk_decompress (TBLS_DEC2=0 selects it)
+extern "C" __global__ void __launch_bounds__(TB_BLOCK, 2)
+    k_pk_decompress2(const uint8_t* __restrict__ pks, uint32_t K, g1a* __restrict__ pk_aff, uint8_t* __restrict__ pk_code) {
+  const uint32_t i0 = 2 * (blockIdx.x * blockDim.x + threadIdx.x);
+  if (i0 >= K) return;
+  g1a a[2];
+  bool inf[2];
+  int code[2];
+  g1_decompress2(a, inf, code, pks + (size_t)i0 * 48, pks + (size_t)(i0 + 1 < K ? i0 + 1 : i0) * 48);
+  for (int j = 0; j < 2 && i0 + j < K; j++) {
+    int c = code[j];
+    if (c == TB_SUCCESS && inf[j]) c = TB_PK_IS_INFINITY;
+    if (c == TB_SUCCESS && !g1_in_group(jac_from_aff(a[j]))) c = TB_POINT_NOT_IN_GROUP;
+    if (c != TB_SUCCESS) {
+      a[j].x = fp_zero();
+      a[j].y = fp_zero();
+    }
+    pk_aff[i0 + j] = a[j];
+    pk_code[i0 + j] = (uint8_t)c;
+  }
 }
 
 // per set: aggregate keys (BlstPublicKey.aggregate semantics), P = [r] apk (affine);
@@ -30,8 +55,10 @@ extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_MIN_WAVES)
              g1a* __restrict__ P2, const g1a* __restrict__ comb) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  if (P2) P2[i] = neg_r_g1(comb, rand[i]);
   const uint32_t b = pk_off[i], e = pk_off[i + 1];
+  // multi_wave 1: multi-key sets go to k_set_pk_wave (P2 here), 2: to
+  // k_set_pk_agg_coop (P2 there too)
+  if (P2 && !(multi_wave == 2 && e - b > 1)) P2[i] = neg_r_g1(comb, rand[i]);
   if (multi_wave && e - b > 1) return;
   g1a out;
   int code = stage_set_pk(pk_aff, pk_code, b, e, rand[i], out, key_idx, tab_n);

@@ -72,6 +72,37 @@ TB_HD TB_INLINE fp12 fp12_mul_by_line_i(const fp12& f, const fp2& A, const fp2& 
   return {c0, c1};
 }
 
+// f * l1 * l2 for two lines of one step (line = (A + B v) + (C v) w): the two
+// lines first (6 Fp2 products; the result L has w^0 coefficient X0 + X1 v +
+// X2 v^2 and w^1 coefficient Y1 v + Y2 v^2), then f * L in 17 (f0 L0 dense,
+// f1 L1 = v f1 (Y1 + Y2 v) sparse, Karatsuba middle term dense): 23 Fp2
+// products instead of 2 x 13.
+//   X0 = A1 A2 + xi C1 C2, X1 = A1 B2 + B1 A2, X2 = B1 B2,
+//   Y1 = A1 C2 + C1 A2,     Y2 = B1 C2 + C1 B2   (the cross terms by Karatsuba)
+TB_HD TB_INLINE fp12 fp12_mul_by_line_pair_i(const fp12& f, const line3& l1, const line3& l2) {
+  fp6 L0;
+  fp2 Y1, Y2;
+  {
+    const fp2 t0 = m2(l1.a, l2.a), t1 = m2(l1.b, l2.b), t2 = m2(l1.c, l2.c);
+    const fp2 s01 = m2(fp2_add(l1.a, l1.b), fp2_add(l2.a, l2.b));
+    const fp2 s02 = m2(fp2_add(l1.a, l1.c), fp2_add(l2.a, l2.c));
+    const fp2 s12 = m2(fp2_add(l1.b, l1.c), fp2_add(l2.b, l2.c));
+    L0 = {fp2_add(t0, fp2_mul_xi(t2)), fp2_sub(s01, fp2_add(t0, t1)), t1};
+    Y1 = fp2_sub(s02, fp2_add(t0, t2));
+    Y2 = fp2_sub(s12, fp2_add(t1, t2));
+  }
+  TB_FENCE();
+  const fp6 t1 = fp6_mul_v(fp6_mul_by_01_f(f.c1, Y1, Y2));  // f1 L1
+  const fp6 s = fp6_add(f.c0, f.c1);
+  const fp6 Ls = {L0.c0, fp2_add(L0.c1, Y1), fp2_add(L0.c2, Y2)};
+  TB_FENCE();
+  const fp6 u = fp6_mul_f(s, Ls);     // (f0 + f1)(L0 + L1)
+  const fp6 t0 = fp6_mul_f(f.c0, L0); // f0 L0
+  const fp6 c1 = fp6_sub(fp6_sub(u, t0), t1);
+  const fp6 c0 = fp6_add(t0, fp6_mul_v(t1));
+  return {c0, c1};
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -342,10 +373,10 @@ __device__ TB_INLINE bool step_is_dbl(int s) { return ((s < 64 ? (DBL_STEPS.lo >
 __device__ TB_INLINE fp12 line_fp12(const line3& l) { return {{l.a, l.b, fp2_zero()}, {fp2_zero(), l.c, fp2_zero()}}; }
 }  // namespace
 
-extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_MIN_WAVES)
-    k_miller_accs(const uint4* __restrict__ lines, const uint8_t* __restrict__ skip, const uint8_t* __restrict__ code_a,
-                  const uint8_t* __restrict__ code_b, uint32_t n, uint32_t per, uint32_t nseg, uint32_t g_pad, fp12* __restrict__ f_out,
-                  uint32_t seg_stride) {
+template <bool PAIRS>
+__device__ TB_INLINE void miller_accs_body(const uint4* __restrict__ lines, const uint8_t* __restrict__ skip,
+                                           const uint8_t* __restrict__ code_a, const uint8_t* __restrict__ code_b, uint32_t n, uint32_t per,
+                                           uint32_t nseg, uint32_t g_pad, fp12* __restrict__ f_out, uint32_t seg_stride) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t j = t / g_pad, g = t % g_pad;
   const uint32_t G = (n + per - 1) / per;
@@ -359,19 +390,44 @@ extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_MIN_WAVES)
   }
   fp12 f = fp12_one();
   bool fresh = true;  // f == 1
+  // the used pairs' offsets, packed 4 bits each (line products in pairs, TB_ACC_PAIRS)
+  uint32_t uidx = 0, nu = 0;
+  for (uint32_t k = 0; k < per; k++)
+    if ((usem >> k) & 1u) uidx |= k << (4 * nu++);
   TB_NOUNROLL for (int s = s_lo; s < s_hi; s++) {
     if (!fresh && step_is_dbl(s)) f = fp12_sqr_i(f);
-    TB_NOUNROLL for (uint32_t k = 0; k < per; k++) {
-      if ((usem >> k) & 1u) {
-        const line3 l = line_load(lines, n, i0 + k, s);
-        if (fresh) {
-          f = line_fp12(l);
-          fresh = false;
-        } else {
-          f = fp12_mul_by_line_i(f, l.a, l.b, l.c);
-        }
+    uint32_t k = 0;
+    if (fresh && nu) {
+      f = line_fp12(line_load(lines, n, i0 + (uidx & 15u), s));
+      fresh = false;
+      k = 1;
+    }
+    if (PAIRS) {
+      TB_NOUNROLL for (; k + 1 < nu; k += 2) {
+        const line3 l1 = line_load(lines, n, i0 + ((uidx >> (4 * k)) & 15u), s);
+        const line3 l2 = line_load(lines, n, i0 + ((uidx >> (4 * k + 4)) & 15u), s);
+        f = fp12_mul_by_line_pair_i(f, l1, l2);
       }
+    }
+    TB_NOUNROLL for (; k < nu; k++) {
+      const line3 l = line_load(lines, n, i0 + ((uidx >> (4 * k)) & 15u), s);
+      f = fp12_mul_by_line_i(f, l.a, l.b, l.c);
     }
   }
   f_out[(size_t)j * seg_stride + g] = fp12_conj(f);
+}
+
+extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_MIN_WAVES)
+    k_miller_accs(const uint4* __restrict__ lines, const uint8_t* __restrict__ skip, const uint8_t* __restrict__ code_a,
+                  const uint8_t* __restrict__ code_b, uint32_t n, uint32_t per, uint32_t nseg, uint32_t g_pad, fp12* __restrict__ f_out,
+                  uint32_t seg_stride) {
+  miller_accs_body<false>(lines, skip, code_a, code_b, n, per, nseg, g_pad, f_out, seg_stride);
+}
+
+// the same with the step's lines multiplied two at a time (fp12_mul_by_line_pair_i)
+extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_MIN_WAVES)
+    k_miller_accs_pairs(const uint4* __restrict__ lines, const uint8_t* __restrict__ skip, const uint8_t* __restrict__ code_a,
+                        const uint8_t* __restrict__ code_b, uint32_t n, uint32_t per, uint32_t nseg, uint32_t g_pad, fp12* __restrict__ f_out,
+                        uint32_t seg_stride) {
+  miller_accs_body<true>(lines, skip, code_a, code_b, n, per, nseg, g_pad, f_out, seg_stride);
 }

@@ -23,9 +23,11 @@ extern "C" unsigned long long tb_sqr_count;  // the squarings among them (301 vs
 extern "C" unsigned long long tb_fp2mul_count;  // lazy Fp2 products (3 M, 980 v_mad_u64_u32 each)
 #define TB_COUNT_MUL() (++tb_mul_count)
 #define TB_COUNT_SQR() (++tb_mul_count, ++tb_sqr_count)
+#define TB_COUNT_N(m, s) (tb_mul_count += (m) + (s), tb_sqr_count += (s))  // m products and s squarings of an fp_*_n batch
 #else
 #define TB_COUNT_MUL() ((void)0)
 #define TB_COUNT_SQR() ((void)0)
+#define TB_COUNT_N(m, s) ((void)0)
 #endif
 
 // ---------------------------------------------------------------------------

@@ -177,10 +177,10 @@ static void acc_plan(uint32_t n_main, uint32_t& per, uint32_t& nseg) {
   double best = 0;
   per = 1;
   nseg = 1;
-  for (uint32_t p : {1u, 2u, 4u, 8u}) {
-    if (e_per > 0 && (int)p != e_per) continue;
-    for (uint32_t sg : {1u, 2u, 4u}) {
-      if (e_seg > 0 && (int)sg != e_seg) continue;
+  for (uint32_t p = 1; p <= 8; p++) {  // 1, 2, 4, 8 (an override may force any count up to 8)
+    if (e_per > 0 ? (int)p != e_per : (p & (p - 1)) != 0) continue;
+    for (uint32_t sg = 1; sg <= 4; sg++) {
+      if (e_seg > 0 ? (int)sg != e_seg : sg == 3) continue;
       const double threads = (double)sg * ((n_main + p - 1) / p);
       const double rounds = std::max(1.0, std::ceil(threads / TB_ACC_FULL));
       const double cost = rounds * (68.0 / sg) * (12.0 + 13.0 * p);
@@ -226,7 +226,7 @@ struct pair_plan {
     if (wave)
       per = 1;
     else if (split)
-      acc_plan(n_main, per, nseg);
+      acc_plan(std::min(n_main, TB_LINE_CHUNK), per, nseg);  // the chunks launch one after another: plan one chunk's fill
     else
       per = n_pairs <= TB_MILLER1_MAX ? 1u : 2u;
     if (n_spread) nseg = 1;  // the spread extra lines need whole loops per thread
@@ -305,17 +305,17 @@ void launch_set_pk(hipStream_t s, uint32_t n, uint32_t n_entries, const uint32_t
                    uint32_t* mlist, uint32_t* mcnt, g1a* P2, const g1a* comb) {
   if (!n) return;
   const dim3 blk(TB_BLOCK), g((n + TB_BLOCK - 1) / TB_BLOCK);
-  const uint32_t multi = n_entries > n ? 1u : 0u;
+  // lane-cooperative aggregation (16 rows per set, k_kcoop.hip, with the
+  // set's -[r] g1); TBLS_AGG_COOP=0 selects the one-wave-per-set kernel (A/B)
+  static const bool agg_coop = !(getenv("TBLS_AGG_COOP") && getenv("TBLS_AGG_COOP")[0] == '0');
+  const uint32_t multi = n_entries > n ? (agg_coop ? 2u : 1u) : 0u;
   hipLaunchKernelGGL(k_set_pk, g, blk, 0, s, pk_off, aff, code, rand, n, P, set_code, n_bad, key_idx, tab_n, multi, P2, comb);
   if (!multi) return;
   (void)hipMemsetAsync(mcnt, 0, 4, s);
   hipLaunchKernelGGL(k_multi_list, g, blk, 0, s, pk_off, n, mlist, mcnt);
-  // lane-cooperative aggregation (16 rows per set, k_kcoop.hip); TBLS_AGG_COOP=0
-  // selects the one-wave-per-set kernel (A/B)
-  static const bool agg_coop = !(getenv("TBLS_AGG_COOP") && getenv("TBLS_AGG_COOP")[0] == '0');
   if (agg_coop)
     hipLaunchKernelGGL(k_set_pk_agg_coop, dim3(std::min<uint32_t>(n, 4096u)), dim3(256), 0, s, pk_off, aff, code, rand,
-                       (const uint32_t*)mlist, (const uint32_t*)mcnt, P, set_code, n_bad, key_idx, tab_n);
+                       (const uint32_t*)mlist, (const uint32_t*)mcnt, P, set_code, n_bad, key_idx, tab_n, P2, comb);
   else
     hipLaunchKernelGGL(k_set_pk_wave, dim3(std::min<uint32_t>(n, 4096u)), dim3(64), 0, s, pk_off, aff, code, rand,
                        (const uint32_t*)mlist, (const uint32_t*)mcnt, P, set_code, n_bad, key_idx, tab_n);
@@ -341,6 +341,15 @@ extern "C" __global__ void k_sig_check_coop(const uint8_t* __restrict__ sigs, ui
                                             uint8_t* __restrict__ sig_code, uint32_t* __restrict__ n_bad);  // k_kcoop.hip
 // small batches: lane-cooperative key and signature stages (k_kcoop.hip);
 // TBLS_KEYS_COOP=0 / TBLS_SIG_COOP=0 select the one-thread-per-item kernels (A/B)
+// two items per thread in the one-thread key / signature decompression
+// stages (k_pk_decompress2, k_sig_check2: both square-root chains
+// interleaved); TBLS_DEC2=1 selects them.  Measured and rejected as the
+// default (round 3, 131,072 sets): keys 3.47 -> 6.17 ms (spills, half the
+// waves), signatures 6.06 -> 6.00 ms; at 16,384 sets twice the latency.
+static bool dec2() {
+  static const bool v = getenv("TBLS_DEC2") && getenv("TBLS_DEC2")[0] == '1';
+  return v;
+}
 static bool keys_coop() {
   static const bool v = !(getenv("TBLS_KEYS_COOP") && getenv("TBLS_KEYS_COOP")[0] == '0');
   return v;
@@ -421,13 +430,19 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
   }
   TB_EV(4, ssig);
   if (n) {
-    if (pp.msm)
+    const dim3 g2((n + 1) / 2 / TB_BLOCK + 1);  // two sets per thread (k_sig_check2)
+    if (pp.msm && dec2())
+      hipLaunchKernelGGL(k_sig_check2, g2, blk, 0, ssig, b.sigs, n, (g2a*)(w + L.sig_aff), w + L.sig_use, w + L.sig_code,
+                         (uint32_t*)(w + L.n_bad), 0u);
+    else if (pp.msm)
       hipLaunchKernelGGL(k_sig_check, g, blk, 0, ssig, b.sigs, n, (g2a*)(w + L.sig_aff), w + L.sig_use, w + L.sig_code,
                          (uint32_t*)(w + L.n_bad), 0u);
     else if (n <= TB_HASH_WAVE_MAX && sig_coop())  // the same, 4 sets per wave, lane-cooperative
       hipLaunchKernelGGL(k_sig_check_coop, dim3((n + 3) / 4), dim3(64), 0, ssig, b.sigs, n, (g2a*)(Q + n), skip + n, w + L.sig_code,
                          (uint32_t*)(w + L.n_bad));
-    else  // the set's signature pair: Q[n + i] = sig_i, skip[n + i] = infinite / invalid
+    else if (dec2())  // the set's signature pair: Q[n + i] = sig_i, skip[n + i] = infinite / invalid
+      hipLaunchKernelGGL(k_sig_check2, g2, blk, 0, ssig, b.sigs, n, Q + n, skip + n, w + L.sig_code, (uint32_t*)(w + L.n_bad), 1u);
+    else
       hipLaunchKernelGGL(k_sig_check, g, blk, 0, ssig, b.sigs, n, Q + n, skip + n, w + L.sig_code, (uint32_t*)(w + L.n_bad), 1u);
   }
   TB_EV(5, ssig);
@@ -471,7 +486,10 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
     TB_EV(1, sa);
     TB_EV(2, sa);
   } else {
-    if (K) hipLaunchKernelGGL(k_pk_decompress, dim3((K + TB_BLOCK - 1) / TB_BLOCK), blk, 0, sa, b.pks, K, (g1a*)(w + L.pk_aff), w + L.pk_code);
+    if (K && dec2())
+      hipLaunchKernelGGL(k_pk_decompress2, dim3(((K + 1) / 2 + TB_BLOCK - 1) / TB_BLOCK), blk, 0, sa, b.pks, K, (g1a*)(w + L.pk_aff), w + L.pk_code);
+    else if (K)
+      hipLaunchKernelGGL(k_pk_decompress, dim3((K + TB_BLOCK - 1) / TB_BLOCK), blk, 0, sa, b.pks, K, (g1a*)(w + L.pk_aff), w + L.pk_code);
     TB_EV(1, sa);
     TB_EV(2, sa);
     launch_set_pk(sa, n, b.n_keys, b.pk_off, use_tab ? c.tab_aff.as<const g1a>() : (const g1a*)(w + L.pk_aff),
@@ -523,7 +541,9 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
         }
         if (pp.seg()) {  // segment-major values: segment j of group g at f[j * n_groups + g]
           const uint32_t g_pad = (mt + TB_BLOCK - 1) / TB_BLOCK * TB_BLOCK;
-          hipLaunchKernelGGL(k_miller_accs, dim3(pp.nseg * g_pad / TB_BLOCK), blk, 0, s, (const uint4*)lines, (const uint8_t*)skip + lo,
+          // TBLS_ACC_PAIRS=1: two lines per product (fp12_mul_by_line_pair_i: 23 vs 26 Fp2 products, more registers)
+          static const bool pairs = getenv("TBLS_ACC_PAIRS") && getenv("TBLS_ACC_PAIRS")[0] == '1';
+          hipLaunchKernelGGL(pairs ? k_miller_accs_pairs : k_miller_accs, dim3(pp.nseg * g_pad / TB_BLOCK), blk, 0, s, (const uint4*)lines, (const uint8_t*)skip + lo,
                              ca + lo, cb + lo, m, pp.per, pp.nseg, g_pad, f + lo / pp.per, pp.n_groups());
         } else {
           hipLaunchKernelGGL(pp.per == 2 ? k_miller_acc2 : k_miller_acc1, dim3((mt + TB_BLOCK - 1) / TB_BLOCK), blk, 0, s,
@@ -1572,6 +1592,14 @@ extern "C" int tbls_dev_batch_partial_timed(int device, const tbls_dev_batch* b,
 
 extern "C" int tbls_dev_batch_stage_profile(int device, const tbls_dev_batch* b, void* stream, void* partial_out, float* stage_ms) {
   return partial_timed(device, b, stream, partial_out, stage_ms, true);
+}
+
+extern "C" int tbls_acc_plan(uint32_t n, uint32_t* per, uint32_t* nseg, int* split) {
+  const pair_plan pp(n);
+  if (per) *per = pp.per;
+  if (nseg) *nseg = pp.nseg;
+  if (split) *split = pp.split ? 1 : 0;
+  return TBLS_SUCCESS;
 }
 
 // batched helpers for building synthetic workloads on the device

@@ -162,6 +162,7 @@ _SIGS = {
         ctypes.c_int,
         [ctypes.c_int, ctypes.POINTER(TblsDevBatch), ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_float)],
     ),
+    "tbls_acc_plan": (ctypes.c_int, [ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_int)]),
     "tbls_sk_to_pk_many": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p]),
     "tbls_sign_many": (
         ctypes.c_int,

@@ -3,7 +3,8 @@ product trees + k_fp12_seg_combine_coop) computes the same Fp12 product as the
 unsegmented k_miller_acc1 / acc2: the partial record of a seeded batch, its
 12 coordinates canonicalized mod p, is identical under every accumulator plan
 (TBLS_ACC_SEG=0: the unsegmented kernels; forced pairs-per-thread x segment
-counts; the default plan), on the per-set signature-pair path (3,000 sets) and
+counts; the default plan; TBLS_ACC_PAIRS=1, the two-line products, with an
+odd pair count), on the per-set signature-pair path (3,000 sets) and
 the bucket-sum path with the wave bit-sum pairs in the last segment (40,000
 sets).  Each plan runs in its own process (the plan is read once per process);
 the verdicts also go through the final exponentiation."""
@@ -20,7 +21,7 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 PLANS = [{"TBLS_ACC_SEG": "0"}, {}, {"TBLS_ACC_PER": "8", "TBLS_ACC_SEG": "4"}, {"TBLS_ACC_PER": "1", "TBLS_ACC_SEG": "2"},
-         {"TBLS_ACC_PER": "4", "TBLS_ACC_SEG": "1"}]
+         {"TBLS_ACC_PER": "4", "TBLS_ACC_SEG": "1"}, {"TBLS_ACC_PAIRS": "1"}, {"TBLS_ACC_PAIRS": "1", "TBLS_ACC_PER": "3", "TBLS_ACC_SEG": "2"}]
 
 
 def _record(n, env_extra, tamper=-1):

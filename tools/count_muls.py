@@ -91,6 +91,25 @@ def main():
     # k_miller2: two pairs per Fp12 accumulator -> work per pair = MILLER2 / 2
     pair = [enc_fp(a[0]) + enc_fp(a[1]) + enc_fp2(b[0]) + enc_fp2(b[1]) for a, b in zip(aff, q)]
     res["miller"] = per_unit("MILLER2", [pair[i] + pair[i + 1] for i in range(0, N, 2)], units_per_rec=2, name="miller")
+    # The split Miller loop's accumulator part per pair, for a plan of `per`
+    # pairs per thread and `nseg` loop segments (k_lines.hip k_miller_accs):
+    # fp12_sqr_i = 12 lazy Fp2 products (36 M), fp12_mul_by_line_i = 13 (39 M);
+    # a segment skips its first step's squaring (f = 1) and takes its first
+    # line as f.  MILLER2 (two pairs per accumulator, 62 squarings) minus its
+    # accumulator share plus the plan's; the segment products' Horner tail (<= 49
+    # Fp12 squarings per batch) is below 0.01 M per pair at 131,072 pairs.
+    X_ABS = 0xD201000000010000
+    dbl = []
+    for b in range(62, -1, -1):
+        dbl.append(1)
+        if (X_ABS >> b) & 1:
+            dbl.append(0)
+    SQR12, LINE12 = 36, 39
+    acc2 = (62 * SQR12) / 2 + 68 * LINE12
+    for per, nseg in ((1, 4), (2, 4), (4, 2), (4, 4), (8, 2), (8, 4)):
+        sq_ = sum(sum(dbl[68 * j // nseg:68 * (j + 1) // nseg]) - dbl[68 * j // nseg] for j in range(nseg))
+        accs = (sq_ * SQR12 + (per * 68 - nseg) * LINE12) / per
+        res[f"miller_seg_{per}x{nseg}"] = res["miller"] - acc2 + accs
     f = [tuple(tuple((i + j + k, 3 * i + 1) for k in range(3)) for j in range(2)) for i in range(2)]
     # one Fp12 product per accumulator, i.e. per two pairs
     res["fp12_prod"] = per_unit("FP12_MUL", [enc_fp12(f[0]) + enc_fp12(f[1])], units_per_rec=2, name="fp12_prod")
