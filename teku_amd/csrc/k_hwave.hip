@@ -67,11 +67,13 @@ struct hcoop_lds {
   g2a qm[2];
   g2j J;
   fp res[6];
+  g2a qa;  // the affine H(m) before [r] (rand != nullptr)
+  int ok;
 };
 
 extern "C" __global__ void __launch_bounds__(256)
     k_set_hash_coop(const uint8_t* __restrict__ msgs, const uint32_t* __restrict__ msg_off, const uint8_t* __restrict__ dst,
-                    uint32_t dlen, uint32_t n, g2a* __restrict__ Q, uint8_t* __restrict__ skip) {
+                    uint32_t dlen, uint32_t n, g2a* __restrict__ Q, uint8_t* __restrict__ skip, const uint64_t* __restrict__ rand) {
   __shared__ hcoop_lds L;
   const uint32_t i = blockIdx.x;
   if (i >= n) return;
@@ -127,7 +129,35 @@ extern "C" __global__ void __launch_bounds__(256)
       a.x = fp2_zero();
       a.y = fp2_zero();
     }
-    Q[i] = a;
+    if (rand && ok && rand[i] == 0) ok = false;  // [0] H(m): no pair
+    if (!rand || !ok || rand[i] == 1) Q[i] = a;
+    L.qa = a;
+    L.ok = ok ? 1 : 0;
     skip[i] = ok ? 0 : 1;
+  }
+  // Multi-key batches (tb_lib.hip launch_partial, r on G2): the set's
+  // randomizer multiplies H(m) here instead of the aggregate key (e(apk,
+  // [r] H) = e([r] apk, H)), on row 0 with coop mixed additions -- the hash
+  // stream has slack beside the key decompression + aggregation chain.  H(m)
+  // is in G2, so no multiple [k] H(m), 2 <= k < 2^64, meets an exceptional
+  // case (tb_ccurve.h).
+  if (rand) {
+    __syncthreads();
+    const uint64_t r = rand[i];
+    if (g == 0 && L.ok && r > 1) {
+      const crow::c2 one2 = {crow::from_const(R1), coop::c32(0)};
+      const coop::cj2 t = coop::mul_u64_aff(crow::from_fp2(L.qa.x), crow::from_fp2(L.qa.y), r, one2, K);
+      const crow::c2 zi = crow::inv(t.z, L.rb[0], K);
+      const crow::c2 zi2 = crow::sqr(zi, K);
+      const crow::c2 zi3 = crow::mul(zi2, zi, K);
+      const crow::c2 ax = crow::mul(t.x, zi2, K), ay = crow::mul(t.y, zi3, K);
+      const fp2 X = crow::to_fp2(ax, L.rb[0]), Y = crow::to_fp2(ay, L.rb[0]);
+      if (d == 0) {
+        g2a o;
+        o.x = X;
+        o.y = Y;
+        Q[i] = o;
+      }
+    }
   }
 }

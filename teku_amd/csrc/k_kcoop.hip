@@ -366,7 +366,8 @@ extern "C" __global__ void __launch_bounds__(256)
     k_set_pk_agg_coop(const uint32_t* __restrict__ pk_off, const g1a* __restrict__ pk_aff, const uint8_t* __restrict__ pk_code,
                       const uint64_t* __restrict__ rand, const uint32_t* __restrict__ list, const uint32_t* __restrict__ cnt,
                       g1a* __restrict__ P, uint8_t* __restrict__ set_code, uint32_t* __restrict__ n_bad,
-                      const uint32_t* __restrict__ key_idx, uint32_t tab_n, g1a* __restrict__ P2, const g1a* __restrict__ comb) {
+                      const uint32_t* __restrict__ key_idx, uint32_t tab_n, g1a* __restrict__ P2, const g1a* __restrict__ comb,
+                      uint32_t unit_r) {
   __shared__ ka_set S;
   tb_latency_prio();
   const int q = crow::row(), d = crow::dig();
@@ -468,7 +469,7 @@ extern "C" __global__ void __launch_bounds__(256)
       const coop::cj1 apk = {S.pt[0][0][d], S.pt[0][1][d], S.pt[0][2][d]};
       const c32 zv[1] = {apk.z};
       const bool zero = S.inf[0] != 0 || crow::zeros_n<1>(zv, S.zb[0]) != 0u;
-      const uint64_t rnd = rand[i];
+      const uint64_t rnd = unit_r ? 1ull : rand[i];  // unit_r: r multiplies H(m) instead (k_set_hash_coop)
       int code = S.bad;
       if (code == TB_SUCCESS && zero) {
         // infinity or an exceptional addition: the exact one-lane body
@@ -481,7 +482,7 @@ extern "C" __global__ void __launch_bounds__(256)
       } else if (code == TB_SUCCESS && rnd == 0) {
         code = TB_PK_IS_INFINITY;  // [0] apk (stage_set_pk_finish)
       } else if (code == TB_SUCCESS) {
-        const coop::cj1 t = coop::mul_u64(apk, rnd, K);
+        const coop::cj1 t = rnd == 1 ? apk : coop::mul_u64(apk, rnd, K);
         const c32 v1[1] = {t.z};
         crow::to_fp_n<1>(v1, S.zb[0], &S.inv[0]);
         if (d == 0) S.inv[0] = fp_inv(S.inv[0]);

@@ -56,12 +56,14 @@ extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_MIN_WAVES)
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint32_t b = pk_off[i], e = pk_off[i + 1];
-  // multi_wave 1: multi-key sets go to k_set_pk_wave (P2 here), 2: to
-  // k_set_pk_agg_coop (P2 there too)
-  if (P2 && !(multi_wave == 2 && e - b > 1)) P2[i] = neg_r_g1(comb, rand[i]);
-  if (multi_wave && e - b > 1) return;
+  // multi_wave & 3 == 1: multi-key sets go to k_set_pk_wave (P2 here), 2: to
+  // k_set_pk_agg_coop (P2 there too); bit 2: the batch's randomizers multiply
+  // H(m) on the G2 side (k_set_hash_coop), so P = apk
+  const uint32_t mw = multi_wave & 3u;
+  if (P2 && !(mw == 2 && e - b > 1)) P2[i] = neg_r_g1(comb, rand[i]);
+  if (mw && e - b > 1) return;
   g1a out;
-  int code = stage_set_pk(pk_aff, pk_code, b, e, rand[i], out, key_idx, tab_n);
+  int code = stage_set_pk(pk_aff, pk_code, b, e, (multi_wave & 4u) ? 1ull : rand[i], out, key_idx, tab_n);
   P[i] = out;
   if (code != TB_SUCCESS) {
     set_code[i] = (uint8_t)code;

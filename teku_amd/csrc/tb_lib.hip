@@ -302,20 +302,22 @@ struct ws_layout {
 // P2 (nullable): signature-pair points -[r_i] g1 (comb: the device's table).
 void launch_set_pk(hipStream_t s, uint32_t n, uint32_t n_entries, const uint32_t* pk_off, const g1a* aff, const uint8_t* code,
                    const uint64_t* rand, g1a* P, uint8_t* set_code, uint32_t* n_bad, const uint32_t* key_idx, uint32_t tab_n,
-                   uint32_t* mlist, uint32_t* mcnt, g1a* P2, const g1a* comb) {
+                   uint32_t* mlist, uint32_t* mcnt, g1a* P2, const g1a* comb, bool r_on_g2 = false) {
   if (!n) return;
   const dim3 blk(TB_BLOCK), g((n + TB_BLOCK - 1) / TB_BLOCK);
   // lane-cooperative aggregation (16 rows per set, k_kcoop.hip, with the
   // set's -[r] g1); TBLS_AGG_COOP=0 selects the one-wave-per-set kernel (A/B)
   static const bool agg_coop = !(getenv("TBLS_AGG_COOP") && getenv("TBLS_AGG_COOP")[0] == '0');
   const uint32_t multi = n_entries > n ? (agg_coop ? 2u : 1u) : 0u;
-  hipLaunchKernelGGL(k_set_pk, g, blk, 0, s, pk_off, aff, code, rand, n, P, set_code, n_bad, key_idx, tab_n, multi, P2, comb);
+  // r_on_g2: the randomizers multiply H(m) (k_set_hash_coop), P = apk here
+  hipLaunchKernelGGL(k_set_pk, g, blk, 0, s, pk_off, aff, code, rand, n, P, set_code, n_bad, key_idx, tab_n, multi | (r_on_g2 ? 4u : 0u), P2,
+                     comb);
   if (!multi) return;
   (void)hipMemsetAsync(mcnt, 0, 4, s);
   hipLaunchKernelGGL(k_multi_list, g, blk, 0, s, pk_off, n, mlist, mcnt);
   if (agg_coop)
     hipLaunchKernelGGL(k_set_pk_agg_coop, dim3(std::min<uint32_t>(n, 4096u)), dim3(256), 0, s, pk_off, aff, code, rand,
-                       (const uint32_t*)mlist, (const uint32_t*)mcnt, P, set_code, n_bad, key_idx, tab_n, P2, comb);
+                       (const uint32_t*)mlist, (const uint32_t*)mcnt, P, set_code, n_bad, key_idx, tab_n, P2, comb, r_on_g2 ? 1u : 0u);
   else
     hipLaunchKernelGGL(k_set_pk_wave, dim3(std::min<uint32_t>(n, 4096u)), dim3(64), 0, s, pk_off, aff, code, rand,
                        (const uint32_t*)mlist, (const uint32_t*)mcnt, P, set_code, n_bad, key_idx, tab_n);
@@ -326,7 +328,7 @@ extern "C" __global__ void k_set_hash_wave(const uint8_t* __restrict__ msgs, con
                                            uint8_t* __restrict__ skip);  // k_hwave.hip
 extern "C" __global__ void k_set_hash_coop(const uint8_t* __restrict__ msgs, const uint32_t* __restrict__ msg_off,
                                            const uint8_t* __restrict__ dst, uint32_t dlen, uint32_t n, g2a* __restrict__ Q,
-                                           uint8_t* __restrict__ skip);  // k_hwave.hip (lane-cooperative, 256 threads)
+                                           uint8_t* __restrict__ skip, const uint64_t* __restrict__ rand);  // k_hwave.hip (lane-cooperative, 256 threads)
 // small batches hash with the lane-cooperative kernel; TBLS_HASH_COOP=0 selects
 // the one-wave cofactor program (k_set_hash_wave) for A/B
 static bool hash_coop() {
@@ -402,10 +404,17 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
     HIPCHK(hipStreamWaitEvent(sb, c.e_fork, 0));
     HIPCHK(hipStreamWaitEvent(sh, c.e_fork, 0));
   }
+  // TBLS_R_ON_G2=1 (A/B, multi-key batches of the coop-hash size): the
+  // randomizers multiply H(m) on the hash stream (k_set_hash_coop) instead of
+  // the aggregate keys.  Measured and rejected (round 3, 64 x 488 keys): the
+  // aggregation stage 1.06 -> 0.48 ms, but the coop G2 scalar multiplication
+  // lengthens the hash 1.82 -> 3.19 ms and the partial 4.70 -> 6.13 ms.
+  static const bool r_g2_env = getenv("TBLS_R_ON_G2") && getenv("TBLS_R_ON_G2")[0] == '1';
+  const bool r_on_g2 = r_g2_env && b.n_keys > n && n && n <= TB_HASH_WAVE_MAX && hash_coop();
   auto launch_hash = [&]() -> int {
     TB_EV(6, sh);
     if (n && n <= TB_HASH_WAVE_MAX && hash_coop())  // one 256-thread workgroup per set: coop SSWU chains and cofactor program
-      hipLaunchKernelGGL(k_set_hash_coop, dim3(n), dim3(256), 0, sh, b.msgs, b.msg_off, dst, dlen, n, Q, skip);
+      hipLaunchKernelGGL(k_set_hash_coop, dim3(n), dim3(256), 0, sh, b.msgs, b.msg_off, dst, dlen, n, Q, skip, r_on_g2 ? b.rand : nullptr);
     else if (n && n <= TB_HASH_WAVE_MAX)  // one workgroup per set: the cofactor clearing lane-parallel
       hipLaunchKernelGGL(k_set_hash_wave, dim3(n), dim3(128), 0, sh, b.msgs, b.msg_off, dst, dlen, n, Q, skip);
     else if (n)
@@ -495,7 +504,7 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
     launch_set_pk(sa, n, b.n_keys, b.pk_off, use_tab ? c.tab_aff.as<const g1a>() : (const g1a*)(w + L.pk_aff),
                   use_tab ? c.tab_code.as<const uint8_t>() : (const uint8_t*)(w + L.pk_code), b.rand, P, w + L.set_code,
                   (uint32_t*)(w + L.n_bad), key_idx, use_tab ? c.tab_n : 0u, (uint32_t*)(w + L.mlist), (uint32_t*)(w + L.mcnt),
-                  pp.msm ? nullptr : P + n, c.comb.as<const g1a>());
+                  pp.msm ? nullptr : P + n, c.comb.as<const g1a>(), r_on_g2);
   }
   TB_EV(3, sa);
   HIPCHK(hipEventRecord(c.e_join[0], sa));

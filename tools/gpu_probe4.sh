@@ -1,0 +1,12 @@
+#!/bin/bash
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+P="timeout -k 10 180 python tools/probe.py"
+{
+$P multikey 64 488 6 &&
+TBLS_R_ON_G2=0 $P multikey 64 488 6 &&
+$P multikey 64 512 6
+} > gpurun_out/probe4.log 2>&1 || { tail -5 gpurun_out/probe4.log; exit 1; }
+grep "^{" gpurun_out/probe4.log

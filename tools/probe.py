@@ -33,8 +33,10 @@ def main():
     else:
         s, k = int(sys.argv[2]), int(sys.argv[3])
         reps = int(sys.argv[4]) if len(sys.argv) > 4 else 5
+        r1 = len(sys.argv) > 5 and sys.argv[5] == "r1"  # randomizers 1: no [r] apk scalar multiplication
         keys, msgs, sigs = synth.multi_key(s, k, first_key=1000, seed=3)
-        db = bench.DevBatch(b"".join(b"".join(x) for x in keys), [k] * s, b"".join(msgs), [32] * s, b"".join(sigs), device)
+        db = bench.DevBatch(b"".join(b"".join(x) for x in keys), [k] * s, b"".join(msgs), [32] * s, b"".join(sigs), device,
+                            rands=[1] * s if r1 else None)
     part = torch.empty(native.PARTIAL_BYTES, dtype=torch.uint8, device=device)
     st = (ctypes.c_float * 8)()
     ts, stages = [], []
