@@ -336,25 +336,35 @@ extern "C" __global__ void __launch_bounds__(64)
 
 // ---------------------------------------------------------------------------
 // Multi-key sets (configs 2/3: 488-512 keys per set; BlstPublicKey.aggregate,
-// BlstPublicKey.java:55-71), lane-cooperative: one 256-thread workgroup (16
-// rows) per set of the compacted list.  Row q sums the set's keys q, q + 16,
-// ... with coop mixed additions, the 16 row sums meet in a 4-level LDS tree of
-// coop general additions, and row 0 forms P = [r] apk (coop, Jacobian input)
-// with one lane-0 inversion.  The coop additions have no exceptional-case
-// branches: a sum that meets P == +-Q (a repeated key, or keys cancelling)
-// ends with Z = 0 and stays there through every later addition, so Z = 0 of
-// the aggregate sends the set to lane 0's one-lane body (stage_set_pk: exact,
-// and infinity -> PK_IS_INFINITY).  For a finite aggregate of group points no
-// multiple [k] apk, 2 <= k < 2^64, meets +-apk (tb_ccurve.h), so [r] apk is
+// BlstPublicKey.java:55-71), lane-cooperative: one 512-thread workgroup (32
+// rows, 256 registers each) per set of the compacted list.
+//   * row q sums the set's keys q, q + 32, ... with coop mixed additions, and
+//     the 32 row sums meet in a 5-level LDS tree of coop additions;
+//   * P = [r] apk by nibbles: row w < 16 forms [r_w] (2^(4w) apk) (4w
+//     doublings, then a 4-bit double-and-add), the 16 terms meet in a 4-level
+//     tree -- the critical path is the 63 doublings of row 15 plus 7 additions
+//     instead of 63 doublings and ~32 additions in one chain;
+//   * row 16 (wave 4, beside it): the set's signature-pair point -[r] g1 from
+//     the comb (P2, when given); both points affine with one lane-0
+//     inversion each.
+// The coop additions have no exceptional-case branches: a sum that meets
+// P == +-Q (a repeated key, or keys cancelling) ends with Z = 0 and stays
+// there through every later addition, so Z = 0 of the aggregate sends the set
+// to lane 0's one-lane body (stage_set_pk: exact, and infinity ->
+// PK_IS_INFINITY).  For a finite aggregate of group points the nibble terms
+// [k 2^(4w)] apk (1 <= k <= 15) and their partial sums over disjoint nibbles
+// never meet +-each other (distinct multiples below 2^64 < r), so [r] apk is
 // exact.  Same outputs as k_set_pk_wave.
 // ---------------------------------------------------------------------------
+#define KA_ROWS 32
 struct ka_set {
-  int32_t pt[16][3][16];  // row sums (X, Y, Z digits)
-  uint32_t inf[16];
-  int32_t zb[2][4][16];   // row 0 ([r] apk) and row 4 (-[r] g1)
+  int32_t pt[KA_ROWS][3][16];  // row sums (X, Y, Z digits), then the nibble terms
+  uint32_t inf[KA_ROWS];
+  int32_t zb[2][4][16];        // row 0 ([r] apk) and row 16 (-[r] g1)
   fp inv[2];
   fp out[2][2];
   int bad;
+  int mode;  // 0: nibble [r] apk, 1: one-lane fallback, 2: the set fails (code in bad)
 };
 
 __device__ TB_NOINLINE int ka_set_generic(const g1a* pk_aff, const uint8_t* pk_code, uint32_t b, uint32_t e, uint64_t r, g1a& o,
@@ -362,7 +372,47 @@ __device__ TB_NOINLINE int ka_set_generic(const g1a* pk_aff, const uint8_t* pk_c
   return stage_set_pk(pk_aff, pk_code, b, e, r, o, key_idx, tab_n);
 }
 
-extern "C" __global__ void __launch_bounds__(256)
+// rows q < rows hold points (pt, inf); tree them into row 0 (all threads call)
+__device__ TB_INLINE void ka_tree(ka_set& S, int rows, int q, int d, const coop::cctx& K) {
+  for (int s = rows / 2; s > 0; s >>= 1) {
+    coop::cj1 acc = {c32(0), c32(0), c32(0)};
+    if (q < s && S.inf[q + s] == 0) {
+      const coop::cj1 o = {S.pt[q + s][0][d], S.pt[q + s][1][d], S.pt[q + s][2][d]};
+      if (S.inf[q] == 0) {
+        const coop::cj1 m = {S.pt[q][0][d], S.pt[q][1][d], S.pt[q][2][d]};
+        acc = coop::add(m, o, K);
+      } else {
+        acc = o;
+      }
+    }
+    __syncthreads();
+    if (q < s && S.inf[q + s] == 0) {
+      S.pt[q][0][d] = acc.x;
+      S.pt[q][1][d] = acc.y;
+      S.pt[q][2][d] = acc.z;
+      if (d == 0) S.inf[q] = 0u;
+    }
+    __syncthreads();
+  }
+}
+
+// (X, Y, Z) -> affine into out[0..1] with one lane-0 inversion (zb, inv: the row's buffers)
+__device__ TB_INLINE void ka_affine(const coop::cj1& t, int32_t (*zb)[16], fp& inv, fp* out, int d, const coop::cctx& K) {
+  const c32 v1[1] = {t.z};
+  crow::to_fp_n<1>(v1, zb, &inv);
+  if (d == 0) inv = fp_inv(inv);
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  const c32 i1 = crow::from_fp(inv);
+  const c32 i2 = coop::csqr(i1, K);
+  c32 a3[2] = {t.x, i2}, b3[2] = {i2, i1}, i3[2];
+  coop::cmul_n<2>(i3, a3, b3, K);  // X / Z^2, 1 / Z^3
+  const c32 y = coop::cmul(t.y, i3[1], K);
+  const c32 v2[2] = {i3[0], y};
+  crow::to_fp_n<2>(v2, zb, out);
+}
+
+extern "C" __global__ void __launch_bounds__(KA_ROWS * 16)
     k_set_pk_agg_coop(const uint32_t* __restrict__ pk_off, const g1a* __restrict__ pk_aff, const uint8_t* __restrict__ pk_code,
                       const uint64_t* __restrict__ rand, const uint32_t* __restrict__ list, const uint32_t* __restrict__ cnt,
                       g1a* __restrict__ P, uint8_t* __restrict__ set_code, uint32_t* __restrict__ n_bad,
@@ -376,12 +426,13 @@ extern "C" __global__ void __launch_bounds__(256)
   const uint32_t total = cnt[0];
   for (uint32_t w = blockIdx.x; w < total; w += gridDim.x) {
     const uint32_t i = list[w], b = pk_off[i], e = pk_off[i + 1];
+    const uint64_t rnd = unit_r ? 1ull : rand[i];  // unit_r: r multiplies H(m) instead (k_set_hash_coop)
     if (threadIdx.x == 0) S.bad = TB_SUCCESS;
     __syncthreads();
     // ---- row sums (row-uniform control flow: every lane of a row walks the same keys)
     coop::cj1 acc = {c32(0), c32(0), c32(0)};
     bool inf = true;
-    for (uint32_t j = b + (uint32_t)q; j < e; j += 16) {
+    for (uint32_t j = b + (uint32_t)q; j < e; j += KA_ROWS) {
       uint32_t k;
       if (!set_key(key_idx, tab_n, j, k)) {
         S.bad = TB_BAD_ENCODING;
@@ -402,37 +453,33 @@ extern "C" __global__ void __launch_bounds__(256)
     S.pt[q][2][d] = acc.z;
     if (d == 0) S.inf[q] = inf ? 1u : 0u;
     __syncthreads();
-    // ---- 4-level tree over the rows
-    for (int s = 8; s > 0; s >>= 1) {
-      if (q < s) {
-        const bool pi = S.inf[q] != 0, qi = S.inf[q + s] != 0;
-        if (!qi) {
-          const coop::cj1 o = {S.pt[q + s][0][d], S.pt[q + s][1][d], S.pt[q + s][2][d]};
-          if (!pi) {
-            const coop::cj1 m = {S.pt[q][0][d], S.pt[q][1][d], S.pt[q][2][d]};
-            acc = coop::add(m, o, K);
-          } else {
-            acc = o;
-          }
+    ka_tree(S, KA_ROWS, q, d, K);
+    // ---- the aggregate: exceptional / infinite -> one-lane body; invalid key or r = 0 -> fail
+    if (q == 0) {
+      const c32 zv[1] = {S.pt[0][2][d]};
+      const bool zero = S.inf[0] != 0 || crow::zeros_n<1>(zv, S.zb[0]) != 0u;
+      if (d == 0) {
+        int mode = 0;
+        if (S.bad != TB_SUCCESS) {
+          mode = 2;
+        } else if (zero) {
+          mode = 1;
+        } else if (rnd == 0) {
+          S.bad = TB_PK_IS_INFINITY;  // [0] apk (stage_set_pk_finish)
+          mode = 2;
         }
+        S.mode = mode;
       }
-      __syncthreads();
-      if (q < s && S.inf[q + s] == 0) {
-        S.pt[q][0][d] = acc.x;
-        S.pt[q][1][d] = acc.y;
-        S.pt[q][2][d] = acc.z;
-        if (d == 0) S.inf[q] = 0u;
-      }
-      __syncthreads();
     }
-    // ---- row 0: the aggregate, [r] apk, affine; row 4 (wave 1, beside it):
-    // the set's signature-pair point -[r] g1 from the comb (P2, when given)
-    if (q == 4 && P2) {
-      const uint64_t rnd = rand[i];
+    __syncthreads();
+    const int mode = S.mode;
+    // ---- row 16: -[r] g1 (one mixed addition per nonzero byte of r: neg_r_g1)
+    if (q == 16 && P2) {
+      const uint64_t rr = rand[i];
       coop::cj1 cacc = {one, one, c32(0)};
       bool cinf = true;
-      for (int k = 0; k < 8; k++) {  // one mixed addition per nonzero byte of r (neg_r_g1)
-        const uint32_t dg = (uint32_t)(rnd >> (8 * k)) & 255u;
+      for (int k = 0; k < 8; k++) {
+        const uint32_t dg = (uint32_t)(rr >> (8 * k)) & 255u;
         if (dg) {
           const g1a* cq = comb + k * 256 + dg;
           const c32 qx = crow::from_fp(cq->x), qy = crow::from_fp(cq->y);
@@ -444,20 +491,7 @@ extern "C" __global__ void __launch_bounds__(256)
           }
         }
       }
-      if (!cinf) {
-        const c32 v1[1] = {cacc.z};
-        crow::to_fp_n<1>(v1, S.zb[1], &S.inv[1]);
-        if (d == 0) S.inv[1] = fp_inv(S.inv[1]);
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-        const c32 i1 = crow::from_fp(S.inv[1]);
-        const c32 i2 = coop::csqr(i1, K);
-        c32 a3[2] = {cacc.x, i2}, b3[2] = {i2, i1}, i3[2];
-        coop::cmul_n<2>(i3, a3, b3, K);
-        const c32 y = coop::cmul(cacc.y, i3[1], K);
-        const c32 v2[2] = {i3[0], y};
-        crow::to_fp_n<2>(v2, S.zb[1], S.out[1]);
-      }
+      if (!cinf) ka_affine(cacc, S.zb[1], S.inv[1], S.out[1], d, K);
       if (d == 0) {
         g1a o;
         o.x = cinf ? fp_zero() : S.out[1][0];
@@ -465,38 +499,43 @@ extern "C" __global__ void __launch_bounds__(256)
         P2[i] = o;
       }
     }
-    if (q == 0) {
-      const coop::cj1 apk = {S.pt[0][0][d], S.pt[0][1][d], S.pt[0][2][d]};
-      const c32 zv[1] = {apk.z};
-      const bool zero = S.inf[0] != 0 || crow::zeros_n<1>(zv, S.zb[0]) != 0u;
-      const uint64_t rnd = unit_r ? 1ull : rand[i];  // unit_r: r multiplies H(m) instead (k_set_hash_coop)
-      int code = S.bad;
-      if (code == TB_SUCCESS && zero) {
-        // infinity or an exceptional addition: the exact one-lane body
-        if (d == 0) {
-          g1a o;
-          code = ka_set_generic(pk_aff, pk_code, b, e, rnd, o, key_idx, tab_n);
-          S.out[0][0] = o.x;
-          S.out[0][1] = o.y;
+    // ---- [r] apk by nibbles on rows 0..15
+    coop::cj1 t = {c32(0), c32(0), c32(0)};
+    bool tinf = true;
+    if (mode == 0 && q < 16) {
+      const uint32_t nib = (uint32_t)(rnd >> (4 * q)) & 15u;
+      if (nib) {
+        coop::cj1 a = {S.pt[0][0][d], S.pt[0][1][d], S.pt[0][2][d]};
+        for (int k = 0; k < 4 * q; k++) a = coop::dbl(a, K);  // 2^(4q) apk
+        t = a;
+        for (int bit = 31 - __builtin_clz(nib) - 1; bit >= 0; --bit) {
+          t = coop::dbl(t, K);
+          if ((nib >> bit) & 1u) t = coop::add(t, a, K);
         }
-      } else if (code == TB_SUCCESS && rnd == 0) {
-        code = TB_PK_IS_INFINITY;  // [0] apk (stage_set_pk_finish)
-      } else if (code == TB_SUCCESS) {
-        const coop::cj1 t = rnd == 1 ? apk : coop::mul_u64(apk, rnd, K);
-        const c32 v1[1] = {t.z};
-        crow::to_fp_n<1>(v1, S.zb[0], &S.inv[0]);
-        if (d == 0) S.inv[0] = fp_inv(S.inv[0]);
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-        const c32 i1 = crow::from_fp(S.inv[0]);
-        const c32 i2 = coop::csqr(i1, K);
-        c32 a3[2] = {t.x, i2}, b3[2] = {i2, i1}, i3[2];
-        coop::cmul_n<2>(i3, a3, b3, K);  // X / Z^2, 1 / Z^3
-        const c32 y = coop::cmul(t.y, i3[1], K);
-        const c32 v2[2] = {i3[0], y};
-        crow::to_fp_n<2>(v2, S.zb[0], S.out[0]);
+        tinf = false;
       }
-      if (d == 0) {  // lane 0's code is the set's in every branch
+    }
+    __syncthreads();  // every row has read the aggregate
+    if (mode == 0 && q < 16) {
+      S.pt[q][0][d] = t.x;
+      S.pt[q][1][d] = t.y;
+      S.pt[q][2][d] = t.z;
+      if (d == 0) S.inf[q] = tinf ? 1u : 0u;
+    }
+    __syncthreads();
+    if (mode == 0) ka_tree(S, 16, q, d, K);
+    if (q == 0) {
+      int code = S.bad;
+      if (mode == 0) {
+        const coop::cj1 rp = {S.pt[0][0][d], S.pt[0][1][d], S.pt[0][2][d]};
+        ka_affine(rp, S.zb[0], S.inv[0], S.out[0], d, K);
+      } else if (mode == 1 && d == 0) {  // infinity or an exceptional addition: the exact one-lane body
+        g1a o;
+        code = ka_set_generic(pk_aff, pk_code, b, e, rnd, o, key_idx, tab_n);
+        S.out[0][0] = o.x;
+        S.out[0][1] = o.y;
+      }
+      if (d == 0) {  // lane 0's code is the set's in every mode
         g1a o;
         o.x = fp_zero();
         o.y = fp_zero();

@@ -210,6 +210,15 @@ static uint32_t seg_dpack(uint32_t nseg) {
   return pack;
 }
 
+// the segmented accumulator kernel: TBLS_ACC_PAIRS=1 two lines per product
+// (fp12_mul_by_line_pair_i: 23 vs 26 Fp2 products, more registers)
+typedef void (*accs_fn)(const uint4*, const uint8_t*, const uint8_t*, const uint8_t*, uint32_t, uint32_t, uint32_t, uint32_t, fp12*,
+                        uint32_t);
+static accs_fn accs_kernel() {
+  static const bool pairs = getenv("TBLS_ACC_PAIRS") && getenv("TBLS_ACC_PAIRS")[0] == '1';
+  return pairs ? k_miller_accs_pairs : k_miller_accs;
+}
+
 struct pair_plan {
   uint32_t n, n_extra, n_pairs, n_main, n_spread, n_xwave, per, nseg;
   bool msm, wave, split;
@@ -230,9 +239,29 @@ struct pair_plan {
     else
       per = n_pairs <= TB_MILLER1_MAX ? 1u : 2u;
     if (n_spread) nseg = 1;  // the spread extra lines need whole loops per thread
+    // TBLS_HALVES=1 (A/B; per-set signature pairs, below TB_MSM_MIN sets): the
+    // n signature pairs' Miller loops as a launch of their own, queued on the
+    // signature stream once the signatures and -[r] g1 exist -- beside
+    // hash_to_G2, which their pairs do not need -- and the n set pairs after
+    // the hash.  Measured and rejected (round 3, 16,384 sets): partial 12.88
+    // vs 12.91 ms (one plan for both halves), 13.47 ms (each half planned for
+    // n pairs): the set pairs' line chain after the hash is the critical path
+    // either way, and the side launch competes with the hash.
+    static const bool halves_env = getenv("TBLS_HALVES") && getenv("TBLS_HALVES")[0] == '1';
+    halves = halves_env && split && !msm && seg() && n_main == 2 * n;
+    if (halves) {  // each half is a launch of n pairs: plan its fill
+      uint32_t p2 = per, s2 = nseg;
+      acc_plan(n, p2, s2);
+      if (p2 > 2 || s2 > 1) {
+        per = p2;
+        nseg = s2;
+      }
+    }
   }
+  bool halves = false;
   bool seg() const { return split && (nseg > 1 || per > 2); }  // k_miller_accs
-  uint32_t n_groups() const { return (n_main + per - 1) / per; }
+  uint32_t half_groups() const { return (n + per - 1) / per; }
+  uint32_t n_groups() const { return halves ? 2 * half_groups() : (n_main + per - 1) / per; }
   uint32_t n_f_main() const { return nseg * n_groups(); }
   uint32_t n_f() const { return n_f_main() + n_xwave; }  // Miller values: accumulators (segment-major), then the wave pairs'
   uint32_t line_pairs() const { return split ? std::min(n_main, TB_LINE_CHUNK) : 0u; }
@@ -316,7 +345,7 @@ void launch_set_pk(hipStream_t s, uint32_t n, uint32_t n_entries, const uint32_t
   (void)hipMemsetAsync(mcnt, 0, 4, s);
   hipLaunchKernelGGL(k_multi_list, g, blk, 0, s, pk_off, n, mlist, mcnt);
   if (agg_coop)
-    hipLaunchKernelGGL(k_set_pk_agg_coop, dim3(std::min<uint32_t>(n, 4096u)), dim3(256), 0, s, pk_off, aff, code, rand,
+    hipLaunchKernelGGL(k_set_pk_agg_coop, dim3(std::min<uint32_t>(n, 4096u)), dim3(512), 0, s, pk_off, aff, code, rand,
                        (const uint32_t*)mlist, (const uint32_t*)mcnt, P, set_code, n_bad, key_idx, tab_n, P2, comb, r_on_g2 ? 1u : 0u);
   else
     hipLaunchKernelGGL(k_set_pk_wave, dim3(std::min<uint32_t>(n, 4096u)), dim3(64), 0, s, pk_off, aff, code, rand,
@@ -464,7 +493,8 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
   // (one 64-lane launch of ~2.5 ms): it waits on e_sig, and only the
   // accumulator launch that absorbs the extra lines waits on e_join[1].
   const bool late_join = !serial && pp.msm && pp.split;
-  if (late_join && !chain) HIPCHK(hipEventRecord(c.e_sig, sb));
+  const bool early_sig = !serial && pp.halves;  // the signature pairs' Miller loops on sb (pair_plan halves)
+  if ((late_join && !chain) || early_sig) HIPCHK(hipEventRecord(c.e_sig, sb));
   TB_EV(8, sb);
   if (pp.msm) {
     hipLaunchKernelGGL(k_msm_bucket, dim3(TB_MSM_PARTS / TB_BLOCK), blk, 0, sb, (const g2a*)(w + L.sig_aff), (const uint8_t*)(w + L.sig_use),
@@ -481,6 +511,20 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
   }
   TB_EV(9, sb);
   HIPCHK(hipEventRecord(c.e_join[1], sb));
+  // one half of a halves plan: lines + segmented accumulator of m = n pairs
+  // from pair offset `off` into the group range [goff, goff + half_groups)
+  auto launch_half = [&](hipStream_t st, uint32_t off, uint32_t goff, uint4* lbuf) {
+    const uint8_t* ca = w + L.set_code;
+    const uint8_t* cb = w + L.sig_code;
+    const uint32_t m = n, mt = pp.half_groups();
+    hipLaunchKernelGGL(k_miller_lines, dim3((m + TB_BLOCK - 1) / TB_BLOCK), blk, 0, st, (const g1a*)P + off, (const g2a*)Q + off,
+                       (const uint8_t*)skip + off, ca + off, cb + off, m, lbuf);
+    const uint32_t g_pad = (mt + TB_BLOCK - 1) / TB_BLOCK * TB_BLOCK;
+    hipLaunchKernelGGL(accs_kernel(), dim3(pp.nseg * g_pad / TB_BLOCK), blk, 0, st, (const uint4*)lbuf, (const uint8_t*)skip + off,
+                       ca + off, cb + off, m, pp.per, pp.nseg, g_pad, (fp12*)(w + L.f) + goff, pp.n_groups());
+  };
+  uint4* lines_a = (uint4*)(w + L.lines);
+  uint4* lines_b = (uint4*)(w + L.lines + (size_t)n * TB_LINE_BYTES_PER_PAIR);
   // --- stream a: public keys, [r] apk (+ -[r] g1 for the signature pairs) -----
   TB_EV(0, sa);
   if (b.n_keys == n && n && n <= TB_HASH_WAVE_MAX && keys_coop()) {
@@ -508,6 +552,11 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
   }
   TB_EV(3, sa);
   HIPCHK(hipEventRecord(c.e_join[0], sa));
+  if (early_sig) {  // the signature pairs (-[r_i] g1, sig_i): keys' P2 + the signature stage, beside the hash
+    HIPCHK(hipStreamWaitEvent(sb, c.e_join[0], 0));
+    launch_half(sb, n, pp.half_groups(), lines_b);
+    HIPCHK(hipEventRecord(c.e_join[1], sb));
+  }
   // --- high-priority stream: hash_to_G2 per set -------------------------------
   // The longest per-set stage (2 wave rounds at 131k sets): with queue
   // priority its waves are dispatched first and the shorter key / signature
@@ -522,11 +571,11 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
     HIPCHK(hipStreamWaitEvent(s, c.e_join[2], 0));
   }
   HIPCHK(hipStreamWaitEvent(s, c.e_join[0], 0));
-  if (!late_join)
+  if (!late_join && !early_sig)
     HIPCHK(hipStreamWaitEvent(s, c.e_join[1], 0));
   else if (!chain)
-    HIPCHK(hipStreamWaitEvent(s, c.e_sig, 0));
-  bool joined = !late_join;
+    HIPCHK(hipStreamWaitEvent(s, c.e_sig, 0));  // the set pairs' lines read the signature codes
+  bool joined = !late_join && !early_sig;
   // --- Miller loops of all pairs (pairs of invalid sets contribute 1) ---------
   const uint32_t np = pp.n_pairs, nf = pp.n_f();
   TB_EV(10, s);
@@ -536,7 +585,10 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
     fp12* f = (fp12*)(w + L.f);
     if (pp.wave)
       hipLaunchKernelGGL(k_miller_wave, dim3(np), dim3(64), 0, s, (const g1a*)P, (const g2a*)Q, (const uint8_t*)skip, ca, cb, np, f);
-    else if (pp.split) {
+    else if (pp.halves) {  // the set pairs (after the hash); the signature pairs ran on sb (or run here when serial)
+      launch_half(s, 0, 0, lines_a);
+      if (!early_sig) launch_half(s, n, pp.half_groups(), lines_b);
+    } else if (pp.split) {
       // chunks of the main pairs; the spread pairs' lines (xlines) are absorbed by the last chunk
       uint4* lines = (uint4*)(w + L.lines);
       for (uint32_t lo = 0; lo < pp.n_main; lo += TB_LINE_CHUNK) {
@@ -551,8 +603,7 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
         if (pp.seg()) {  // segment-major values: segment j of group g at f[j * n_groups + g]
           const uint32_t g_pad = (mt + TB_BLOCK - 1) / TB_BLOCK * TB_BLOCK;
           // TBLS_ACC_PAIRS=1: two lines per product (fp12_mul_by_line_pair_i: 23 vs 26 Fp2 products, more registers)
-          static const bool pairs = getenv("TBLS_ACC_PAIRS") && getenv("TBLS_ACC_PAIRS")[0] == '1';
-          hipLaunchKernelGGL(pairs ? k_miller_accs_pairs : k_miller_accs, dim3(pp.nseg * g_pad / TB_BLOCK), blk, 0, s, (const uint4*)lines, (const uint8_t*)skip + lo,
+          hipLaunchKernelGGL(accs_kernel(), dim3(pp.nseg * g_pad / TB_BLOCK), blk, 0, s, (const uint4*)lines, (const uint8_t*)skip + lo,
                              ca + lo, cb + lo, m, pp.per, pp.nseg, g_pad, f + lo / pp.per, pp.n_groups());
         } else {
           hipLaunchKernelGGL(pp.per == 2 ? k_miller_acc2 : k_miller_acc1, dim3((mt + TB_BLOCK - 1) / TB_BLOCK), blk, 0, s,

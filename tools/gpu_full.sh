@@ -7,7 +7,7 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 SETS=${SETS:-131072}
-PARGS="--steps 1 --warmup 0 --sets-per-gpu $SETS --lat-reps 0 --no-cpu-baseline --no-1m"
+PARGS="--steps 1 --warmup 0 --sets-per-gpu $SETS --lat-reps 0 --no-cpu-baseline --no-1m --no-extra --no-kzg"
 echo "== pytest -m gpu" && timeout -k 10 900 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; rc=$?; tail -4 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
 echo "== bench" && timeout -k 10 600 python bench.py --sets-per-gpu $SETS > gpurun_out/bench.json 2> gpurun_out/bench.err; rc=$?; cat gpurun_out/bench.json; tail -3 gpurun_out/bench.err; [ $rc -eq 0 ] || exit $rc
 [ -n "$NOPROF" ] && exit 0
