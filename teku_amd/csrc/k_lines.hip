@@ -373,10 +373,11 @@ __device__ TB_INLINE bool step_is_dbl(int s) { return ((s < 64 ? (DBL_STEPS.lo >
 __device__ TB_INLINE fp12 line_fp12(const line3& l) { return {{l.a, l.b, fp2_zero()}, {fp2_zero(), l.c, fp2_zero()}}; }
 }  // namespace
 
-template <bool PAIRS>
+template <bool PAIRS, bool LDSF = false>
 __device__ TB_INLINE void miller_accs_body(const uint4* __restrict__ lines, const uint8_t* __restrict__ skip,
                                            const uint8_t* __restrict__ code_a, const uint8_t* __restrict__ code_b, uint32_t n, uint32_t per,
-                                           uint32_t nseg, uint32_t g_pad, fp12* __restrict__ f_out, uint32_t seg_stride) {
+                                           uint32_t nseg, uint32_t g_pad, fp12* __restrict__ f_out, uint32_t seg_stride,
+                                           fp12* fsh = nullptr) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t j = t / g_pad, g = t % g_pad;
   const uint32_t G = (n + per - 1) / per;
@@ -388,7 +389,9 @@ __device__ TB_INLINE void miller_accs_body(const uint4* __restrict__ lines, cons
     const uint32_t i = i0 + k;
     if (i < n && skip[i] == 0 && code_a[i] == 0 && code_b[i] == 0) usem |= 1u << k;
   }
-  fp12 f = fp12_one();
+  fp12 freg;
+  fp12& f = LDSF ? fsh[threadIdx.x] : freg;  // LDSF: the accumulator lives in LDS, not in 144 registers
+  f = fp12_one();
   bool fresh = true;  // f == 1
   // the used pairs' offsets, packed 4 bits each (line products in pairs, TB_ACC_PAIRS)
   uint32_t uidx = 0, nu = 0;
@@ -430,4 +433,16 @@ extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_MIN_WAVES)
                         const uint8_t* __restrict__ code_b, uint32_t n, uint32_t per, uint32_t nseg, uint32_t g_pad, fp12* __restrict__ f_out,
                         uint32_t seg_stride) {
   miller_accs_body<true>(lines, skip, code_a, code_b, n, per, nseg, g_pad, f_out, seg_stride);
+}
+
+// the accumulator f in LDS (576 B per thread, 36.9 KB per 64-thread block;
+// four blocks per CU fit the 160 KB): the register file then holds only the
+// products' operands and temporaries (A/B against scratch spills,
+// TBLS_ACC_LDS=1)
+extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_MIN_WAVES)
+    k_miller_accs_lds(const uint4* __restrict__ lines, const uint8_t* __restrict__ skip, const uint8_t* __restrict__ code_a,
+                      const uint8_t* __restrict__ code_b, uint32_t n, uint32_t per, uint32_t nseg, uint32_t g_pad, fp12* __restrict__ f_out,
+                      uint32_t seg_stride) {
+  __shared__ fp12 fsh[TB_BLOCK];
+  miller_accs_body<false, true>(lines, skip, code_a, code_b, n, per, nseg, g_pad, f_out, seg_stride, fsh);
 }

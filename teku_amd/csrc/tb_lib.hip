@@ -216,7 +216,8 @@ typedef void (*accs_fn)(const uint4*, const uint8_t*, const uint8_t*, const uint
                         uint32_t);
 static accs_fn accs_kernel() {
   static const bool pairs = getenv("TBLS_ACC_PAIRS") && getenv("TBLS_ACC_PAIRS")[0] == '1';
-  return pairs ? k_miller_accs_pairs : k_miller_accs;
+  static const bool lds = getenv("TBLS_ACC_LDS") && getenv("TBLS_ACC_LDS")[0] == '1';
+  return pairs ? k_miller_accs_pairs : (lds ? k_miller_accs_lds : k_miller_accs);
 }
 
 struct pair_plan {

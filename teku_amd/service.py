@@ -30,13 +30,13 @@ exceptionally with BlsException (BLS.batchVerify throws, BLS.java:235-237).
 """
 
 import queue
-import secrets
 import threading
 from concurrent.futures import Future
 from typing import Callable, List, Optional, Sequence
 
 from . import bls as _bls
-from .synth import SetArray
+from . import native
+from .synth import SetArray, fast_multipliers
 
 DEFAULT_MIN_BATCH_SIZE_TO_SPLIT = 25  # AggregatingSignatureVerificationService.java:42
 DEFAULT_MAX_BATCH_SIZE = 16384
@@ -62,10 +62,10 @@ def _set_tuple(pks, msg, sig):
     return (blob, len(pks), bytes(msg), sigb)
 
 
-def _hip_batch(sets) -> bool:
-    rands = [int.from_bytes(secrets.token_bytes(8), "big") or 1 for _ in sets]  # BlstBLS12381.java:191-195
+def _hip_batch(sets, timing=None) -> bool:
+    rands = fast_multipliers(len(sets))  # BlstBLS12381.java:191-195 (nextBatchRandomMultiplier), one CSPRNG call
     try:
-        return SetArray.from_tuples(sets).batch_verify(rands)
+        return SetArray.from_tuples(sets).batch_verify(rands, timing=timing)
     except ValueError:  # an empty key list in the batch: settle it per set
         return False
 
@@ -99,6 +99,13 @@ class AggregatingSignatureVerificationService:
         self.task_count = 0
         self.batch_sizes: List[int] = []
         self.device_passes = 0
+        # device metrics beside the reference's: per batch
+        # pass, the library's tbls_timing (kernel pipeline ms over the devices,
+        # host ms API entry -> verdict, devices used)
+        self.sets_verified = 0
+        self.device_ms_total = 0.0
+        self.host_ms_total = 0.0
+        self.last_batch_timing: Optional[dict] = None
 
     # -- Service lifecycle -------------------------------------------------
     def start(self):
@@ -181,7 +188,7 @@ class AggregatingSignatureVerificationService:
         if not tasks:
             return
         self.device_passes += 1
-        if self._batch_fn(all_sets):
+        if self._batch_timed(all_sets):
             for t in tasks:
                 t.result.set_result(True)
             return
@@ -198,6 +205,38 @@ class AggregatingSignatureVerificationService:
             n = len(t.sets)
             t.result.set_result(all(verdicts[k : k + n]))
             k += n
+
+    def _batch_timed(self, sets) -> bool:
+        """One batch pass, with the device timing when the default batch
+        function runs (a custom batch_fn is timed on the host only)."""
+        if self._batch_fn is not _hip_batch:
+            return self._batch_fn(sets)
+        t = native.TblsTiming()
+        ok = _hip_batch(sets, timing=t)
+        self.sets_verified += len(sets)
+        self.device_ms_total += t.device_ms
+        self.host_ms_total += t.total_ms
+        self.last_batch_timing = {"sets": len(sets), "device_ms": t.device_ms, "total_ms": t.total_ms, "n_devices": t.n_devices}
+        return ok
+
+    def metrics(self) -> dict:
+        """The reference's executor metrics (AggregatingSignatureVerificationService.java:76-98:
+        signature_verifications_queue_size, _batch_count_total, _task_count_total,
+        _batch_size histogram) and the device's: sets verified per second of
+        kernel time (summed over devices) and of host wall time, the last
+        batch's timing."""
+        return {
+            "signature_verifications_queue_size": self.queue_size(),
+            "signature_verifications_batch_count_total": self.batch_count,
+            "signature_verifications_task_count_total": self.task_count,
+            "signature_verifications_batch_size": list(self.batch_sizes),
+            "device_passes_total": self.device_passes,
+            "device_sets_verified_total": self.sets_verified,
+            "device_kernel_ms_total": self.device_ms_total,
+            "device_sets_per_s": self.sets_verified / (self.device_ms_total * 1e-3) if self.device_ms_total > 0 else None,
+            "host_sets_per_s": self.sets_verified / (self.host_ms_total * 1e-3) if self.host_ms_total > 0 else None,
+            "last_batch": self.last_batch_timing,
+        }
 
     def _split(self, tasks: List[SignatureTask]):
         """The reference's fallback (l.208-227): halve down to

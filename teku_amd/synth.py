@@ -176,14 +176,14 @@ class SetArray:
         return cls(b"".join(s[0] for s in sets), [s[1] for s in sets], b"".join(s[2] for s in sets), [len(s[2]) for s in sets],
                    b"".join(s[3] for s in sets))
 
-    def batch_verify(self, rands: Sequence[int], n_gpus: int = 0) -> bool:
+    def batch_verify(self, rands: Sequence[int], n_gpus: int = 0, timing: "native.TblsTiming" = None) -> bool:
         if isinstance(rands, np.ndarray):  # uint64 array (fast_multipliers): passed in place
             assert rands.dtype == np.uint64 and rands.flags.c_contiguous and len(rands) >= self.n
             rr = rands.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))
         else:
             rr = (ctypes.c_uint64 * max(1, self.n))(*rands)
         ok = ctypes.c_int(0)
-        rc = native.lib().tbls_batch_verify(self.ptr, self.n, rr, n_gpus, ctypes.byref(ok), None)
+        rc = native.lib().tbls_batch_verify(self.ptr, self.n, rr, n_gpus, ctypes.byref(ok), ctypes.byref(timing) if timing is not None else None)
         if rc == native.BAD_ARGUMENT:
             raise ValueError("empty public key list in batch")
         native.check(rc, "tbls_batch_verify")

@@ -126,6 +126,8 @@ def test_config4_16k_through_service(S):
     assert got == exp
     assert [i for i, v in enumerate(got) if not v] == sorted(bad)
     assert svc.device_passes == 2
+    m = svc.metrics()  # device metrics from the library's tbls_timing
+    assert m["device_sets_verified_total"] == n and m["device_sets_per_s"] > 0 and m["last_batch"]["n_devices"] >= 1
 
 
 N5, SHARD5 = 1048576, 131072  # config 5: 8 GPUs x 131,072 sets

@@ -68,6 +68,10 @@ def test_valid_and_invalid_tasks_one_batch(keyset):
     svc.batch_verify_signatures(ts)
     assert [t.result.result() for t in ts] == [i not in bad for i in range(12)]
     assert calls == {"batch": 1, "each": 1}  # one failed batch -> one per-set pass, no halving
+    m = svc.metrics()  # the reference's executor metrics (AggregatingSignatureVerificationService.java:76-98)
+    assert m["signature_verifications_batch_count_total"] == 1 and m["signature_verifications_task_count_total"] == 12
+    assert m["signature_verifications_batch_size"] == [12] and m["device_passes_total"] == 2
+    assert m["device_sets_per_s"] is None  # a custom batch_fn has no device timing
     assert svc.batch_count == 1 and svc.task_count == 12
 
 
