@@ -237,6 +237,27 @@ extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_LINES_WAVES)
   }
 }
 
+// the same with the pair's G1 point and the twist point T in LDS (A/B
+// against scratch spills, TBLS_LINES_LDS=1)
+extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_LINES_WAVES)
+    k_miller_lines_lds(const g1a* __restrict__ P, const g2a* __restrict__ Q, const uint8_t* __restrict__ skip,
+                       const uint8_t* __restrict__ code_a, const uint8_t* __restrict__ code_b, uint32_t n, uint4* __restrict__ lines) {
+  __shared__ g1a psh[TB_BLOCK];
+  __shared__ g2p tsh[TB_BLOCK];
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  if (skip[i] != 0 || code_a[i] != 0 || code_b[i] != 0) return;
+  g1a& p = psh[threadIdx.x];
+  g2p& T = tsh[threadIdx.x];
+  p = P[i];
+  T = {Q[i].x, Q[i].y, fp2_one()};
+  int s = 0;
+  TB_NOUNROLL for (int b = 62; b >= 0; --b) {
+    line_store(lines, n, i, s++, dbl_step_f(T, p));
+    if ((X_ABS >> b) & 1) line_store(lines, n, i, s++, add_step_f(T, Q[i], p));
+  }
+}
+
 // Thread t accumulates the main pairs PER t .. PER t + PER - 1 (< n; their
 // lines in `lines`, stride n) and, at each step s, at most one line of the
 // n_extra pairs in `xlines` (stride n_extra; the signature side's bit-sum

@@ -220,6 +220,13 @@ static accs_fn accs_kernel() {
   return pairs ? k_miller_accs_pairs : (lds ? k_miller_accs_lds : k_miller_accs);
 }
 
+// the line kernel: TBLS_LINES_LDS=1 keeps P and T in LDS (k_miller_lines_lds)
+typedef void (*lines_fn)(const g1a*, const g2a*, const uint8_t*, const uint8_t*, const uint8_t*, uint32_t, uint4*);
+static lines_fn lines_kernel() {
+  static const bool lds = getenv("TBLS_LINES_LDS") && getenv("TBLS_LINES_LDS")[0] == '1';
+  return lds ? k_miller_lines_lds : k_miller_lines;
+}
+
 struct pair_plan {
   uint32_t n, n_extra, n_pairs, n_main, n_spread, n_xwave, per, nseg;
   bool msm, wave, split;
@@ -518,7 +525,7 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
     const uint8_t* ca = w + L.set_code;
     const uint8_t* cb = w + L.sig_code;
     const uint32_t m = n, mt = pp.half_groups();
-    hipLaunchKernelGGL(k_miller_lines, dim3((m + TB_BLOCK - 1) / TB_BLOCK), blk, 0, st, (const g1a*)P + off, (const g2a*)Q + off,
+    hipLaunchKernelGGL(lines_kernel(), dim3((m + TB_BLOCK - 1) / TB_BLOCK), blk, 0, st, (const g1a*)P + off, (const g2a*)Q + off,
                        (const uint8_t*)skip + off, ca + off, cb + off, m, lbuf);
     const uint32_t g_pad = (mt + TB_BLOCK - 1) / TB_BLOCK * TB_BLOCK;
     hipLaunchKernelGGL(accs_kernel(), dim3(pp.nseg * g_pad / TB_BLOCK), blk, 0, st, (const uint4*)lbuf, (const uint8_t*)skip + off,
@@ -595,7 +602,7 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
       for (uint32_t lo = 0; lo < pp.n_main; lo += TB_LINE_CHUNK) {
         const uint32_t m = std::min(TB_LINE_CHUNK, pp.n_main - lo), mt = (m + pp.per - 1) / pp.per;
         const uint32_t ex = lo + m == pp.n_main ? pp.n_spread : 0u;
-        hipLaunchKernelGGL(k_miller_lines, dim3((m + TB_BLOCK - 1) / TB_BLOCK), blk, 0, s, (const g1a*)P + lo, (const g2a*)Q + lo,
+        hipLaunchKernelGGL(lines_kernel(), dim3((m + TB_BLOCK - 1) / TB_BLOCK), blk, 0, s, (const g1a*)P + lo, (const g2a*)Q + lo,
                            (const uint8_t*)skip + lo, ca + lo, cb + lo, m, lines);
         if (ex && !joined) {  // this accumulator launch reads the extra pairs' lines and skip flags
           HIPCHK(hipStreamWaitEvent(s, c.e_join[1], 0));

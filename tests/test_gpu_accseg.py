@@ -22,7 +22,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 PLANS = [{"TBLS_ACC_SEG": "0"}, {}, {"TBLS_ACC_PER": "8", "TBLS_ACC_SEG": "4"}, {"TBLS_ACC_PER": "1", "TBLS_ACC_SEG": "2"},
          {"TBLS_ACC_PER": "4", "TBLS_ACC_SEG": "1"}, {"TBLS_ACC_PAIRS": "1"}, {"TBLS_ACC_PAIRS": "1", "TBLS_ACC_PER": "3", "TBLS_ACC_SEG": "2"},
-         {"TBLS_HALVES": "1"}, {"TBLS_HALVES": "1", "TBLS_ACC_PER": "3", "TBLS_ACC_SEG": "4"}, {"TBLS_ACC_PER": "3", "TBLS_ACC_SEG": "4"}]
+         {"TBLS_HALVES": "1"}, {"TBLS_HALVES": "1", "TBLS_ACC_PER": "3", "TBLS_ACC_SEG": "4"}, {"TBLS_ACC_PER": "3", "TBLS_ACC_SEG": "4"},
+         {"TBLS_ACC_LDS": "1", "TBLS_LINES_LDS": "1"}, {"TBLS_ACC_LDS": "1", "TBLS_ACC_PER": "2", "TBLS_ACC_SEG": "2"}]
 
 
 def _record(n, env_extra, tamper=-1):
