@@ -404,10 +404,14 @@ __device__ TB_INLINE void miller_accs_body(const uint4* __restrict__ lines, cons
   const uint32_t G = (n + per - 1) / per;
   if (j >= nseg || g >= G) return;
   const int s_lo = (int)(TB_LINE_STEPS * j / nseg), s_hi = (int)(TB_LINE_STEPS * (j + 1) / nseg);
-  const uint32_t i0 = per * g;
+  // group g owns pairs g, g + G, g + 2G, ...: the lanes of a wave then read
+  // consecutive pairs' lines (one 1 KB transaction per 16-byte group) instead
+  // of pairs `per` apart (a 128-byte line per lane, each line re-fetched per
+  // pair: 24 GB per 131k launch at per = 8, profiles/r03_probe_*)
+  const uint32_t i0 = g;
   uint32_t usem = 0;
   for (uint32_t k = 0; k < per; k++) {
-    const uint32_t i = i0 + k;
+    const uint32_t i = g + k * G;
     if (i < n && skip[i] == 0 && code_a[i] == 0 && code_b[i] == 0) usem |= 1u << k;
   }
   fp12 freg;
@@ -422,19 +426,19 @@ __device__ TB_INLINE void miller_accs_body(const uint4* __restrict__ lines, cons
     if (!fresh && step_is_dbl(s)) f = fp12_sqr_i(f);
     uint32_t k = 0;
     if (fresh && nu) {
-      f = line_fp12(line_load(lines, n, i0 + (uidx & 15u), s));
+      f = line_fp12(line_load(lines, n, i0 + (uidx & 15u) * G, s));
       fresh = false;
       k = 1;
     }
     if (PAIRS) {
       TB_NOUNROLL for (; k + 1 < nu; k += 2) {
-        const line3 l1 = line_load(lines, n, i0 + ((uidx >> (4 * k)) & 15u), s);
-        const line3 l2 = line_load(lines, n, i0 + ((uidx >> (4 * k + 4)) & 15u), s);
+        const line3 l1 = line_load(lines, n, i0 + ((uidx >> (4 * k)) & 15u) * G, s);
+        const line3 l2 = line_load(lines, n, i0 + ((uidx >> (4 * k + 4)) & 15u) * G, s);
         f = fp12_mul_by_line_pair_i(f, l1, l2);
       }
     }
     TB_NOUNROLL for (; k < nu; k++) {
-      const line3 l = line_load(lines, n, i0 + ((uidx >> (4 * k)) & 15u), s);
+      const line3 l = line_load(lines, n, i0 + ((uidx >> (4 * k)) & 15u) * G, s);
       f = fp12_mul_by_line_i(f, l.a, l.b, l.c);
     }
   }
