@@ -96,8 +96,9 @@ def plan_counts(S):
             mads["miller"] = round(mads["miller"] + d / 3 * mc.get("mads_per_fp2_mul", 980))
         mc["mads_per_unit"] = mads
     kern = dict(STAGE_KERNEL)
+    lines_k = "k_miller_lines" if os.environ.get("TBLS_LINES_LDS", "1") == "0" else "k_miller_lines_lds"
     if seg:
-        kern["miller"] = "k_miller_lines + k_miller_accs"
+        kern["miller"] = f"{lines_k} + k_miller_accs"
     return mc, kern, {"per": per, "nseg": nseg, "kernel": "k_miller_accs" if seg else "k_miller_acc1/2"}
 
 
@@ -487,12 +488,16 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(True)
+    for _ in range(args.steps):  # the plain partial: no stage events inside the timed region
+        step(args.serial)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    stage_steps = 2 if not args.serial else args.steps  # the overlapped stage times from two event-timed steps after it
+    if not args.serial:
+        for _ in range(stage_steps):
+            step(True)
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -569,7 +574,7 @@ def main():
         del b1m
         batch = DevBatch(pks, [1] * S, msgs, [32] * S, sigs, device)  # the profiled steps below use the 131k shard
 
-    stage_ms = [a / args.steps for a in stage_acc]
+    stage_ms = [a / stage_steps for a in stage_acc]
     # Exclusive per-stage kernel times (every stage alone on the stream): the
     # roofline's denominators.  In the timed steps the stages overlap, so
     # their event brackets include each other's work.
