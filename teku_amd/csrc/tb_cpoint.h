@@ -232,6 +232,57 @@ TBC_FN cj2 mul_u64_aff(const c2& qx, const c2& qy, uint64_t k, const c2& one, co
   return r;
 }
 
+// add-2007-bl over Fp2 (the G1 add above), 5 product levels
+TBC_FN cj2 add(const cj2& p, const cj2& q, const cctx& K) {
+  c2 m1[2], s1[2];
+  {
+    const c2 am[2] = {p.y, q.y}, bm[2] = {q.z, p.z}, as[2] = {p.z, q.z};
+    f2_round<2, 2>(m1, am, bm, s1, as, K);  // Y1 Z2, Y2 Z1; Z1Z1, Z2Z2
+  }
+  const c2 Z1Z1 = s1[0], Z2Z2 = s1[1];
+  c2 m2[4];
+  {
+    const c2 am[4] = {p.x, q.x, m1[0], m1[1]}, bm[4] = {Z2Z2, Z1Z1, Z2Z2, Z1Z1};
+    f2_round<4, 0>(m2, am, bm, nullptr, nullptr, K);  // U1, U2, S1, S2
+  }
+  const c2 U1 = m2[0], S1 = m2[2];
+  const c2 H = norm(sub(m2[1], U1));
+  const c2 S = sub(m2[3], S1);
+  const c2 rr = norm(add(S, S));
+  c2 s3[3];
+  {
+    const c2 as[3] = {norm(add(H, H)), rr, norm(add(p.z, q.z))};
+    f2_round<0, 3>(nullptr, nullptr, nullptr, s3, as, K);  // I, rr^2, (Z1 + Z2)^2
+  }
+  const c2 I = s3[0];
+  c2 m4[3];
+  {
+    const c2 am[3] = {H, U1, norm(sub(sub(s3[2], Z1Z1), Z2Z2))}, bm[3] = {I, I, H};
+    f2_round<3, 0>(m4, am, bm, nullptr, nullptr, K);  // J, V, Z3
+  }
+  cj2 r;
+  r.x = norm(sub(sub(sub(s3[1], m4[0]), m4[1]), m4[1]));
+  c2 m5[2];
+  {
+    const c2 am[2] = {rr, S1}, bm[2] = {norm(sub(m4[1], r.x)), m4[0]};
+    f2_round<2, 0>(m5, am, bm, nullptr, nullptr, K);
+  }
+  r.y = norm(sub(sub(m5[0], m5[1]), m5[1]));
+  r.z = m4[2];
+  return r;
+}
+
+// [k]q for Jacobian q, k >= 1, MSB first (k uniform over the row)
+TBC_FN cj2 mul_u64(const cj2& q, uint64_t k, const cctx& K) {
+  cj2 r = q;
+  const int top = 63 - __builtin_clzll(k);
+  TB_NOUNROLL for (int i = top - 1; i >= 0; --i) {
+    r = dbl(r, K);
+    if ((k >> i) & 1) r = add(r, q, K);
+  }
+  return r;
+}
+
 
 }  // namespace coop
 }  // namespace tb

@@ -104,7 +104,11 @@ __device__ TB_INLINE fp2 to_fp2(const c2& a, rowbuf& B) {
 // a^-1 in Fp2: conj(a) / N(a), the Fp inversion on the row's lane 0
 __device__ TB_INLINE c2 inv(const c2& a, rowbuf& B, const cctx& K) {
   const fp n = to_fp(norm2(a, K), B.d, &B.f);
+#if defined(TB_ROW_INV_INLINE)  // k_hrow.hip: keep the kernel's 256-register bound
+  if (dig() == 0) B.f = fp_inv_body(n);
+#else
   if (dig() == 0) B.f = fp_inv(n);
+#endif
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
   const c32 ni = from_fp(B.f);

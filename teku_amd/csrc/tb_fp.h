@@ -422,7 +422,7 @@ TB_HD TB_INLINE fp bez_update(const fp& x, int32_t f, const fp& y, int32_t g) {
   return r;
 }
 
-TB_HD TB_NOINLINE fp fp_inv(fp A) {
+TB_HD TB_INLINE fp fp_inv_body(fp A) {
   A = fp_canon(A);
   uint32_t a[12], b[12];
   TB_UNROLL for (int i = 0; i < 12; i++) {
@@ -490,6 +490,9 @@ TB_HD TB_NOINLINE fp fp_inv(fp A) {
   fp r = fp_mul(v, fp_from_const(INV_CORR));
   return zero ? fp_zero() : r;
 }
+// outlined form (the one-lane kernels); fp_inv_body inlines it where a
+// kernel's register bound must cover the inversion too (k_hrow.hip)
+TB_HD TB_NOINLINE fp fp_inv(fp A) { return fp_inv_body(A); }
 // a^e for a fixed exponent given as a sliding-window schedule (w = 4,
 // tools/gen_constants.py window_schedule): 375 squarings + 86 multiplications
 // for the 379-bit square-root exponents, vs 378 + 228 for binary.

@@ -21,6 +21,7 @@
 
 #include "../../include/tekubls.h"
 #include "tb_kdecl.h"
+#include "tb_hrow.h"
 #include "tb_host.h"
 
 static_assert(TB_PARTIAL_BYTES == TBLS_PARTIAL_BYTES, "partial record size");
@@ -277,9 +278,19 @@ struct pair_plan {
   uint32_t line_pairs() const { return split ? std::min(n_main, TB_LINE_CHUNK) : 0u; }
 };
 
+// hash_to_G2 on one coop row per set (k_hrow.hip) for batches above the
+// workgroup-per-set kernels' range and up to TBLS_HASH_ROW_MAX sets (default
+// TB_HASH_ROW_MAX); 0 disables it (A/B).  Above it the one-lane k_set_hash.
+#define TB_HASH_ROW_MAX 4096u
+static uint32_t hash_row_max() {
+  static const uint32_t v = getenv("TBLS_HASH_ROW_MAX") ? (uint32_t)atoi(getenv("TBLS_HASH_ROW_MAX")) : TB_HASH_ROW_MAX;
+  return v;
+}
+static bool hash_row(uint32_t n) { return n > TB_HASH_WAVE_MAX && n <= hash_row_max(); }
+
 struct ws_layout {
   size_t pk_aff, pk_code, P, Q, skip, set_code, sig_code, f, fpart, fpart2, segv, n_bad, result;
-  size_t sig_aff, sig_use, msm_cnt, msm_off, msm_cur, msm_idx, msm_part, msm_sum, mlist, mcnt, lines, xlines, total;
+  size_t sig_aff, sig_use, msm_cnt, msm_off, msm_cur, msm_idx, msm_part, msm_sum, mlist, mcnt, lines, xlines, hrow, total;
   uint32_t nb_f;
   ws_layout() : total(0) {}
   ws_layout(const pair_plan& pp, uint32_t K) {
@@ -306,6 +317,7 @@ struct ws_layout {
     msm_sum = o;  o = align_up(o + (msm ? (size_t)TB_MSM_BUCKETS * sizeof(g2j) : 0));
     mlist = o;    o = align_up(o + (size_t)n * 4);
     mcnt = o;     o = align_up(o + 4);
+    hrow = o;     o = align_up(o + (hash_row(n) ? (size_t)n * sizeof(hrow_set) : 0));
     lines = o;    o = align_up(o + (size_t)pp.line_pairs() * TB_LINE_BYTES_PER_PAIR);
     xlines = o;   o = align_up(o + (size_t)pp.n_spread * TB_LINE_BYTES_PER_PAIR);
     f = o;        o = align_up(o + (size_t)(nf ? nf : 1) * sizeof(fp12));
@@ -456,6 +468,15 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
       hipLaunchKernelGGL(k_set_hash_coop, dim3(n), dim3(256), 0, sh, b.msgs, b.msg_off, dst, dlen, n, Q, skip, r_on_g2 ? b.rand : nullptr);
     else if (n && n <= TB_HASH_WAVE_MAX)  // one workgroup per set: the cofactor clearing lane-parallel
       hipLaunchKernelGGL(k_set_hash_wave, dim3(n), dim3(128), 0, sh, b.msgs, b.msg_off, dst, dlen, n, Q, skip);
+    else if (hash_row(n)) {  // one coop row per set (k_hrow.hip): five launches
+      static const int force_fix = getenv("TBLS_HROW_FORCE_FIX") && getenv("TBLS_HROW_FORCE_FIX")[0] == '1';
+      hrow_set* H = (hrow_set*)(w + L.hrow);
+      hipLaunchKernelGGL(k_hrow_field, g, blk, 0, sh, b.msgs, b.msg_off, dst, dlen, n, H);
+      hipLaunchKernelGGL(k_hrow_sswu, dim3((2 * n + 3) / 4), dim3(64), 0, sh, n, H);
+      hipLaunchKernelGGL(k_hrow_iso, g, blk, 0, sh, n, H);
+      hipLaunchKernelGGL(k_hrow_cof, dim3((n + 3) / 4), dim3(64), 0, sh, n, (const hrow_set*)H, Q, skip, force_fix);
+      hipLaunchKernelGGL(k_hrow_fix, g, blk, 0, sh, n, (const hrow_set*)H, Q, skip);
+    }
     else if (n)
       hipLaunchKernelGGL(k_set_hash, g, blk, 0, sh, b.msgs, b.msg_off, dst, dlen, n, Q, skip);
     TB_EV(7, sh);
