@@ -319,7 +319,10 @@ def extra_configs(device, stream, reps):
         "sets_per_s": 64 / (statistics.median(lat) * 1e-3),
         "p50_ms_key_table": statistics.median(lat_tab),
         "sets_per_s_key_table": 64 / (statistics.median(lat_tab) * 1e-3),
-        "aggregation_kernel": "k_set_pk_wave (one 64-lane wave per set: strided mixed adds, LDS tree, [r] apk)",
+        "aggregation_kernel": ("k_set_pk_wave (one 64-lane wave per set: strided mixed adds, LDS tree, [r] apk)"
+                               if os.environ.get("TBLS_AGG_COOP") == "0" else
+                               "k_set_pk_agg_coop (32 coop rows per set: row sums of mixed adds, LDS tree, [r] apk by nibbles on "
+                               "16 rows, -[r] g1 on row 17; critical path: the 60 doublings to 2^60 apk)"),
         "aggregation_ms": agg_ms,
         "aggregation_frac": (agg_m * MAC_PER_M * 64 / (agg_ms * 1e-3)) / peak if agg_m and agg_ms > 0 else None,
         "aggregation_fp_products_per_set": agg_m,

@@ -43,8 +43,7 @@ extern "C" __global__ void __launch_bounds__(TB_BLOCK)
 }
 
 // map m = 2 i + j of set i on row m mod 4 of workgroup m / 4
-extern "C" __global__ void __launch_bounds__(64, 2) k_hrow_sswu(uint32_t n, hrow_set* __restrict__ H) {
-  __shared__ crow::rowbuf rb[4];
+__device__ TB_INLINE void hrow_sswu_body(uint32_t n, hrow_set* __restrict__ H, crow::rowbuf* rb) {
   const int g = crow::row(), d = crow::dig();
   const uint32_t m = blockIdx.x * 4u + (uint32_t)g;
   if (m >= 2u * n) return;  // whole rows leave: the row ops are row-local
@@ -53,6 +52,16 @@ extern "C" __global__ void __launch_bounds__(64, 2) k_hrow_sswu(uint32_t n, hrow
   const g2a q = crow::sswu(h.u[m & 1u], rb[g], K);
   if (d == 0) h.qm[m & 1u] = q;
 }
+// register bounds for 2 / 3 / 4 waves per SIMD (k_hrow_sswu: 228 / 168 + 148 B
+// scratch / 128 + 272 B); tb_lib.hip picks one (TBLS_HROW_WAVES)
+#define TB_HROW_SSWU(NAME, W)                                                                        \
+  extern "C" __global__ void __launch_bounds__(64, W) NAME(uint32_t n, hrow_set* __restrict__ H) { \
+    __shared__ crow::rowbuf rb[4];                                                                   \
+    hrow_sswu_body(n, H, rb);                                                                        \
+  }
+TB_HROW_SSWU(k_hrow_sswu, 2)
+TB_HROW_SSWU(k_hrow_sswu3, 3)
+TB_HROW_SSWU(k_hrow_sswu4, 4)
 
 extern "C" __global__ void __launch_bounds__(TB_BLOCK) k_hrow_iso(uint32_t n, hrow_set* __restrict__ H) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -79,9 +88,8 @@ __device__ TB_INLINE cj2 cpsi2(const cj2& p, const cctx& K) {
 }  // namespace
 
 // force_fix (tests): every set takes the k_hrow_fix path
-extern "C" __global__ void __launch_bounds__(64, 2)
-    k_hrow_cof(uint32_t n, const hrow_set* __restrict__ H, g2a* __restrict__ Q, uint8_t* __restrict__ skip, int force_fix) {
-  __shared__ crow::rowbuf rb[4];
+__device__ TB_INLINE void hrow_cof_body(uint32_t n, const hrow_set* __restrict__ H, g2a* __restrict__ Q, uint8_t* __restrict__ skip,
+                                        int force_fix, crow::rowbuf* rb) {
   const int g = crow::row(), d = crow::dig();
   const uint32_t i = blockIdx.x * 4u + (uint32_t)g;
   if (i >= n) return;
@@ -113,6 +121,16 @@ extern "C" __global__ void __launch_bounds__(64, 2)
     skip[i] = 0;
   }
 }
+
+// 2 / 3 waves per SIMD (256 + 236 B scratch / 168 + 656 B)
+#define TB_HROW_COF(NAME, W)                                                                                       \
+  extern "C" __global__ void __launch_bounds__(64, W)                                                              \
+      NAME(uint32_t n, const hrow_set* __restrict__ H, g2a* __restrict__ Q, uint8_t* __restrict__ skip, int force_fix) { \
+    __shared__ crow::rowbuf rb[4];                                                                                 \
+    hrow_cof_body(n, H, Q, skip, force_fix, rb);                                                                   \
+  }
+TB_HROW_COF(k_hrow_cof, 2)
+TB_HROW_COF(k_hrow_cof3, 3)
 
 extern "C" __global__ void __launch_bounds__(TB_BLOCK)
     k_hrow_fix(uint32_t n, const hrow_set* __restrict__ H, g2a* __restrict__ Q, uint8_t* __restrict__ skip) {

@@ -472,9 +472,11 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
       static const int force_fix = getenv("TBLS_HROW_FORCE_FIX") && getenv("TBLS_HROW_FORCE_FIX")[0] == '1';
       hrow_set* H = (hrow_set*)(w + L.hrow);
       hipLaunchKernelGGL(k_hrow_field, g, blk, 0, sh, b.msgs, b.msg_off, dst, dlen, n, H);
-      hipLaunchKernelGGL(k_hrow_sswu, dim3((2 * n + 3) / 4), dim3(64), 0, sh, n, H);
+      // TBLS_HROW_WAVES: the coop kernels' register bound, waves per SIMD (A/B)
+      static const int hw = getenv("TBLS_HROW_WAVES") ? atoi(getenv("TBLS_HROW_WAVES")) : 2;
+      hipLaunchKernelGGL(hw >= 4 ? k_hrow_sswu4 : hw == 3 ? k_hrow_sswu3 : k_hrow_sswu, dim3((2 * n + 3) / 4), dim3(64), 0, sh, n, H);
       hipLaunchKernelGGL(k_hrow_iso, g, blk, 0, sh, n, H);
-      hipLaunchKernelGGL(k_hrow_cof, dim3((n + 3) / 4), dim3(64), 0, sh, n, (const hrow_set*)H, Q, skip, force_fix);
+      hipLaunchKernelGGL(hw >= 3 ? k_hrow_cof3 : k_hrow_cof, dim3((n + 3) / 4), dim3(64), 0, sh, n, (const hrow_set*)H, Q, skip, force_fix);
       hipLaunchKernelGGL(k_hrow_fix, g, blk, 0, sh, n, (const hrow_set*)H, Q, skip);
     }
     else if (n)
