@@ -287,6 +287,14 @@ static uint32_t hash_row_max() {
   return v;
 }
 static bool hash_row(uint32_t n) { return n > TB_HASH_WAVE_MAX && n <= hash_row_max(); }
+// above the row hash and up to TBLS_HASH_PAIR_MAX sets (default 32,768: the
+// pairs' lanes then fill every SIMD once): two lanes per set, one SSWU map
+// each (k_set_hash_pair); 0 disables it (A/B)
+#define TB_HASH_PAIR_MAX 32768u
+static bool hash_pair(uint32_t n) {
+  static const uint32_t v = getenv("TBLS_HASH_PAIR_MAX") ? (uint32_t)atoi(getenv("TBLS_HASH_PAIR_MAX")) : TB_HASH_PAIR_MAX;
+  return n > TB_HASH_WAVE_MAX && !hash_row(n) && n <= v;
+}
 
 struct ws_layout {
   size_t pk_aff, pk_code, P, Q, skip, set_code, sig_code, f, fpart, fpart2, segv, n_bad, result;
@@ -479,6 +487,8 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
       hipLaunchKernelGGL(hw >= 3 ? k_hrow_cof3 : k_hrow_cof, dim3((n + 3) / 4), dim3(64), 0, sh, n, (const hrow_set*)H, Q, skip, force_fix);
       hipLaunchKernelGGL(k_hrow_fix, g, blk, 0, sh, n, (const hrow_set*)H, Q, skip);
     }
+    else if (hash_pair(n))
+      hipLaunchKernelGGL(k_set_hash_pair, dim3((2 * n + TB_BLOCK - 1) / TB_BLOCK), blk, 0, sh, b.msgs, b.msg_off, dst, dlen, n, Q, skip);
     else if (n)
       hipLaunchKernelGGL(k_set_hash, g, blk, 0, sh, b.msgs, b.msg_off, dst, dlen, n, Q, skip);
     TB_EV(7, sh);
