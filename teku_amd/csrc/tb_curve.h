@@ -366,8 +366,41 @@ TB_HD TB_INLINE g2j g2_psi2(const g2j& p) {
   return {fp2_mul_fp(p.x, fp_from_const(PSI2_CX[0])), fp2_mul_fp(p.y, fp_from_const(PSI2_CY[0])), p.z};
 }
 
+// [|x|]P for the fixed |x| = 0xd201000000010000 (bits 63, 62, 60, 57, 48, 16):
+// runs of doublings with the 5 additions inlined between them as straight-line
+// code -- the general jac_mul_u64's conditional addition inside the loop either
+// widens every doubling step's live set (inlined) or pays the callee-saved
+// register spill of an outlined call per addition (G2: ~450 scratch accesses
+// a call).  TB_G2_XRUNS=0 keeps jac_mul_u64 (A/B).
+#ifndef TB_G2_XRUNS
+#define TB_G2_XRUNS 1
+#endif
+TB_HD constexpr int XRUN_DBL[6] = {1, 2, 3, 9, 32, 16};  // doublings before addition k (the last run has none after it)
+TB_HD constexpr uint64_t xruns_value() {
+  uint64_t v = 1;
+  for (int k = 0; k < 6; k++) {
+    v <<= XRUN_DBL[k];
+    if (k < 5) v += 1;
+  }
+  return v;
+}
+static_assert(xruns_value() == 0xd201000000010000ull, "XRUN_DBL spells |x|");
+TB_HD TB_NOINLINE g2j g2_mul_xabs(const g2j& P) {
+  g2j r = P;
+  TB_UNROLL for (int k = 0; k < 5; k++) {
+    TB_NOUNROLL for (int i = 0; i < XRUN_DBL[k]; i++) r = jac_dbl_i(r);
+    r = jac_add_i(r, P);
+  }
+  TB_NOUNROLL for (int i = 0; i < XRUN_DBL[5]; i++) r = jac_dbl_i(r);
+  return r;
+}
+
 // [x]P with x = -0xd201000000010000
+#if TB_G2_XRUNS
+TB_HD TB_INLINE g2j g2_mul_x(const g2j& p) { return jac_neg(g2_mul_xabs(p)); }
+#else
 TB_HD TB_INLINE g2j g2_mul_x(const g2j& p) { return jac_neg(jac_mul_u64(p, X_ABS)); }
+#endif
 TB_HD TB_INLINE g1j g1_mul_x(const g1j& p) { return jac_neg(jac_mul_u64(p, X_ABS)); }
 
 // Scott: Q in G2 <=> psi(Q) == [x]Q
