@@ -366,7 +366,7 @@ TB_HD TB_INLINE g2j g2_psi2(const g2j& p) {
   return {fp2_mul_fp(p.x, fp_from_const(PSI2_CX[0])), fp2_mul_fp(p.y, fp_from_const(PSI2_CY[0])), p.z};
 }
 
-// [|x|]P for the fixed |x| = 0xd201000000010000 (bits 63, 62, 60, 57, 48, 16):
+// [|x|]P (G1 and G2) for the fixed |x| = 0xd201000000010000 (bits 63, 62, 60, 57, 48, 16):
 // runs of doublings with the 5 additions inlined between them as straight-line
 // code -- the general jac_mul_u64's conditional addition inside the loop either
 // widens every doubling step's live set (inlined) or pays the callee-saved
@@ -385,8 +385,9 @@ TB_HD constexpr uint64_t xruns_value() {
   return v;
 }
 static_assert(xruns_value() == 0xd201000000010000ull, "XRUN_DBL spells |x|");
-TB_HD TB_NOINLINE g2j g2_mul_xabs(const g2j& P) {
-  g2j r = P;
+template <typename F>
+TB_HD TB_NOINLINE jac<F> jac_mul_xabs(const jac<F>& P) {
+  jac<F> r = P;
   TB_UNROLL for (int k = 0; k < 5; k++) {
     TB_NOUNROLL for (int i = 0; i < XRUN_DBL[k]; i++) r = jac_dbl_i(r);
     r = jac_add_i(r, P);
@@ -396,12 +397,22 @@ TB_HD TB_NOINLINE g2j g2_mul_xabs(const g2j& P) {
 }
 
 // [x]P with x = -0xd201000000010000
+// TB_G1_XRUNS=1: the same for G1 (g1_mul_x, the key subgroup check): its
+// doubling loop loses 18 scratch accesses per step; built and CPU-tested, not
+// yet measured on the GPU, so off by default.
+#ifndef TB_G1_XRUNS
+#define TB_G1_XRUNS 0
+#endif
 #if TB_G2_XRUNS
-TB_HD TB_INLINE g2j g2_mul_x(const g2j& p) { return jac_neg(g2_mul_xabs(p)); }
+TB_HD TB_INLINE g2j g2_mul_x(const g2j& p) { return jac_neg(jac_mul_xabs(p)); }
 #else
 TB_HD TB_INLINE g2j g2_mul_x(const g2j& p) { return jac_neg(jac_mul_u64(p, X_ABS)); }
 #endif
+#if TB_G1_XRUNS
+TB_HD TB_INLINE g1j g1_mul_x(const g1j& p) { return jac_neg(jac_mul_xabs(p)); }
+#else
 TB_HD TB_INLINE g1j g1_mul_x(const g1j& p) { return jac_neg(jac_mul_u64(p, X_ABS)); }
+#endif
 
 // Scott: Q in G2 <=> psi(Q) == [x]Q
 TB_HD TB_NOINLINE bool g2_in_group(const g2j& q) {
@@ -412,7 +423,11 @@ TB_HD TB_NOINLINE bool g2_in_group(const g2j& q) {
 // Scott: P in G1 <=> phi(P) == [-x^2]P, phi(X,Y,Z) = (beta X, Y, Z)
 TB_HD TB_NOINLINE bool g1_in_group(const g1j& p) {
   if (jac_is_inf(p)) return true;
+#if TB_G1_XRUNS
+  g1j t = jac_mul_xabs(jac_mul_xabs(p));  // [x^2]P
+#else
   g1j t = jac_mul_u64(jac_mul_u64(p, X_ABS), X_ABS);  // [x^2]P
+#endif
   g1j phi = {fp_mul(p.x, fp_from_const(BETA)), p.y, p.z};
   return jac_eq(phi, jac_neg(t));
 }
