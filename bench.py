@@ -217,42 +217,61 @@ def cpu_threads():
     return max(1, n), cap, quota
 
 
+def granted_threads(T, cap, quota):
+    """The threads this process is granted: min(affinity, environment cap,
+    cgroup quota rounded down) -- on the GPU box affinity names every CPU of
+    the machine (256) while the box's share is 16 (OMP_NUM_THREADS / MAX_JOBS,
+    cpu.max), and Teku sizes its verifier pool from the cores it may use
+    (P2PConfig.java:42-43)."""
+    g = T
+    if cap:
+        g = min(g, cap)
+    if quota:
+        g = min(g, max(1, int(quota)))
+    return max(1, g)
+
+
 def cpu_baseline_oracle(pks, msgs, sigs, sample_sets=4096, sample_1t=512):
     """The C oracle (oracle/c/bls_oracle.c, 'port') timed on this host over a
-    bounded sample of the same workload: the first `sample_sets` sets on every
-    core of this box's share, the first `sample_1t` sets on one thread, and
-    the p50 of a 128-set batch (config 1) on every core."""
+    bounded sample of the same workload: the first `sample_sets` sets on the
+    threads this process is granted (`granted_threads`: the headline), the
+    same sample on every CPU of the affinity mask (oversubscribed beyond the
+    grant: secondary), the first `sample_1t` sets on one thread, and the p50
+    of a 128-set batch (config 1) on the granted threads."""
     from oracle import c_oracle as C
 
     T, cap, quota = cpu_threads()
+    Tg = granted_threads(T, cap, quota)
     pk = [pks[48 * j : 48 * j + 48] for j in range(sample_sets)]
     ms = [msgs[32 * j : 32 * j + 32] for j in range(sample_sets)]
     sg = [sigs[96 * j : 96 * j + 96] for j in range(sample_sets)]
     rr = synth.random_multipliers(sample_sets)
     t0 = time.perf_counter()
-    assert C.batch_verify(pk, ms, sg, rr, threads=T), "C oracle rejected the valid sample"
+    assert C.batch_verify(pk, ms, sg, rr, threads=Tg), "C oracle rejected the valid sample"
     dt = time.perf_counter() - t0
     t0 = time.perf_counter()
     assert C.batch_verify(pk[:sample_1t], ms[:sample_1t], sg[:sample_1t], rr[:sample_1t], threads=1)
     dt1 = time.perf_counter() - t0
-    lat = timed(lambda: C.batch_verify(pk[:128], ms[:128], sg[:128], rr[:128], threads=T), 7)
-    dt_cap = None
-    if cap and cap < T:  # the same sample on the environment's thread cap
+    lat = timed(lambda: C.batch_verify(pk[:128], ms[:128], sg[:128], rr[:128], threads=Tg), 7)
+    dt_all = None
+    if T > Tg:  # the same sample on every CPU of the affinity mask (beyond the grant)
         t0 = time.perf_counter()
-        assert C.batch_verify(pk, ms, sg, rr, threads=cap)
-        dt_cap = time.perf_counter() - t0
+        assert C.batch_verify(pk, ms, sg, rr, threads=T)
+        dt_all = time.perf_counter() - t0
     return {
         "value": sample_sets / dt,
         "unit": "sigs/s",
-        "cores": T,
+        "cores": Tg,
         "kind": "port",
-        "sample": f"oracle/c batch_verify of the first {sample_sets} sets of this workload on {T} pthreads ({dt:.1f} s) and of the first "
+        "sample": f"oracle/c batch_verify of the first {sample_sets} sets of this workload on {Tg} pthreads ({dt:.1f} s; the "
+        f"threads this process is granted: min(affinity {T}, env cap {cap}, cgroup quota {quota})) and of the first "
         f"{sample_1t} on 1 thread ({dt1:.1f} s); the build's own C restatement (6x64-bit CIOS Montgomery), not blst",
         "value_1thread": sample_1t / dt1,
+        "threads_granted": Tg,
         "threads_affinity": T,
         "env_thread_cap": cap,
-        "value_env_cap": sample_sets / dt_cap if dt_cap else None,
         "cgroup_cpu_quota_cores": quota,
+        "value_affinity_oversubscribed": sample_sets / dt_all if dt_all else None,
         "cpu_model": cpu_model(),
         "machine_cpus": os.cpu_count(),
         "p50_latency_ms_128": statistics.median(lat),

@@ -104,9 +104,10 @@ typedef struct {
  * through prepareBatchVerify/completeBatchVerify (BLS.java:275-336,
  * BlstBLS12381.java:112-189).  rand[i] in [1, 2^64] as BlstBLS12381
  * .nextBatchRandomMultiplier (l.191-195) -- the caller owns the RNG.  n_gpus:
- * shards sets over that many devices (0 = all initialised devices); each
- * device produces one Fp12 partial product, gathered for one final
- * exponentiation.  *ok = 1 iff every set is valid and the pairing product is
+ * at most that many devices (0 = all initialised devices); the batch goes to
+ * the least-loaded device, or is sharded over several when it has at least
+ * 2 x tbls_shard_min() sets (tbls_place_plan); each device produces one Fp12
+ * partial product, gathered for one final exponentiation.  *ok = 1 iff every set is valid and the pairing product is
  * 1.  n == 0 -> *ok = 0 (BLS.java:240-241).  A set with n_pks == 0 ->
  * TBLS_BAD_ARGUMENT (BlstPublicKey.aggregate checkArgument, l.56). */
 int tbls_batch_verify(const tbls_set* sets, size_t n, const uint64_t* rand, int n_gpus, int* ok, tbls_timing* t);
@@ -151,7 +152,7 @@ int tbls_fast_aggregate_verify_many(const tbls_set* sets, size_t n, int* ok_per_
  * AggregatingSignatureVerificationService.batchVerifySignatures
  * (statetransition/.../signatures/AggregatingSignatureVerificationService.java:
  * 188-227) after a failed randomized batch.  Chunks of 65536 sets are spread
- * over n_gpus devices (0 = all). */
+ * over at most n_gpus devices (0 = all), the least-loaded first. */
 int tbls_verify_each(const tbls_set* sets, size_t n, int n_gpus, int* ok_per_set);
 
 /* ---- batched deserialization and aggregation ----
@@ -214,6 +215,25 @@ int tbls_dev_batch_stage_profile(int device, const tbls_dev_batch* b, void* stre
  * *split = 1 when the split line / accumulator kernels run (0: one-workgroup
  * wave Miller loops for small batches).  Always TBLS_SUCCESS. */
 int tbls_acc_plan(uint32_t n, uint32_t* per, uint32_t* nseg, int* split);
+
+/* Device placement of a batch (introspection for tests and tuning; no device
+ * work), the function tbls_batch_verify / tbls_verify_each / the single-call
+ * entries use (tb_lib.hip place_plan): n sets (n_pks[i] keys
+ * each; NULL = one key each) over n_devices devices with load[d] batches in
+ * flight (NULL = idle) are sharded over
+ *   G = min(n_devices capped by n_gpus > 0, max(1, n / shard_min_sets))
+ * devices (shard_min_sets = 0: all of them) -- the G least-loaded ones,
+ * ties broken round-robin from rr, in ascending order in dev_out[0..G) (the
+ * first is the gather root) -- with contiguous shards balanced by key count:
+ * device dev_out[k] gets sets [cut_out[k], cut_out[k+1]) (cut_out: G + 1
+ * entries).  Returns G >= 1, or -TBLS_BAD_ARGUMENT.  A concurrent caller of
+ * the live library sees the devices its batch holds as loaded, so N service
+ * workers with small batches land on N different devices
+ * (AggregatingSignatureVerificationService.java:121-132, 202-205). */
+int tbls_place_plan(size_t n, const uint32_t* n_pks, int n_devices, int n_gpus, const int* load, uint32_t rr, uint32_t shard_min_sets,
+                    int* dev_out, size_t* cut_out);
+/* The live shard_min_sets (2048, or TBLS_SHARD_MIN). */
+uint32_t tbls_shard_min(void);
 
 /* Multiply g partial records (device memory, contiguous) and run the final
  * exponentiation: *ok = 1 iff no invalid set and the product is 1. */

@@ -7,6 +7,7 @@ package tech.pegasys.teku.bls.impl.hip;
 
 import java.util.Arrays;
 import java.util.List;
+import java.util.Objects;
 import org.apache.tuweni.bytes.Bytes48;
 import tech.pegasys.teku.bls.impl.BlsException;
 import tech.pegasys.teku.bls.impl.PublicKey;
@@ -102,13 +103,21 @@ final class HipPublicKey implements PublicKey {
     return v;
   }
 
+  // BlstPublicKey.java:115-130: the compressed bytes' hash, and equal to any
+  // PublicKey (of any implementation) with the same compressed bytes
   @Override
   public int hashCode() {
-    return Arrays.hashCode(bytes);
+    return toBytesCompressed().hashCode();
   }
 
   @Override
   public boolean equals(final Object obj) {
-    return obj instanceof HipPublicKey o && Arrays.equals(o.bytes, bytes);
+    if (this == obj) {
+      return true;
+    }
+    if (!(obj instanceof PublicKey o)) {
+      return false;
+    }
+    return Objects.equals(toBytesCompressed(), o.toBytesCompressed());
   }
 }

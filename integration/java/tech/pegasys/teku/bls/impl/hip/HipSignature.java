@@ -8,6 +8,7 @@ package tech.pegasys.teku.bls.impl.hip;
 import java.nio.charset.StandardCharsets;
 import java.util.Arrays;
 import java.util.List;
+import java.util.Objects;
 import org.apache.tuweni.bytes.Bytes;
 import tech.pegasys.teku.bls.impl.BlsException;
 import tech.pegasys.teku.bls.impl.PublicKey;
@@ -115,13 +116,21 @@ final class HipSignature implements Signature {
     return TekuBlsHip.sigValidate(bytes, new int[1]) == TekuBlsHip.SUCCESS;
   }
 
+  // BlstSignature.java:152-165: the compressed bytes' hash, and equal to any
+  // Signature (of any implementation) with the same compressed bytes
   @Override
   public int hashCode() {
-    return Arrays.hashCode(bytes);
+    return toBytesCompressed().hashCode();
   }
 
   @Override
   public boolean equals(final Object obj) {
-    return obj instanceof HipSignature o && Arrays.equals(o.bytes, bytes);
+    if (this == obj) {
+      return true;
+    }
+    if (!(obj instanceof Signature o)) {
+      return false;
+    }
+    return Objects.equals(toBytesCompressed(), o.toBytesCompressed());
   }
 }

@@ -18,30 +18,83 @@
 
 #define JNAME(n) Java_tech_pegasys_teku_bls_impl_hip_TekuBlsHip_##n
 
-/* byte[] -> malloc'd copy (NULL array -> NULL); *len = its length */
-static uint8_t* bytes_in(JNIEnv* env, jbyteArray a, jsize* len) {
-  if (!a) {
-    if (len) *len = 0;
+/* Every entry validates its Java arguments before the library sees a pointer
+ * into them: NULL arrays, lengths (fixed-size keys / signatures / secret
+ * keys, n + 1 monotone message offsets inside the message bytes, sum(nPks)
+ * keys, n signatures, n randomizers, output arrays large enough), failed
+ * region copies (a pending Java exception) and failed allocations all return
+ * TBLS_BAD_ARGUMENT / TBLS_DEVICE_ERROR without calling the library. */
+
+static jsize alen(JNIEnv* env, jarray a) { return a ? (*env)->GetArrayLength(env, a) : -1; }
+
+/* byte[] -> malloc'd copy; NULL on a NULL array, a failed allocation or a
+ * failed copy (*rc says which); *len = its length */
+static uint8_t* bytes_in(JNIEnv* env, jbyteArray a, jsize* len, int* rc) {
+  const jsize n = alen(env, a);
+  if (len) *len = n < 0 ? 0 : n;
+  if (n < 0) {
+    *rc = TBLS_BAD_ARGUMENT;
     return NULL;
   }
-  const jsize n = (*env)->GetArrayLength(env, a);
   uint8_t* p = (uint8_t*)malloc(n ? (size_t)n : 1);
-  if (p && n) (*env)->GetByteArrayRegion(env, a, 0, n, (jbyte*)p);
-  if (len) *len = n;
+  if (!p) {
+    *rc = TBLS_DEVICE_ERROR;
+    return NULL;
+  }
+  if (n) (*env)->GetByteArrayRegion(env, a, 0, n, (jbyte*)p);
+  if ((*env)->ExceptionCheck(env)) {
+    free(p);
+    *rc = TBLS_BAD_ARGUMENT;
+    return NULL;
+  }
   return p;
 }
 
-static int32_t* ints_in(JNIEnv* env, jintArray a, jsize* len) {
-  const jsize n = (*env)->GetArrayLength(env, a);
+static int32_t* ints_in(JNIEnv* env, jintArray a, jsize* len, int* rc) {
+  const jsize n = alen(env, a);
+  if (len) *len = n < 0 ? 0 : n;
+  if (n < 0) {
+    *rc = TBLS_BAD_ARGUMENT;
+    return NULL;
+  }
   int32_t* p = (int32_t*)malloc(sizeof(int32_t) * (n ? (size_t)n : 1));
-  if (p && n) (*env)->GetIntArrayRegion(env, a, 0, n, (jint*)p);
-  if (len) *len = n;
+  if (!p) {
+    *rc = TBLS_DEVICE_ERROR;
+    return NULL;
+  }
+  if (n) (*env)->GetIntArrayRegion(env, a, 0, n, (jint*)p);
+  if ((*env)->ExceptionCheck(env)) {
+    free(p);
+    *rc = TBLS_BAD_ARGUMENT;
+    return NULL;
+  }
   return p;
 }
 
-static void set_int(JNIEnv* env, jintArray a, int v) {
+/* exactly `want` bytes into a caller buffer */
+static int fixed_in(JNIEnv* env, jbyteArray a, jbyte* out, jsize want) {
+  if (alen(env, a) != want) return TBLS_BAD_ARGUMENT;
+  (*env)->GetByteArrayRegion(env, a, 0, want, out);
+  return (*env)->ExceptionCheck(env) ? TBLS_BAD_ARGUMENT : TBLS_SUCCESS;
+}
+
+static int set_int(JNIEnv* env, jintArray a, int v) {
+  if (alen(env, a) < 1) return TBLS_BAD_ARGUMENT;
   jint x = v;
   (*env)->SetIntArrayRegion(env, a, 0, 1, &x);
+  return (*env)->ExceptionCheck(env) ? TBLS_BAD_ARGUMENT : TBLS_SUCCESS;
+}
+
+/* n sets' shape: nPks[i] >= 0 summing to <= keys_avail, msgOff n + 1 monotone
+ * offsets in [0, msgs_len] */
+static int sets_shape_ok(const int32_t* np, jsize n, const int32_t* mo, jsize n_off, jsize msgs_len, size_t keys_avail) {
+  if (n_off != n + 1 || mo[0] != 0) return 0;
+  size_t k = 0;
+  for (jsize i = 0; i < n; i++) {
+    if (np[i] < 0 || mo[i + 1] < mo[i] || mo[i + 1] > msgs_len) return 0;
+    k += (size_t)np[i];
+  }
+  return k <= keys_avail;
 }
 
 JNIEXPORT jint JNICALL JNAME(init)(JNIEnv* env, jclass c, jint n, jint flags) {
@@ -60,16 +113,15 @@ JNIEXPORT jint JNICALL JNAME(deviceCount)(JNIEnv* env, jclass c) {
 JNIEXPORT jint JNICALL JNAME(pkValidate)(JNIEnv* env, jclass c, jbyteArray pk) {
   (void)c;
   jbyte b[48];
-  if ((*env)->GetArrayLength(env, pk) != 48) return TBLS_BAD_ENCODING;
-  (*env)->GetByteArrayRegion(env, pk, 0, 48, b);
+  if (fixed_in(env, pk, b, 48)) return TBLS_BAD_ENCODING;
   return tbls_pk_validate((const uint8_t*)b);
 }
 
 JNIEXPORT jint JNICALL JNAME(sigValidate)(JNIEnv* env, jclass c, jbyteArray sig, jintArray isInf) {
   (void)c;
   jbyte b[96];
-  if ((*env)->GetArrayLength(env, sig) != 96) return TBLS_BAD_ENCODING;
-  (*env)->GetByteArrayRegion(env, sig, 0, 96, b);
+  if (fixed_in(env, sig, b, 96)) return TBLS_BAD_ENCODING;
+  if (alen(env, isInf) < 1) return TBLS_BAD_ARGUMENT;
   int inf = 0;
   const int rc = tbls_sig_validate((const uint8_t*)b, &inf);
   set_int(env, isInf, inf);
@@ -79,13 +131,16 @@ JNIEXPORT jint JNICALL JNAME(sigValidate)(JNIEnv* env, jclass c, jbyteArray sig,
 JNIEXPORT jint JNICALL JNAME(aggregatePks)(JNIEnv* env, jclass c, jbyteArray pks, jint k, jbyteArray out) {
   (void)c;
   jsize n;
-  uint8_t* p = bytes_in(env, pks, &n);
+  int rc = TBLS_SUCCESS;
+  if (k < 0 || alen(env, out) < 48) return TBLS_BAD_ARGUMENT;
+  uint8_t* p = bytes_in(env, pks, &n, &rc);
+  if (!p) return rc;
   if ((size_t)n < 48u * (size_t)k) {
     free(p);
     return TBLS_BAD_ARGUMENT;
   }
   uint8_t o[48];
-  const int rc = tbls_aggregate_pks(p, (size_t)k, o);
+  rc = tbls_aggregate_pks(p, (size_t)k, o);
   free(p);
   if (rc == TBLS_SUCCESS) (*env)->SetByteArrayRegion(env, out, 0, 48, (const jbyte*)o);
   return rc;
@@ -94,13 +149,16 @@ JNIEXPORT jint JNICALL JNAME(aggregatePks)(JNIEnv* env, jclass c, jbyteArray pks
 JNIEXPORT jint JNICALL JNAME(aggregateSigs)(JNIEnv* env, jclass c, jbyteArray sigs, jint k, jbyteArray out) {
   (void)c;
   jsize n;
-  uint8_t* p = bytes_in(env, sigs, &n);
+  int rc = TBLS_SUCCESS;
+  if (k < 0 || alen(env, out) < 96) return TBLS_BAD_ARGUMENT;
+  uint8_t* p = bytes_in(env, sigs, &n, &rc);
+  if (!p) return rc;
   if ((size_t)n < 96u * (size_t)k) {
     free(p);
     return TBLS_BAD_ARGUMENT;
   }
   uint8_t o[96];
-  const int rc = tbls_aggregate_sigs(p, (size_t)k, o);
+  rc = tbls_aggregate_sigs(p, (size_t)k, o);
   free(p);
   if (rc == TBLS_SUCCESS) (*env)->SetByteArrayRegion(env, out, 0, 96, (const jbyte*)o);
   return rc;
@@ -110,22 +168,23 @@ JNIEXPORT jint JNICALL JNAME(sign)(JNIEnv* env, jclass c, jbyteArray sk, jbyteAr
   (void)c;
   jsize ml, dl;
   jbyte s[32];
-  (*env)->GetByteArrayRegion(env, sk, 0, 32, s);
-  uint8_t* m = bytes_in(env, msg, &ml);
-  uint8_t* d = bytes_in(env, dst, &dl);
+  int rc = TBLS_SUCCESS;
+  if (fixed_in(env, sk, s, 32) || alen(env, out) < 96) return TBLS_BAD_ARGUMENT;
+  uint8_t* m = bytes_in(env, msg, &ml, &rc);
+  uint8_t* d = m ? bytes_in(env, dst, &dl, &rc) : NULL;
   uint8_t o[96];
-  const int rc = tbls_sign((const uint8_t*)s, m, (size_t)ml, d, (size_t)dl, o);
+  if (m && d) rc = tbls_sign((const uint8_t*)s, m, (size_t)ml, d, (size_t)dl, o);
   memset(s, 0, sizeof s);
   free(m);
   free(d);
-  if (rc == TBLS_SUCCESS) (*env)->SetByteArrayRegion(env, out, 0, 96, (const jbyte*)o);
+  if (m && d && rc == TBLS_SUCCESS) (*env)->SetByteArrayRegion(env, out, 0, 96, (const jbyte*)o);
   return rc;
 }
 
 JNIEXPORT jint JNICALL JNAME(skToPk)(JNIEnv* env, jclass c, jbyteArray sk, jbyteArray out) {
   (void)c;
   jbyte s[32];
-  (*env)->GetByteArrayRegion(env, sk, 0, 32, s);
+  if (fixed_in(env, sk, s, 32) || alen(env, out) < 48) return TBLS_BAD_ARGUMENT;
   uint8_t o[48];
   const int rc = tbls_sk_to_pk((const uint8_t*)s, o);
   memset(s, 0, sizeof s);
@@ -137,13 +196,13 @@ JNIEXPORT jint JNICALL JNAME(verify)(JNIEnv* env, jclass c, jbyteArray pk, jbyte
                                      jintArray okOut) {
   (void)c;
   jbyte p[48], s[96];
-  (*env)->GetByteArrayRegion(env, pk, 0, 48, p);
-  (*env)->GetByteArrayRegion(env, sig, 0, 96, s);
+  if (fixed_in(env, pk, p, 48) || fixed_in(env, sig, s, 96) || alen(env, okOut) < 1) return TBLS_BAD_ARGUMENT;
   jsize ml, dl;
-  uint8_t* m = bytes_in(env, msg, &ml);
-  uint8_t* d = bytes_in(env, dst, &dl);
+  int rc = TBLS_SUCCESS;
+  uint8_t* m = bytes_in(env, msg, &ml, &rc);
+  uint8_t* d = m ? bytes_in(env, dst, &dl, &rc) : NULL;
   int ok = 0;
-  const int rc = tbls_verify((const uint8_t*)p, m, (size_t)ml, (const uint8_t*)s, d, (size_t)dl, &ok);
+  if (m && d) rc = tbls_verify((const uint8_t*)p, m, (size_t)ml, (const uint8_t*)s, d, (size_t)dl, &ok);
   free(m);
   free(d);
   set_int(env, okOut, ok);
@@ -153,21 +212,39 @@ JNIEXPORT jint JNICALL JNAME(verify)(JNIEnv* env, jclass c, jbyteArray pk, jbyte
 JNIEXPORT jint JNICALL JNAME(aggregateVerify)(JNIEnv* env, jclass c, jbyteArray pks, jbyteArray msgs, jintArray msgOff,
                                               jbyteArray sig, jintArray okOut) {
   (void)c;
-  jsize no, ml;
-  int32_t* off = ints_in(env, msgOff, &no);
-  const size_t n = no > 0 ? (size_t)no - 1 : 0;
-  uint8_t* p = bytes_in(env, pks, NULL);
-  uint8_t* m = bytes_in(env, msgs, &ml);
+  jsize no, ml, pl;
+  int rc = TBLS_SUCCESS;
   jbyte s[96];
-  (*env)->GetByteArrayRegion(env, sig, 0, 96, s);
-  const uint8_t** mp = (const uint8_t**)malloc(sizeof(uint8_t*) * (n ? n : 1));
-  uint32_t* lens = (uint32_t*)malloc(sizeof(uint32_t) * (n ? n : 1));
-  for (size_t i = 0; i < n; i++) {
-    mp[i] = m + off[i];
-    lens[i] = (uint32_t)(off[i + 1] - off[i]);
-  }
+  if (fixed_in(env, sig, s, 96) || alen(env, okOut) < 1) return TBLS_BAD_ARGUMENT;
+  int32_t* off = ints_in(env, msgOff, &no, &rc);
+  uint8_t* p = off ? bytes_in(env, pks, &pl, &rc) : NULL;
+  uint8_t* m = p ? bytes_in(env, msgs, &ml, &rc) : NULL;
+  const size_t n = no > 0 ? (size_t)no - 1 : 0;
+  const uint8_t** mp = NULL;
+  uint32_t* lens = NULL;
   int ok = 0;
-  const int rc = tbls_aggregate_verify(p, mp, lens, n, (const uint8_t*)s, &ok);
+  if (m) {
+    /* one key per message: n keys, n + 1 offsets */
+    static const int32_t one = 1;
+    int32_t* ones = (int32_t*)malloc(sizeof(int32_t) * (n ? n : 1));
+    mp = (const uint8_t**)malloc(sizeof(uint8_t*) * (n ? n : 1));
+    lens = (uint32_t*)malloc(sizeof(uint32_t) * (n ? n : 1));
+    if (!ones || !mp || !lens) {
+      rc = TBLS_DEVICE_ERROR;
+    } else {
+      for (size_t i = 0; i < n; i++) ones[i] = one;
+      if (no < 1 || !sets_shape_ok(ones, (jsize)n, off, no, ml, (size_t)pl / 48)) {
+        rc = TBLS_BAD_ARGUMENT;
+      } else {
+        for (size_t i = 0; i < n; i++) {
+          mp[i] = m + off[i];
+          lens[i] = (uint32_t)(off[i + 1] - off[i]);
+        }
+        rc = tbls_aggregate_verify(p, mp, lens, n, (const uint8_t*)s, &ok);
+      }
+    }
+    free(ones);
+  }
   free(lens);
   free(mp);
   free(m);
@@ -177,9 +254,11 @@ JNIEXPORT jint JNICALL JNAME(aggregateVerify)(JNIEnv* env, jclass c, jbyteArray 
   return rc;
 }
 
-/* the flattened sets of batchVerify / verifyEach -> tbls_set[n] (pointers into the copies) */
+/* the flattened sets of batchVerify / verifyEach -> tbls_set[n] (pointers
+ * into the copies; the shape was checked by sets_shape_ok) */
 static tbls_set* sets_of(const uint8_t* pk, const int32_t* np, const uint8_t* m, const int32_t* mo, const uint8_t* sg, size_t n) {
   tbls_set* sets = (tbls_set*)malloc(sizeof(tbls_set) * (n ? n : 1));
+  if (!sets) return NULL;
   size_t k = 0;
   for (size_t i = 0; i < n; i++) {
     sets[i].pks = pk + 48 * k;
@@ -192,37 +271,101 @@ static tbls_set* sets_of(const uint8_t* pk, const int32_t* np, const uint8_t* m,
   return sets;
 }
 
+/* the common inputs of batchVerify / verifyEach, copied and checked */
+typedef struct {
+  jsize n, n_off, ml, pl, sl;
+  int32_t *np, *mo;
+  uint8_t *pk, *m, *sg;
+} flat_sets;
+
+static void flat_free(flat_sets* f) {
+  free(f->sg);
+  free(f->m);
+  free(f->pk);
+  free(f->mo);
+  free(f->np);
+}
+
+/* key_unit: 48 (compressed keys) or 4 (table indices) */
+static int flat_in(JNIEnv* env, flat_sets* f, jbyteArray pks, jintArray keyIdx, jintArray nPks, jbyteArray msgs, jintArray msgOff,
+                   jbyteArray sigs) {
+  int rc = TBLS_SUCCESS;
+  memset(f, 0, sizeof *f);
+  f->np = ints_in(env, nPks, &f->n, &rc);
+  if (f->np) f->mo = ints_in(env, msgOff, &f->n_off, &rc);
+  if (f->mo) {
+    if (keyIdx) {
+      jsize ni;
+      f->pk = (uint8_t*)ints_in(env, keyIdx, &ni, &rc);
+      f->pl = ni * 4;
+    } else {
+      f->pk = bytes_in(env, pks, &f->pl, &rc);
+    }
+  }
+  if (f->pk) f->m = bytes_in(env, msgs, &f->ml, &rc);
+  if (f->m) f->sg = bytes_in(env, sigs, &f->sl, &rc);
+  if (!f->sg) return rc;
+  const size_t unit = keyIdx ? 4 : 48;
+  if (!sets_shape_ok(f->np, f->n, f->mo, f->n_off, f->ml, (size_t)f->pl / unit) || (size_t)f->sl < 96u * (size_t)f->n)
+    return TBLS_BAD_ARGUMENT;
+  return TBLS_SUCCESS;
+}
+
+static uint64_t* rand_in(JNIEnv* env, jlongArray rand, jsize n, int* rc) {
+  if (alen(env, rand) < n) {
+    *rc = TBLS_BAD_ARGUMENT;
+    return NULL;
+  }
+  uint64_t* r = (uint64_t*)malloc(sizeof(uint64_t) * (n ? (size_t)n : 1));
+  if (!r) {
+    *rc = TBLS_DEVICE_ERROR;
+    return NULL;
+  }
+  if (n) (*env)->GetLongArrayRegion(env, rand, 0, n, (jlong*)r);
+  if ((*env)->ExceptionCheck(env)) {
+    free(r);
+    *rc = TBLS_BAD_ARGUMENT;
+    return NULL;
+  }
+  return r;
+}
+
 JNIEXPORT jint JNICALL JNAME(batchVerify)(JNIEnv* env, jclass c, jbyteArray pks, jintArray nPks, jbyteArray msgs,
                                           jintArray msgOff, jbyteArray sigs, jlongArray rand, jint nGpus, jintArray okOut) {
   (void)c;
-  jsize n;
-  int32_t* np = ints_in(env, nPks, &n);
-  int32_t* mo = ints_in(env, msgOff, NULL);
-  uint8_t* pk = bytes_in(env, pks, NULL);
-  uint8_t* m = bytes_in(env, msgs, NULL);
-  uint8_t* sg = bytes_in(env, sigs, NULL);
-  uint64_t* r = (uint64_t*)malloc(sizeof(uint64_t) * (n ? (size_t)n : 1));
-  if (n) (*env)->GetLongArrayRegion(env, rand, 0, n, (jlong*)r);
-  tbls_set* sets = sets_of(pk, np, m, mo, sg, (size_t)n);
+  if (alen(env, okOut) < 1) return TBLS_BAD_ARGUMENT;
+  flat_sets f;
+  int rc = flat_in(env, &f, pks, NULL, nPks, msgs, msgOff, sigs);
   int ok = 0;
-  const int rc = tbls_batch_verify(sets, (size_t)n, r, nGpus, &ok, NULL);
-  free(sets);
-  free(r);
-  free(sg);
-  free(m);
-  free(pk);
-  free(mo);
-  free(np);
+  if (rc == TBLS_SUCCESS) {
+    uint64_t* r = rand_in(env, rand, f.n, &rc);
+    tbls_set* sets = r ? sets_of(f.pk, f.np, f.m, f.mo, f.sg, (size_t)f.n) : NULL;
+    if (r && !sets) rc = TBLS_DEVICE_ERROR;
+    if (sets) rc = tbls_batch_verify(sets, (size_t)f.n, r, nGpus, &ok, NULL);
+    free(sets);
+    free(r);
+  }
+  flat_free(&f);
   set_int(env, okOut, ok);
   return rc;
 }
 
 JNIEXPORT jint JNICALL JNAME(pkTableLoad)(JNIEnv* env, jclass c, jbyteArray pks, jint k, jbyteArray codes) {
   (void)c;
-  uint8_t* p = bytes_in(env, pks, NULL);
+  jsize pl;
+  int rc = TBLS_SUCCESS;
+  if (k < 0 || alen(env, codes) < k) return TBLS_BAD_ARGUMENT;
+  uint8_t* p = bytes_in(env, pks, &pl, &rc);
+  if (!p) return rc;
   uint8_t* cd = (uint8_t*)malloc(k ? (size_t)k : 1);
-  const int rc = tbls_pk_table_load(p, (size_t)k, cd);
-  if (k) (*env)->SetByteArrayRegion(env, codes, 0, k, (const jbyte*)cd);
+  if (!cd) {
+    rc = TBLS_DEVICE_ERROR;
+  } else if ((size_t)pl < 48u * (size_t)k) {
+    rc = TBLS_BAD_ARGUMENT;
+  } else {
+    rc = tbls_pk_table_load(p, (size_t)k, cd);
+    if (k) (*env)->SetByteArrayRegion(env, codes, 0, k, (const jbyte*)cd);
+  }
   free(cd);
   free(p);
   return rc;
@@ -231,33 +374,30 @@ JNIEXPORT jint JNICALL JNAME(pkTableLoad)(JNIEnv* env, jclass c, jbyteArray pks,
 JNIEXPORT jint JNICALL JNAME(batchVerifyIdx)(JNIEnv* env, jclass c, jintArray keyIdx, jintArray nPks, jbyteArray msgs,
                                              jintArray msgOff, jbyteArray sigs, jlongArray rand, jint nGpus, jintArray okOut) {
   (void)c;
-  jsize n;
-  int32_t* idx = ints_in(env, keyIdx, NULL);
-  int32_t* np = ints_in(env, nPks, &n);
-  int32_t* mo = ints_in(env, msgOff, NULL);
-  uint8_t* m = bytes_in(env, msgs, NULL);
-  uint8_t* sg = bytes_in(env, sigs, NULL);
-  uint64_t* r = (uint64_t*)malloc(sizeof(uint64_t) * (n ? (size_t)n : 1));
-  if (n) (*env)->GetLongArrayRegion(env, rand, 0, n, (jlong*)r);
-  tbls_set_idx* sets = (tbls_set_idx*)malloc(sizeof(tbls_set_idx) * (n ? (size_t)n : 1));
-  size_t k = 0;
-  for (jsize i = 0; i < n; i++) {
-    sets[i].key_idx = (const uint32_t*)idx + k;
-    sets[i].n_pks = (uint32_t)np[i];
-    sets[i].msg = m + mo[i];
-    sets[i].msg_len = (uint32_t)(mo[i + 1] - mo[i]);
-    sets[i].sig = sg + 96 * (size_t)i;
-    k += (size_t)np[i];
-  }
+  if (alen(env, okOut) < 1 || !keyIdx) return TBLS_BAD_ARGUMENT;
+  flat_sets f;
+  int rc = flat_in(env, &f, NULL, keyIdx, nPks, msgs, msgOff, sigs);
   int ok = 0;
-  const int rc = tbls_batch_verify_idx(sets, (size_t)n, r, nGpus, &ok, NULL);
-  free(sets);
-  free(r);
-  free(sg);
-  free(m);
-  free(mo);
-  free(np);
-  free(idx);
+  if (rc == TBLS_SUCCESS) {
+    uint64_t* r = rand_in(env, rand, f.n, &rc);
+    tbls_set_idx* sets = r ? (tbls_set_idx*)malloc(sizeof(tbls_set_idx) * (f.n ? (size_t)f.n : 1)) : NULL;
+    if (r && !sets) rc = TBLS_DEVICE_ERROR;
+    if (sets) {
+      size_t k = 0;
+      for (jsize i = 0; i < f.n; i++) {
+        sets[i].key_idx = (const uint32_t*)f.pk + k;
+        sets[i].n_pks = (uint32_t)f.np[i];
+        sets[i].msg = f.m + f.mo[i];
+        sets[i].msg_len = (uint32_t)(f.mo[i + 1] - f.mo[i]);
+        sets[i].sig = f.sg + 96 * (size_t)i;
+        k += (size_t)f.np[i];
+      }
+      rc = tbls_batch_verify_idx(sets, (size_t)f.n, r, nGpus, &ok, NULL);
+    }
+    free(sets);
+    free(r);
+  }
+  flat_free(&f);
   set_int(env, okOut, ok);
   return rc;
 }
@@ -265,32 +405,41 @@ JNIEXPORT jint JNICALL JNAME(batchVerifyIdx)(JNIEnv* env, jclass c, jintArray ke
 JNIEXPORT jint JNICALL JNAME(verifyEach)(JNIEnv* env, jclass c, jbyteArray pks, jintArray nPks, jbyteArray msgs,
                                          jintArray msgOff, jbyteArray sigs, jint nGpus, jintArray okPerSet) {
   (void)c;
-  jsize n;
-  int32_t* np = ints_in(env, nPks, &n);
-  int32_t* mo = ints_in(env, msgOff, NULL);
-  uint8_t* pk = bytes_in(env, pks, NULL);
-  uint8_t* m = bytes_in(env, msgs, NULL);
-  uint8_t* sg = bytes_in(env, sigs, NULL);
-  tbls_set* sets = sets_of(pk, np, m, mo, sg, (size_t)n);
-  int* ok = (int*)calloc(n ? (size_t)n : 1, sizeof(int));
-  const int rc = tbls_verify_each(sets, (size_t)n, nGpus, ok);
-  if (n) (*env)->SetIntArrayRegion(env, okPerSet, 0, n, (const jint*)ok);
-  free(ok);
-  free(sets);
-  free(sg);
-  free(m);
-  free(pk);
-  free(mo);
-  free(np);
+  flat_sets f;
+  int rc = flat_in(env, &f, pks, NULL, nPks, msgs, msgOff, sigs);
+  if (rc == TBLS_SUCCESS && alen(env, okPerSet) < f.n) rc = TBLS_BAD_ARGUMENT;
+  if (rc == TBLS_SUCCESS) {
+    tbls_set* sets = sets_of(f.pk, f.np, f.m, f.mo, f.sg, (size_t)f.n);
+    int* ok = (int*)calloc(f.n ? (size_t)f.n : 1, sizeof(int));
+    if (!sets || !ok) {
+      rc = TBLS_DEVICE_ERROR;
+    } else {
+      rc = tbls_verify_each(sets, (size_t)f.n, nGpus, ok);
+      if (f.n) (*env)->SetIntArrayRegion(env, okPerSet, 0, f.n, (const jint*)ok);
+    }
+    free(ok);
+    free(sets);
+  }
+  flat_free(&f);
   return rc;
 }
 
 JNIEXPORT jint JNICALL JNAME(pkValidateMany)(JNIEnv* env, jclass c, jbyteArray pks, jint n, jbyteArray codes) {
   (void)c;
-  uint8_t* p = bytes_in(env, pks, NULL);
+  jsize pl;
+  int rc = TBLS_SUCCESS;
+  if (n < 0 || alen(env, codes) < n) return TBLS_BAD_ARGUMENT;
+  uint8_t* p = bytes_in(env, pks, &pl, &rc);
+  if (!p) return rc;
   uint8_t* cd = (uint8_t*)malloc(n ? (size_t)n : 1);
-  const int rc = tbls_pk_validate_many(p, (size_t)n, cd);
-  if (n) (*env)->SetByteArrayRegion(env, codes, 0, n, (const jbyte*)cd);
+  if (!cd) {
+    rc = TBLS_DEVICE_ERROR;
+  } else if ((size_t)pl < 48u * (size_t)n) {
+    rc = TBLS_BAD_ARGUMENT;
+  } else {
+    rc = tbls_pk_validate_many(p, (size_t)n, cd);
+    if (n) (*env)->SetByteArrayRegion(env, codes, 0, n, (const jbyte*)cd);
+  }
   free(cd);
   free(p);
   return rc;
@@ -298,13 +447,23 @@ JNIEXPORT jint JNICALL JNAME(pkValidateMany)(JNIEnv* env, jclass c, jbyteArray p
 
 JNIEXPORT jint JNICALL JNAME(sigValidateMany)(JNIEnv* env, jclass c, jbyteArray sigs, jint n, jbyteArray codes, jbyteArray isInf) {
   (void)c;
-  uint8_t* s = bytes_in(env, sigs, NULL);
+  jsize sl;
+  int rc = TBLS_SUCCESS;
+  if (n < 0 || alen(env, codes) < n || alen(env, isInf) < n) return TBLS_BAD_ARGUMENT;
+  uint8_t* s = bytes_in(env, sigs, &sl, &rc);
+  if (!s) return rc;
   uint8_t* cd = (uint8_t*)malloc(n ? (size_t)n : 1);
   uint8_t* inf = (uint8_t*)malloc(n ? (size_t)n : 1);
-  const int rc = tbls_sig_validate_many(s, (size_t)n, cd, inf);
-  if (n) {
-    (*env)->SetByteArrayRegion(env, codes, 0, n, (const jbyte*)cd);
-    (*env)->SetByteArrayRegion(env, isInf, 0, n, (const jbyte*)inf);
+  if (!cd || !inf) {
+    rc = TBLS_DEVICE_ERROR;
+  } else if ((size_t)sl < 96u * (size_t)n) {
+    rc = TBLS_BAD_ARGUMENT;
+  } else {
+    rc = tbls_sig_validate_many(s, (size_t)n, cd, inf);
+    if (n) {
+      (*env)->SetByteArrayRegion(env, codes, 0, n, (const jbyte*)cd);
+      (*env)->SetByteArrayRegion(env, isInf, 0, n, (const jbyte*)inf);
+    }
   }
   free(inf);
   free(cd);
@@ -315,17 +474,31 @@ JNIEXPORT jint JNICALL JNAME(sigValidateMany)(JNIEnv* env, jclass c, jbyteArray 
 JNIEXPORT jint JNICALL JNAME(aggregateSigsMany)(JNIEnv* env, jclass c, jbyteArray sigs, jintArray off, jint groups,
                                                 jbyteArray out, jintArray status) {
   (void)c;
-  uint8_t* s = bytes_in(env, sigs, NULL);
-  int32_t* o = ints_in(env, off, NULL);
-  uint8_t* res = (uint8_t*)malloc(96 * (size_t)(groups ? groups : 1));
-  int* st = (int*)calloc(groups ? (size_t)groups : 1, sizeof(int));
-  const int rc = tbls_aggregate_sigs_many(s, (const uint32_t*)o, (size_t)groups, res, st);
-  if (groups) {
-    (*env)->SetByteArrayRegion(env, out, 0, 96 * groups, (const jbyte*)res);
-    (*env)->SetIntArrayRegion(env, status, 0, groups, (const jint*)st);
+  jsize sl, no;
+  int rc = TBLS_SUCCESS;
+  if (groups < 0 || alen(env, out) < 96 * (jsize)groups || alen(env, status) < groups) return TBLS_BAD_ARGUMENT;
+  uint8_t* s = bytes_in(env, sigs, &sl, &rc);
+  int32_t* o = s ? ints_in(env, off, &no, &rc) : NULL;
+  if (o) {
+    /* groups + 1 monotone offsets (in signatures) inside sigs */
+    int shape = no == groups + 1 && o[0] == 0;
+    for (jsize g = 0; shape && g < groups; g++) shape = o[g + 1] >= o[g] && (size_t)o[g + 1] * 96u <= (size_t)sl;
+    uint8_t* res = (uint8_t*)malloc(96 * (size_t)(groups ? groups : 1));
+    int* st = (int*)calloc(groups ? (size_t)groups : 1, sizeof(int));
+    if (!res || !st) {
+      rc = TBLS_DEVICE_ERROR;
+    } else if (!shape) {
+      rc = TBLS_BAD_ARGUMENT;
+    } else {
+      rc = tbls_aggregate_sigs_many(s, (const uint32_t*)o, (size_t)groups, res, st);
+      if (groups) {
+        (*env)->SetByteArrayRegion(env, out, 0, 96 * groups, (const jbyte*)res);
+        (*env)->SetIntArrayRegion(env, status, 0, groups, (const jint*)st);
+      }
+    }
+    free(st);
+    free(res);
   }
-  free(st);
-  free(res);
   free(o);
   free(s);
   return rc;

@@ -61,7 +61,60 @@ def _buf(b: bytes):
 # ---------------------------------------------------------------------------
 # SPI value types
 # ---------------------------------------------------------------------------
-class HipPublicKey:
+def java_bytes_hash(b: bytes) -> int:
+    """tuweni Bytes.hashCode (31 * h + signed byte, int32): the hash BlstPublicKey
+    / BlstSignature return (BlstPublicKey.java:115-118, BlstSignature.java:152-155)."""
+    h = 1
+    for x in b:
+        h = (31 * h + (x - 256 if x > 127 else x)) & 0xFFFFFFFF
+    return h - (1 << 32) if h & 0x80000000 else h
+
+
+class PublicKey:
+    """impl/PublicKey.java:20-82: the SPI interface every implementation's key
+    type implements (a foreign implementation's key subclasses or registers)."""
+
+    __slots__ = ()
+
+    def to_bytes_compressed(self) -> bytes:  # pragma: no cover - interface
+        raise NotImplementedError
+
+    # BlstPublicKey.java:115-130: equal to ANY PublicKey with the same
+    # compressed bytes; the compressed bytes' hash
+    def __eq__(self, o):
+        if self is o:
+            return True
+        return isinstance(o, PublicKey) and self.to_bytes_compressed() == o.to_bytes_compressed()
+
+    def __hash__(self):
+        return java_bytes_hash(self.to_bytes_compressed())
+
+    def hash_code(self) -> int:
+        return java_bytes_hash(self.to_bytes_compressed())
+
+
+class Signature:
+    """impl/Signature.java:20-91: the SPI interface of signatures."""
+
+    __slots__ = ()
+
+    def to_bytes_compressed(self) -> bytes:  # pragma: no cover - interface
+        raise NotImplementedError
+
+    # BlstSignature.java:152-165
+    def __eq__(self, o):
+        if self is o:
+            return True
+        return isinstance(o, Signature) and self.to_bytes_compressed() == o.to_bytes_compressed()
+
+    def __hash__(self):
+        return java_bytes_hash(self.to_bytes_compressed())
+
+    def hash_code(self) -> int:
+        return java_bytes_hash(self.to_bytes_compressed())
+
+
+class HipPublicKey(PublicKey):
     """impl/PublicKey.java:20-82 (BlstPublicKey.java analogue).  Holds the
     compressed bytes; validity (!infinity && in G1) is computed on the GPU and
     memoised (BlstPublicKey.java:74-75)."""
@@ -108,14 +161,9 @@ class HipPublicKey:
     def verify_signature(self, signature: "HipSignature", message: bytes) -> bool:
         return signature.verify(self, message)
 
-    def __eq__(self, o):
-        return isinstance(o, HipPublicKey) and o._b == self._b
-
-    def __hash__(self):
-        return hash(self._b)
 
 
-class HipSignature:
+class HipSignature(Signature):
     """impl/Signature.java:20-91 (BlstSignature.java analogue)."""
 
     __slots__ = ("_b",)
@@ -181,11 +229,6 @@ class HipSignature:
             raise native.NativeError(rc, "tbls_aggregate_verify")
         return rc == native.SUCCESS and ok.value == 1
 
-    def __eq__(self, o):
-        return isinstance(o, HipSignature) and o._b == self._b
-
-    def __hash__(self):
-        return hash(self._b)
 
 
 class HipSecretKey:

@@ -165,11 +165,22 @@ void launch_points(const uint8_t* d_com, const uint8_t* d_proof, uint32_t un, g1
 }
 
 // compute_challenge digests of n host blobs (tb_sha256_host.h), blobs on
-// separate threads beyond the first
-void host_digests(const uint8_t* blobs, const uint8_t* com, size_t n, uint8_t* out) {
+// separate threads beyond the first.  Called under the tkzg_* entry points
+// (JNI): no exception may leave it -- a thread that cannot be created (busy
+// JVM, thread or memory limits) leaves its blob, and every blob without a
+// thread, to this thread.
+void host_digests(const uint8_t* blobs, const uint8_t* com, size_t n, uint8_t* out) noexcept {
+  auto one = [=](size_t i) { tbh::kzg_challenge_digest(blobs + i * BLOB, BLOB, com + 48 * i, out + 32 * i); };
   std::vector<std::thread> th;
-  for (size_t i = 1; i < n; i++) th.emplace_back([=]() { tbh::kzg_challenge_digest(blobs + i * BLOB, BLOB, com + 48 * i, out + 32 * i); });
-  if (n) tbh::kzg_challenge_digest(blobs, BLOB, com, out);
+  size_t spawned = 1;  // blobs [1, spawned) have a thread
+  try {
+    th.reserve(n ? n - 1 : 0);
+    for (; spawned < n; spawned++) th.emplace_back(one, spawned);
+  } catch (...) {
+    // std::system_error / std::bad_alloc: hash the rest here
+  }
+  if (n) one(0);
+  for (size_t i = spawned; i < n; i++) one(i);
   for (auto& t : th) t.join();
 }
 

@@ -98,6 +98,7 @@ struct dev_ctx {
   dbuf recs;  // partial records gathered for the final exponentiation (gather_partials, device 0)
   dbuf comb;  // (d 2^(8w)) g1 for w < 8, d < 256 (k_g1_comb_init): the signature pairs' G1 side
   hbuf hin, hout;
+  int load = 0;  // batches placed on this device and not yet finished (g_place_mu)
 };
 
 // Order a new user of c.ws (on stream s) after the previous one; call
@@ -110,6 +111,94 @@ std::vector<dev_ctx*> g_ctx;
 bool g_inited = false;
 
 size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
+
+// ---------------------------------------------------------------------------
+// Placement of a batch on the devices.  The reference runs
+// numThreads service workers side by side, each with its own batch
+// (AggregatingSignatureVerificationService.java:121-132, 202-205), so a
+// device should hold one caller's batch, not every caller's:
+//  * a batch of n sets is sharded over G = min(D', floor(n / shard_min)) >= 1
+//    devices (D' = the initialised devices, capped by n_gpus > 0), so a shard
+//    never drops below shard_min sets: below ~2,048 sets a device's partial is
+//    latency-bound (5.7 ms at 1,024 sets, 9.3 ms at 4,096, 12.3 ms at 16,384
+//    on one MI355X), and splitting it further gains
+//    little while it takes every device from every other caller;
+//  * the G devices are the least-loaded ones (batches placed and not yet
+//    finished), ties broken round-robin from a counter, then taken in
+//    ascending order (lock order; the lowest is the gather root);
+//  * shards are contiguous and balanced by key count, as teku_amd/dist.py
+//    shard_bounds.
+// TBLS_SHARD_MIN overrides shard_min (0: always every allowed device).
+// tbls_place_plan exposes the same function for CPU tests.
+// ---------------------------------------------------------------------------
+#define TB_SHARD_MIN 2048u
+uint32_t shard_min() {
+  static const uint32_t v = getenv("TBLS_SHARD_MIN") ? (uint32_t)atoi(getenv("TBLS_SHARD_MIN")) : TB_SHARD_MIN;
+  return v;
+}
+
+// n sets (keys(i) keys each) over D devices with loads load[0..D): returns G
+// and fills dev[0..G) (ascending) and cut[0..G] (cut[0] = 0, cut[G] = n).
+template <class KEYS>
+int place_plan(size_t n, const KEYS& keys, int D, int n_gpus, const int* load, uint32_t rr, uint32_t smin, int* dev, size_t* cut) {
+  if (D < 1) return 0;
+  int Gmax = (n_gpus > 0 && n_gpus < D) ? n_gpus : D;
+  size_t g = smin ? n / smin : (size_t)Gmax;
+  int G = (int)std::min<size_t>(std::max<size_t>(g, 1), (size_t)Gmax);
+  if ((size_t)G > n) G = n ? (int)n : 1;
+  std::vector<int> order(D);
+  for (int d = 0; d < D; d++) order[d] = d;
+  std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
+    const int la = load ? load[a] : 0, lb = load ? load[b] : 0;
+    if (la != lb) return la < lb;
+    return (uint32_t)(a - (int)(rr % (uint32_t)D) + D) % (uint32_t)D < (uint32_t)(b - (int)(rr % (uint32_t)D) + D) % (uint32_t)D;
+  });
+  std::sort(order.begin(), order.begin() + G);
+  for (int k = 0; k < G; k++) dev[k] = order[k];
+  uint64_t totalK = 0;
+  for (size_t i = 0; i < n; i++) totalK += keys(i) + 1;
+  for (int k = 0; k <= G; k++) cut[k] = n;
+  cut[0] = 0;
+  uint64_t acc = 0;
+  int k = 1;
+  for (size_t i = 0; i < n && k < G; i++) {
+    acc += keys(i) + 1;
+    while (k < G && acc * G >= totalK * (uint64_t)k) cut[k++] = i + 1;
+  }
+  return G;
+}
+
+// The live placement: plan under g_place_mu and count the batch on its
+// devices until the guard ends.
+std::mutex g_place_mu;
+uint32_t g_place_rr = 0;
+struct placed {
+  int G = 0;
+  std::vector<int> dev;
+  std::vector<size_t> cut;
+  placed() = default;
+  placed(const placed&) = delete;
+  placed& operator=(const placed&) = delete;
+  ~placed() {
+    std::lock_guard<std::mutex> lk(g_place_mu);
+    for (int k = 0; k < G; k++) g_ctx[dev[k]]->load--;
+  }
+};
+template <class KEYS>
+void place_batch(placed& pl, size_t n, const KEYS& keys, int n_gpus, uint32_t smin) {
+  std::lock_guard<std::mutex> lk(g_place_mu);
+  const int D = (int)g_ctx.size();
+  std::vector<int> load(D);
+  for (int d = 0; d < D; d++) load[d] = g_ctx[d]->load;
+  pl.dev.assign(D, 0);
+  pl.cut.assign(D + 1, 0);
+  pl.G = place_plan(n, keys, D, n_gpus, load.data(), g_place_rr++, smin, pl.dev.data(), pl.cut.data());
+  for (int k = 0; k < pl.G; k++) g_ctx[pl.dev[k]]->load++;
+}
+// one device for a whole call (single verifications, helpers)
+void place_one(placed& pl) {
+  place_batch(pl, 1, [](size_t) { return 1u; }, 0, 1);
+}
 
 // --------------------------------------------------------------------------
 // workspace layout for one device pipeline over n sets / K keys
@@ -902,11 +991,11 @@ struct rccl_api {
   decltype(&ncclGather) Gather = nullptr;
   decltype(&ncclGroupStart) GroupStart = nullptr;
   decltype(&ncclGroupEnd) GroupEnd = nullptr;
-  // One single-process communicator per participating-device count G, over
-  // devices 0 .. G-1: a batch sharded over G < (initialised devices) gathers
-  // on a G-rank communicator, so no rank of the collective is left waiting
-  // (batches smaller than the device count, or n_gpus < device count).
-  std::map<int, std::vector<ncclComm_t>> comms;
+  // One single-process communicator per participating device set (a bit
+  // mask over the library's devices): a batch placed on G of the initialised
+  // devices gathers on a G-rank communicator over exactly those, so no rank
+  // of the collective is left waiting.
+  std::map<uint32_t, std::vector<ncclComm_t>> comms;
 };
 rccl_api g_rccl;
 
@@ -927,22 +1016,26 @@ bool rccl_load_locked() {
   return g_rccl.ok;
 }
 
-// The G-rank communicator (created on first use); nullptr if RCCL is absent.
-const std::vector<ncclComm_t>* rccl_comms_locked(int G) {
+// The communicator over devices devs[0..G) (created on first use); nullptr
+// if RCCL is absent.
+const std::vector<ncclComm_t>* rccl_comms_locked(const std::vector<int>& devs, int G) {
   if (!rccl_load_locked() || G < 1 || G > (int)g_ctx.size()) return nullptr;
-  auto it = g_rccl.comms.find(G);
+  uint32_t mask = 0;
+  for (int k = 0; k < G; k++) mask |= 1u << devs[k];
+  auto it = g_rccl.comms.find(mask);
   if (it != g_rccl.comms.end()) return &it->second;
-  std::vector<int> devs;
-  for (int g = 0; g < G; g++) devs.push_back(g_ctx[g]->dev);
+  std::vector<int> hw;
+  for (int k = 0; k < G; k++) hw.push_back(g_ctx[devs[k]]->dev);
   std::vector<ncclComm_t> cm(G, nullptr);
-  if (g_rccl.CommInitAll(cm.data(), G, devs.data()) != ncclSuccess) return nullptr;
-  return &(g_rccl.comms[G] = cm);
+  if (g_rccl.CommInitAll(cm.data(), G, hw.data()) != ncclSuccess) return nullptr;
+  return &(g_rccl.comms[mask] = cm);
 }
 
-// Device records dpart[g] (on each device's stream) -> c0->recs (device 0).
-// Leaves the calling thread on device 0 (the caller's caller_device restores).
-int gather_partials(gather_mode mode, int G, const std::vector<uint8_t*>& dpart) {
-  dev_ctx* c0 = ctx_for(0);
+// Device records dpart[k] (on device devs[k]'s stream, k < G) -> the root's
+// recs buffer (root = devs[0]).  Leaves the calling thread on the root device
+// (the caller's caller_device restores).
+int gather_partials(gather_mode mode, const std::vector<int>& devs, int G, const std::vector<uint8_t*>& dpart) {
+  dev_ctx* c0 = ctx_for(devs[0]);
   HIPCHK(hipSetDevice(c0->dev));
   if (c0->recs.ensure((size_t)G * TBLS_PARTIAL_BYTES)) return TBLS_DEVICE_ERROR;
   uint8_t* recv = c0->recs.as<uint8_t>();
@@ -950,15 +1043,15 @@ int gather_partials(gather_mode mode, int G, const std::vector<uint8_t*>& dpart)
     const std::vector<ncclComm_t>* cm = nullptr;
     {
       std::lock_guard<std::mutex> lk(g_mu);
-      cm = rccl_comms_locked(G);
+      cm = rccl_comms_locked(devs, G);
     }
     // ncclGather writes comm_size * 580 bytes at the root: recv holds G records
     if (!cm || (int)cm->size() != G) return TBLS_DEVICE_ERROR;
-    for (int g = 0; g < G; g++) HIPCHK(hipSetDevice(ctx_for(g)->dev));  // every device reachable before the group opens
+    for (int g = 0; g < G; g++) HIPCHK(hipSetDevice(ctx_for(devs[g])->dev));  // every device reachable before the group opens
     if (g_rccl.GroupStart() != ncclSuccess) return TBLS_DEVICE_ERROR;
     int bad = 0;
     for (int g = 0; g < G; g++) {
-      dev_ctx* c = ctx_for(g);
+      dev_ctx* c = ctx_for(devs[g]);
       if (hipSetDevice(c->dev) != hipSuccess) {  // every rank must still join: the group ends below
         bad = 1;
         continue;
@@ -967,9 +1060,9 @@ int gather_partials(gather_mode mode, int G, const std::vector<uint8_t*>& dpart)
     }
     bad |= g_rccl.GroupEnd() != ncclSuccess;
     if (bad) return TBLS_DEVICE_ERROR;
-    // device 0's stream holds the gather; the others' sends complete on theirs
+    // the root's stream holds the gather; the others' sends complete on theirs
     for (int g = 1; g < G; g++) {
-      dev_ctx* c = ctx_for(g);
+      dev_ctx* c = ctx_for(devs[g]);
       HIPCHK(hipSetDevice(c->dev));
       HIPCHK(hipEventRecord(c->e_join[0], c->stream));
       HIPCHK(hipSetDevice(c0->dev));
@@ -980,7 +1073,7 @@ int gather_partials(gather_mode mode, int G, const std::vector<uint8_t*>& dpart)
   }
   if (mode == GATHER_PEER) {
     for (int g = 0; g < G; g++) {
-      dev_ctx* c = ctx_for(g);
+      dev_ctx* c = ctx_for(devs[g]);
       HIPCHK(hipSetDevice(c->dev));
       HIPCHK(hipMemcpyPeerAsync(recv + (size_t)g * TBLS_PARTIAL_BYTES, c0->dev, dpart[g], c->dev, TBLS_PARTIAL_BYTES, c->stream));
       if (g) {
@@ -994,7 +1087,7 @@ int gather_partials(gather_mode mode, int G, const std::vector<uint8_t*>& dpart)
   }
   std::vector<uint8_t> host((size_t)G * TBLS_PARTIAL_BYTES);
   for (int g = 0; g < G; g++) {
-    dev_ctx* c = ctx_for(g);
+    dev_ctx* c = ctx_for(devs[g]);
     HIPCHK(hipSetDevice(c->dev));
     if (c->hout.ensure(TBLS_PARTIAL_BYTES)) return TBLS_DEVICE_ERROR;
     HIPCHK(hipMemcpyAsync(c->hout.p, dpart[g], TBLS_PARTIAL_BYTES, hipMemcpyDeviceToHost, c->stream));
@@ -1018,10 +1111,13 @@ struct upload {
   }
 };
 
-int with_device0(const std::function<int(dev_ctx&)>& fn) {
+// one-call helpers run on the least-loaded device (place_one)
+int with_device(const std::function<int(dev_ctx&)>& fn) {
   const caller_device keep;
   if (ensure_init()) return TBLS_DEVICE_ERROR;
-  dev_ctx* c = ctx_for(0);
+  placed pl;
+  place_one(pl);
+  dev_ctx* c = ctx_for(pl.dev[0]);
   std::lock_guard<std::mutex> lk(c->mu);
   HIPCHK(hipSetDevice(c->dev));
   // ws may still be in use by device-API work queued on a caller's stream
@@ -1174,36 +1270,23 @@ int batch_verify_impl(const SET* sets, size_t n, const uint64_t* rand, int n_gpu
   if (n == 0) return TBLS_SUCCESS;  // BLS.java:240-241
   for (size_t i = 0; i < n; i++)
     if (sets[i].n_pks == 0) return TBLS_BAD_ARGUMENT;
-  int G = (int)g_ctx.size();
-  if (n_gpus > 0 && n_gpus < G) G = n_gpus;
-  if ((size_t)G > n) G = (int)n;
+  placed pl;  // the devices and shard cuts (place_plan), counted as busy until we return
+  place_batch(pl, n, [&](size_t i) { return sets[i].n_pks; }, n_gpus, shard_min());
+  const int G = pl.G;
   std::vector<double> dms(G, 0);
   int rc = TBLS_SUCCESS;
   if (G == 1 && !gather_forced()) {
-    rc = verify_on_device(0, sets, n, rand, ETH2_DST, 43, ok, nullptr, &dms[0]);
+    rc = verify_on_device(pl.dev[0], sets, n, rand, ETH2_DST, 43, ok, nullptr, &dms[0]);
   } else {
-    // contiguous shards balanced by key count
-    uint64_t totalK = 0;
-    for (size_t i = 0; i < n; i++) totalK += sets[i].n_pks + 1;
-    std::vector<size_t> cut(G + 1, n);
-    cut[0] = 0;
-    {
-      uint64_t acc = 0;
-      int g = 1;
-      for (size_t i = 0; i < n && g < G; i++) {
-        acc += sets[i].n_pks + 1;
-        while (g < G && acc * G >= totalK * (uint64_t)g) cut[g++] = i + 1;  // as dist.shard_bounds
-      }
-    }
-    // every device's lock for the whole batch, in device order (no deadlock)
+    // only the placed devices' locks, for the whole batch, in ascending device order (no deadlock)
     std::vector<std::unique_lock<std::mutex>> locks;
-    for (int g = 0; g < G; g++) locks.emplace_back(ctx_for(g)->mu);
+    for (int g = 0; g < G; g++) locks.emplace_back(ctx_for(pl.dev[g])->mu);
     std::vector<uint8_t*> dpart(G, nullptr);
     std::vector<int> rcs(G, 0);
     auto stage = [&](int g) {
       ws_layout L;
       uint32_t nn;
-      rcs[g] = shard_launch(ctx_for(g), sets, cut[g], cut[g + 1], rand, ETH2_DST, 43, &dpart[g], L, &nn);
+      rcs[g] = shard_launch(ctx_for(pl.dev[g]), sets, pl.cut[g], pl.cut[g + 1], rand, ETH2_DST, 43, &dpart[g], L, &nn);
     };
     if (G == 1) {
       stage(0);
@@ -1214,10 +1297,11 @@ int batch_verify_impl(const SET* sets, size_t n, const uint64_t* rand, int n_gpu
     }
     for (int g = 0; g < G; g++)
       if (rcs[g]) return rcs[g];
-    rc = gather_partials(gather_sel(), G, dpart);
-    if (!rc) rc = launch_final(*ctx_for(0), ctx_for(0)->recs.p, (uint32_t)G, ctx_for(0)->stream, ok);
+    rc = gather_partials(gather_sel(), pl.dev, G, dpart);
+    dev_ctx* root = ctx_for(pl.dev[0]);
+    if (!rc) rc = launch_final(*root, root->recs.p, (uint32_t)G, root->stream, ok);
     for (int g = 0; g < G && !rc; g++) {
-      dev_ctx* c = ctx_for(g);
+      dev_ctx* c = ctx_for(pl.dev[g]);
       (void)hipSetDevice(c->dev);
       (void)hipStreamSynchronize(c->stream);
       float ms = 0;
@@ -1292,7 +1376,9 @@ static int verify_one(const uint8_t* pks, uint32_t n_pks, const uint8_t* msg, si
   tbls_set s = {pks, n_pks, msg, (uint32_t)len, sig};
   uint8_t code = 0;
   uint64_t one = 1;
-  int rc = verify_on_device(0, &s, 1, &one, dst, (uint32_t)dlen, ok, &code, nullptr);
+  placed pl;
+  place_one(pl);
+  int rc = verify_on_device(pl.dev[0], &s, 1, &one, dst, (uint32_t)dlen, ok, &code, nullptr);
   if (code_out) *code_out = code;
   return rc;
 }
@@ -1368,28 +1454,29 @@ extern "C" int tbls_verify_each(const tbls_set* sets, size_t n, int n_gpus, int*
   const caller_device keep;
   if (ensure_init()) return TBLS_DEVICE_ERROR;
   if (n == 0) return TBLS_SUCCESS;
-  int G = (int)g_ctx.size();
-  if (n_gpus > 0 && n_gpus < G) G = n_gpus;
   const size_t nchunks = (n + TB_EACH_CHUNK - 1) / TB_EACH_CHUNK;
-  if ((size_t)G > nchunks) G = (int)nchunks;
+  // one device per chunk, at most nchunks least-loaded devices (place_plan with
+  // one-set "chunks"); chunk k runs on pl.dev[k % G], one host thread per device
+  placed pl;
+  place_batch(pl, nchunks, [](size_t) { return 0u; }, n_gpus, 1);
+  const int G = pl.G;
   std::vector<uint8_t> ok(n, 0);
   std::vector<int> rcs(G, 0);
-  // chunk k runs on device k % G; one host thread per device
-  auto work = [&](int dv) {
-    for (size_t k = dv; k < nchunks && !rcs[dv]; k += G) {
+  auto work = [&](int k0) {
+    for (size_t k = k0; k < nchunks && !rcs[k0]; k += G) {
       const size_t lo = k * TB_EACH_CHUNK, hi = std::min(n, lo + TB_EACH_CHUNK);
-      rcs[dv] = run_each(dv, sets, lo, hi, ok.data() + lo);
+      rcs[k0] = run_each(pl.dev[k0], sets, lo, hi, ok.data() + lo);
     }
   };
   if (G == 1) {
     work(0);
   } else {
     std::vector<std::thread> th;
-    for (int dv = 0; dv < G; dv++) th.emplace_back(work, dv);
+    for (int k = 0; k < G; k++) th.emplace_back(work, k);
     for (auto& x : th) x.join();
   }
-  for (int dv = 0; dv < G; dv++)
-    if (rcs[dv]) return rcs[dv];
+  for (int k = 0; k < G; k++)
+    if (rcs[k]) return rcs[k];
   for (size_t i = 0; i < n; i++) ok_per_set[i] = (sets[i].n_pks != 0 && ok[i]) ? 1 : 0;  // BLS.java:193-195
   return TBLS_SUCCESS;
 }
@@ -1435,11 +1522,13 @@ extern "C" int tbls_aggregate_verify(const uint8_t* pks, const uint8_t* const* m
   std::vector<tbls_set> sets(n);
   std::vector<uint64_t> ones(n, 1);
   for (size_t i = 0; i < n; i++) sets[i] = {pks + 48 * i, 1, msgs[i], msg_lens[i], i == 0 ? sig : INF_SIG};
-  return verify_on_device(0, sets.data(), n, ones.data(), ETH2_DST, 43, ok, nullptr, nullptr);
+  placed pl;
+  place_one(pl);
+  return verify_on_device(pl.dev[0], sets.data(), n, ones.data(), ETH2_DST, 43, ok, nullptr, nullptr);
 }
 
 extern "C" int tbls_pk_validate(const uint8_t pk[48]) {
-  return with_device0([&](dev_ctx& c) -> int {
+  return with_device([&](dev_ctx& c) -> int {
     upload u;
     size_t o = u.add(pk, 48);
     uint8_t* d;
@@ -1454,7 +1543,7 @@ extern "C" int tbls_pk_validate(const uint8_t pk[48]) {
 }
 
 extern "C" int tbls_sig_validate(const uint8_t sig[96], int* is_inf) {
-  return with_device0([&](dev_ctx& c) -> int {
+  return with_device([&](dev_ctx& c) -> int {
     upload u;
     size_t o = u.add(sig, 96);
     uint8_t* d;
@@ -1473,7 +1562,7 @@ extern "C" int tbls_sig_validate(const uint8_t sig[96], int* is_inf) {
 // ---- batched deserialization / aggregation ----
 extern "C" int tbls_pk_validate_many(const uint8_t* pks, size_t n, uint8_t* codes) {
   if (n == 0) return TBLS_SUCCESS;
-  return with_device0([&](dev_ctx& c) -> int {
+  return with_device([&](dev_ctx& c) -> int {
     upload u;
     size_t o = u.add(pks, 48 * n);
     uint8_t* d;
@@ -1489,7 +1578,7 @@ extern "C" int tbls_pk_validate_many(const uint8_t* pks, size_t n, uint8_t* code
 
 extern "C" int tbls_sig_validate_many(const uint8_t* sigs, size_t n, uint8_t* codes, uint8_t* is_inf) {
   if (n == 0) return TBLS_SUCCESS;
-  return with_device0([&](dev_ctx& c) -> int {
+  return with_device([&](dev_ctx& c) -> int {
     upload u;
     size_t o = u.add(sigs, 96 * n);
     uint8_t* d;
@@ -1514,7 +1603,7 @@ extern "C" int tbls_aggregate_sigs_many(const uint8_t* sigs, const uint32_t* off
   for (size_t g = 0; g < groups; g++)
     if (off[g + 1] < off[g]) return TBLS_BAD_ARGUMENT;
   const size_t total = off[groups];
-  return with_device0([&](dev_ctx& c) -> int {
+  return with_device([&](dev_ctx& c) -> int {
     upload u;
     size_t os = u.add(sigs, 96 * total);
     size_t oo = u.add(off, 4 * (groups + 1));
@@ -1533,7 +1622,7 @@ extern "C" int tbls_aggregate_sigs_many(const uint8_t* sigs, const uint32_t* off
 
 extern "C" int tbls_aggregate_pks(const uint8_t* pks, size_t k, uint8_t out[48]) {
   if (k == 0) return TBLS_BAD_ARGUMENT;  // BlstPublicKey.java:56 checkArgument
-  return with_device0([&](dev_ctx& c) -> int {
+  return with_device([&](dev_ctx& c) -> int {
     upload u;
     size_t o = u.add(pks, 48 * k);
     uint8_t* d;
@@ -1556,7 +1645,7 @@ extern "C" int tbls_aggregate_pks(const uint8_t* pks, size_t k, uint8_t out[48])
 }
 
 extern "C" int tbls_aggregate_sigs(const uint8_t* sigs, size_t k, uint8_t out[96]) {
-  return with_device0([&](dev_ctx& c) -> int {
+  return with_device([&](dev_ctx& c) -> int {
     upload u;
     size_t o = u.add(sigs, 96 * k);
     uint8_t* d;
@@ -1574,7 +1663,7 @@ extern "C" int tbls_aggregate_sigs(const uint8_t* sigs, size_t k, uint8_t out[96
 
 extern "C" int tbls_hash_to_g2(const uint8_t* msg, size_t len, const uint8_t* dst, size_t dlen, uint8_t out[96]) {
   if (dlen > 255) return TBLS_BAD_ARGUMENT;
-  return with_device0([&](dev_ctx& c) -> int {
+  return with_device([&](dev_ctx& c) -> int {
     upload u;
     uint32_t off[2] = {0, (uint32_t)len};
     size_t om = u.add(msg, len), oo = u.add(off, 8), od = u.add(dst, dlen);
@@ -1594,7 +1683,7 @@ extern "C" int tbls_sign(const uint8_t sk[32], const uint8_t* msg, size_t len, c
   bool zero = true;
   for (int i = 0; i < 32; i++) zero = zero && sk[i] == 0;
   if (zero) return TBLS_BAD_SCALAR;  // BlstBLS12381.java:54-56
-  return with_device0([&](dev_ctx& c) -> int {
+  return with_device([&](dev_ctx& c) -> int {
     upload u;
     uint64_t w[4];
     sk_to_words(sk, w);
@@ -1612,7 +1701,7 @@ extern "C" int tbls_sign(const uint8_t sk[32], const uint8_t* msg, size_t len, c
 
 extern "C" int tbls_sk_to_pk(const uint8_t sk[32], uint8_t out[48]) {
   if (!sk_in_range(sk)) return TBLS_BAD_SCALAR;
-  return with_device0([&](dev_ctx& c) -> int {
+  return with_device([&](dev_ctx& c) -> int {
     upload u;
     uint64_t w[4];
     sk_to_words(sk, w);
@@ -1697,6 +1786,20 @@ extern "C" int tbls_dev_batch_stage_profile(int device, const tbls_dev_batch* b,
   return partial_timed(device, b, stream, partial_out, stage_ms, true);
 }
 
+extern "C" int tbls_place_plan(size_t n, const uint32_t* n_pks, int n_devices, int n_gpus, const int* load, uint32_t rr,
+                               uint32_t shard_min_sets, int* dev_out, size_t* cut_out) {
+  if (n_devices < 1 || n_devices > 32 || !dev_out || !cut_out) return -TBLS_BAD_ARGUMENT;
+  std::vector<int> dev(n_devices);
+  std::vector<size_t> cut(n_devices + 1);
+  const int G = place_plan(n, [&](size_t i) { return n_pks ? n_pks[i] : 1u; }, n_devices, n_gpus, load, rr, shard_min_sets, dev.data(),
+                           cut.data());
+  for (int k = 0; k < G; k++) dev_out[k] = dev[k];
+  for (int k = 0; k <= G; k++) cut_out[k] = cut[k];
+  return G;
+}
+
+extern "C" uint32_t tbls_shard_min(void) { return shard_min(); }
+
 extern "C" int tbls_acc_plan(uint32_t n, uint32_t* per, uint32_t* nseg, int* split) {
   const pair_plan pp(n);
   if (per) *per = pp.per;
@@ -1707,7 +1810,7 @@ extern "C" int tbls_acc_plan(uint32_t n, uint32_t* per, uint32_t* nseg, int* spl
 
 // batched helpers for building synthetic workloads on the device
 extern "C" int tbls_sk_to_pk_many(const uint8_t* sks, size_t n, uint8_t* out) {
-  return with_device0([&](dev_ctx& c) -> int {
+  return with_device([&](dev_ctx& c) -> int {
     std::vector<uint64_t> w(4 * n);
     for (size_t i = 0; i < n; i++) sk_to_words(sks + 32 * i, &w[4 * i]);
     upload u;
@@ -1725,7 +1828,7 @@ extern "C" int tbls_sk_to_pk_many(const uint8_t* sks, size_t n, uint8_t* out) {
 extern "C" int tbls_sign_many(const uint8_t* sks, const uint8_t* msgs, const uint32_t* msg_off, size_t n, const uint8_t* dst, size_t dlen,
                               uint8_t* out) {
   if (dlen > 255) return TBLS_BAD_ARGUMENT;
-  return with_device0([&](dev_ctx& c) -> int {
+  return with_device([&](dev_ctx& c) -> int {
     std::vector<uint64_t> w(4 * n);
     for (size_t i = 0; i < n; i++) sk_to_words(sks + 32 * i, &w[4 * i]);
     upload u;

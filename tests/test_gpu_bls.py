@@ -543,3 +543,36 @@ def test_batched_deserialization_and_aggregation(hip, sets8):
         if g:
             native.check(L.tbls_aggregate_sigs(b"".join(g), len(g), one), "aggregate_sigs")
             assert one.raw == r
+
+
+def test_concurrent_callers_threads(hip, sets8):
+    """Service workers call batchVerify side by side (the reference's numThreads
+    workers, AggregatingSignatureVerificationService.java:121-132, 202-205):
+    each batch is placed on the least-loaded device and holds only that
+    device's lock, and every caller gets its own verdict (valid and tampered
+    batches interleaved from 4 threads)."""
+    import threading
+
+    bls = hip[0]
+    sks, pks, msgs, sigs = sets8
+    bad = list(sigs)
+    bad[6] = O.sign(sks[6], msgs[5])
+    results, errors = {}, []
+
+    def worker(w):
+        try:
+            for k in range(6):
+                tampered = (w + k) % 2 == 1
+                results[(w, k)] = (_raw(bls, pks, msgs, bad if tampered else sigs), not tampered)
+        except Exception as e:  # pragma: no cover - reported below
+            errors.append(e)
+
+    th = [threading.Thread(target=worker, args=(w,)) for w in range(4)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    assert not errors, errors
+    assert len(results) == 24
+    for key, (got, want) in results.items():
+        assert got is want, key
