@@ -45,7 +45,9 @@ extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_MIN_WAVES)
   static_assert(sizeof(g2a) == 48 * 4, "g2a is 48 words");
   TB_UNROLL for (int k = 0; k < 48; k++) ow[k] = (uint32_t)__shfl_xor((int)qw[k], 1);
   if (j) return;
-  const g2j h = g2_clear_cofactor(iso_map_jac(e2p_add_aff_aff(q, o)));
+  const g2j p = iso_map_jac(e2p_add_aff_aff(q, o));
+  g2j h;
+  if (!g2_clear_cofactor_nx(h, p)) h = g2_clear_cofactor(p);  // exceptional chain or infinity: exact (tb_stages.h stage_set_hash)
   g2a a;
   const bool ok = jac_to_aff(a, h);
   if (!ok) {

@@ -396,6 +396,47 @@ TB_HD TB_NOINLINE jac<F> jac_mul_xabs(const jac<F>& P) {
   return r;
 }
 
+// ---- branch-free forms (the throughput hash, k_set_hash) --------------------
+// add-2007-bl without the exceptional branch: P == +-Q or an infinite input
+// gives Z3 = 0 (H = 0, or Z3 = 2 Z1 Z2 H with Z1 Z2 = 0), and Z = 0 stays 0
+// through doubling and addition.  So a chain of these that ends with Z != 0
+// met no exceptional case and equals the exact formulas' result; a chain that
+// ends with Z = 0 is recomputed with the exact functions by the caller.  No
+// branch, no call: the chain keeps its points in registers.
+template <typename F>
+TB_HD TB_INLINE jac<F> jac_add_nx(const jac<F>& p, const jac<F>& q) {
+  F Z1Z1 = f_sqr(p.z);
+  F Z2Z2 = f_sqr(q.z);
+  F U1 = f_mul(p.x, Z2Z2);
+  F U2 = f_mul(q.x, Z1Z1);
+  F S1 = f_mul(f_mul(p.y, q.z), Z2Z2);
+  F S2 = f_mul(f_mul(q.y, p.z), Z1Z1);
+  F H = f_sub(U2, U1);
+  F r = f_dbl(f_sub(S2, S1));
+  F I = f_sqr(f_dbl(H));
+  F J = f_mul(H, I);
+  F V = f_mul(U1, I);
+  jac<F> o;
+  o.x = f_sub(f_sub(f_sqr(r), J), f_dbl(V));
+  o.y = f_sub(f_mul(r, f_sub(V, o.x)), f_dbl(f_mul(S1, J)));
+  o.z = f_mul(f_sub(f_sub(f_sqr(f_add(p.z, q.z)), Z1Z1), Z2Z2), H);
+  return o;
+}
+
+// [|x|]P branch-free: the doubling runs of XRUN_DBL as one loop over the runs
+// (one doubling body and one addition body in the code: a ~180 KB leaf instead
+// of jac_mul_xabs's ~360 KB of unrolled runs), the additions jac_add_nx.
+template <typename F>
+TB_HD TB_NOINLINE jac<F> jac_mul_xabs_nx(const jac<F>& P) {
+  jac<F> r = P;
+  TB_NOUNROLL for (int k = 0; k < 6; k++) {
+    const int nd = k == 0 ? 1 : k == 1 ? 2 : k == 2 ? 3 : k == 3 ? 9 : k == 4 ? 32 : 16;  // XRUN_DBL[k]
+    TB_NOUNROLL for (int i = 0; i < nd; i++) r = jac_dbl_i(r);
+    if (k < 5) r = jac_add_nx(r, P);
+  }
+  return r;
+}
+
 // [x]P with x = -0xd201000000010000
 // TB_G1_XRUNS=1: the same for G1 (g1_mul_x, the key subgroup check): its
 // doubling loop loses 18 scratch accesses per step; built and CPU-tested, not
@@ -443,6 +484,21 @@ TB_HD TB_NOINLINE g2j g2_clear_cofactor(const g2j& p) {
   r = jac_add(r, jac_neg(t2));
   r = jac_add(r, g2_psi2(jac_dbl(p)));
   return r;
+}
+
+// The same h_eff P branch-free (jac_add_nx, jac_mul_xabs_nx), with the terms
+// that need P folded first so that P dies before the multiplications:
+//   A = psi^2(2P) - P - psi(P),  t1 = [x]P,  result = [x](t1 + psi(P)) - t1 + A.
+// Returns false when the chain met an exceptional case or the result is
+// infinite (Z = 0): the caller then runs g2_clear_cofactor (exact).
+TB_HD TB_INLINE bool g2_clear_cofactor_nx(g2j& out, const g2j& p) {
+  const g2j t2 = g2_psi(p);
+  const g2j A = jac_add_nx(jac_add_nx(g2_psi2(jac_dbl_i(p)), jac_neg(p)), jac_neg(t2));
+  const g2j t1 = jac_mul_xabs_nx(p);  // [|x|]P = -[x]P
+  // [x]([x]P + psi P) = -[|x|](psi P - [|x|]P)
+  const g2j t3 = jac_mul_xabs_nx(jac_add_nx(t2, jac_neg(t1)));
+  out = jac_add_nx(jac_add_nx(jac_neg(t3), t1), A);  // t3 - t1 + A with t3 = -[|x|](.), -t1 = +[|x|]P
+  return !fp2_is_zero(out.z);
 }
 
 }  // namespace tb

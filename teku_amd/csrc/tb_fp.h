@@ -495,52 +495,66 @@ TB_HD TB_INLINE fp fp_inv_body(fp A) {
 TB_HD TB_NOINLINE fp fp_inv(fp A) { return fp_inv_body(A); }
 // a^e for a fixed exponent given as a sliding-window schedule (w = 4,
 // tools/gen_constants.py window_schedule): 375 squarings + 86 multiplications
-// for the 379-bit square-root exponents, vs 378 + 228 for binary.
+// for the 379-bit square-root exponents, vs 378 + 228 for binary.  The chain
+// stays on 14 x 29-bit limbs from the first product to the last: a Montgomery
+// product of normalized limbs returns normalized limbs (mont29), so the
+// to29 / from29 conversions of fp_mul (a third of a lone product's non-
+// multiply instructions) happen once per exponentiation instead of once per
+// step.
 TB_HD TB_NOINLINE fp fp_pow_win(const fp& a, uint32_t first, const uint16_t* sched, int nstep) {
-  fp tab[8];  // a^1, a^3, ..., a^15
-  tab[0] = a;
-  const fp a2 = fp_sqr(a);
-  TB_NOUNROLL for (int i = 1; i < 8; i++) tab[i] = fp_mul(tab[i - 1], a2);
-  fp r = tab[first];
-  TB_NOUNROLL for (int k = 0; k < nstep; k++) {
-    const uint32_t e = sched[k];
-    TB_NOUNROLL for (uint32_t j = 0; j < (e >> 4); j++) r = fp_sqr(r);
-    if ((e & 15u) < 8u) r = fp_mul(r, tab[e & 15u]);
-  }
-  return r;
-}
-// Two bases, same fixed exponent, interleaved: every squaring / product step
-// is a 2-wide fp_*_n<2>, giving the multiplier two independent chains (a lone
-// exponentiation is one long dependent chain).
-TB_HD TB_NOINLINE void fp_pow_win2(fp& r0, fp& r1, const fp& a0, const fp& a1, uint32_t first, const uint16_t* sched, int nstep) {
-  fp t0[8], t1[8], sq[2], r[2];
-  t0[0] = a0;
-  t1[0] = a1;
-  {
-    const fp x[2] = {a0, a1};
-    fp_sqr_n<2>(sq, x);
-  }
-  TB_NOUNROLL for (int i = 1; i < 8; i++) {
-    const fp x[2] = {t0[i - 1], t1[i - 1]};
-    fp_mul_n<2>(r, x, sq);
-    t0[i] = r[0];
-    t1[i] = r[1];
-  }
-  r[0] = t0[first];
-  r[1] = t1[first];
+  uint32_t tab[8][1][14];  // a^1, a^3, ..., a^15
+  uint32_t a2[1][14], r[1][14], t[1][14];
+  to29(tab[0][0], a);
+  mont29<1, true>(a2, tab[0], tab[0]);
+  TB_NOUNROLL for (int i = 1; i < 8; i++) mont29<1, false>(tab[i], tab[i - 1], a2);
+  TB_UNROLL for (int i = 0; i < 14; i++) r[0][i] = tab[first][0][i];
   TB_NOUNROLL for (int k = 0; k < nstep; k++) {
     const uint32_t e = sched[k];
     TB_NOUNROLL for (uint32_t j = 0; j < (e >> 4); j++) {
-      const fp x[2] = {r[0], r[1]};
-      fp_sqr_n<2>(r, x);
+      mont29<1, true>(t, r, r);
+      TB_UNROLL for (int i = 0; i < 14; i++) r[0][i] = t[0][i];
+    }
+    if ((e & 15u) < 8u) {
+      mont29<1, false>(t, r, tab[e & 15u]);
+      TB_UNROLL for (int i = 0; i < 14; i++) r[0][i] = t[0][i];
+    }
+  }
+#if !TB_DEVICE_PASS && defined(TB_COUNT_MULS)
+  for (int k = 0; k < nstep; k++) {
+    tb_mul_count += (sched[k] >> 4) + ((sched[k] & 15u) < 8u ? 1 : 0);
+    tb_sqr_count += sched[k] >> 4;
+  }
+  tb_mul_count += 8;  // the table
+  tb_sqr_count += 1;
+#endif
+  fp out;
+  from29(out, r[0]);
+  return out;
+}
+// Two bases, same fixed exponent, interleaved: every squaring / product step
+// is a 2-wide mont29<2>, giving the multiplier two independent chains (a lone
+// exponentiation is one long dependent chain); 29-bit limbs throughout as above.
+TB_HD TB_NOINLINE void fp_pow_win2(fp& r0, fp& r1, const fp& a0, const fp& a1, uint32_t first, const uint16_t* sched, int nstep) {
+  uint32_t tab[8][2][14];
+  uint32_t sq[2][14], r[2][14], t[2][14];
+  to29(tab[0][0], a0);
+  to29(tab[0][1], a1);
+  mont29<2, true>(sq, tab[0], tab[0]);
+  TB_NOUNROLL for (int i = 1; i < 8; i++) mont29<2, false>(tab[i], tab[i - 1], sq);
+  TB_UNROLL for (int j = 0; j < 2; j++) TB_UNROLL for (int i = 0; i < 14; i++) r[j][i] = tab[first][j][i];
+  TB_NOUNROLL for (int k = 0; k < nstep; k++) {
+    const uint32_t e = sched[k];
+    TB_NOUNROLL for (uint32_t j = 0; j < (e >> 4); j++) {
+      mont29<2, true>(t, r, r);
+      TB_UNROLL for (int q = 0; q < 2; q++) TB_UNROLL for (int i = 0; i < 14; i++) r[q][i] = t[q][i];
 #if !TB_DEVICE_PASS && defined(TB_COUNT_MULS)
       tb_mul_count += 2;
       tb_sqr_count += 2;
 #endif
     }
     if ((e & 15u) < 8u) {
-      const fp x[2] = {r[0], r[1]}, y[2] = {t0[e & 15u], t1[e & 15u]};
-      fp_mul_n<2>(r, x, y);
+      mont29<2, false>(t, r, tab[e & 15u]);
+      TB_UNROLL for (int q = 0; q < 2; q++) TB_UNROLL for (int i = 0; i < 14; i++) r[q][i] = t[q][i];
 #if !TB_DEVICE_PASS && defined(TB_COUNT_MULS)
       tb_mul_count += 2;
 #endif
@@ -550,8 +564,8 @@ TB_HD TB_NOINLINE void fp_pow_win2(fp& r0, fp& r1, const fp& a0, const fp& a1, u
   tb_mul_count += 16;  // the table
   tb_sqr_count += 2;
 #endif
-  r0 = r[0];
-  r1 = r[1];
+  from29(r0, r[0]);
+  from29(r1, r[1]);
 }
 TB_HD TB_INLINE fp fp_sqrt_cand(const fp& a) { return fp_pow_win(a, EXPW_SQRT_FIRST, EXPW_SQRT, EXPW_SQRT_N); }     // a^((p+1)/4)
 TB_HD TB_INLINE fp fp_pow_pm3d4(const fp& a) { return fp_pow_win(a, EXPW_PM3D4_FIRST, EXPW_PM3D4, EXPW_PM3D4_N); }  // a^((p-3)/4)

@@ -79,8 +79,18 @@ TB_HD TB_INLINE int stage_set_sig(const uint8_t* b96, uint64_t r, g2j& rs) {
 }
 
 // Q = hash_to_G2(m) affine; false for the (negligible) infinity case
+// The cofactor clearing branch-free in the caller (g2_clear_cofactor_nx: no
+// call frames around its additions; ~half of the hash), the exact
+// g2_clear_cofactor only when that chain meets an exceptional case or ends at
+// infinity.  Same Q as hash_to_g2 + jac_to_aff.
 TB_HD TB_INLINE bool stage_set_hash(const xmd_ctx& c, g2a& Q) {
-  g2j h = hash_to_g2(c);
+  fp2 u0, u1;
+  hash_to_field_fp2(u0, u1, c);
+  g2a q0, q1;
+  map_to_curve_sswu2(q0, q1, u0, u1);
+  const g2j p = iso_map_jac(e2p_add_aff_aff(q0, q1));
+  g2j h;
+  if (!g2_clear_cofactor_nx(h, p)) h = g2_clear_cofactor(p);
   bool ok = jac_to_aff(Q, h);
   if (!ok) {
     Q.x = fp2_zero();

@@ -47,6 +47,9 @@ enum {
   TOP_FP_SQR_RAW = 33,
   TOP_FP2_MUL_RAW = 34,
   TOP_FP2_SQR_RAW = 35,
+  // branch-free cofactor clearing (tb_curve.h g2_clear_cofactor_nx): out = u32
+  // ok flag || its affine result || the exact g2_clear_cofactor's
+  TOP_CLEAR_COF_NX = 36,
 };
 
 #define TB_TEST_IN 1536
@@ -245,6 +248,14 @@ TB_HD TB_NOINLINE void test_op(int op, const uint8_t* in, uint8_t* out) {
       tio_put_g2j_aff(out, g2_clear_cofactor(p));
       break;
     }
+    case TOP_CLEAR_COF_NX: {
+      g2j p = {tio_fp2(in), tio_fp2(in + 96), fp2_one()}, h;
+      const bool ok = g2_clear_cofactor_nx(h, p);
+      tio_put_u32(out, ok ? 1u : 0u);
+      tio_put_g2j_aff(out + 4, h);
+      tio_put_g2j_aff(out + 4 + 200, g2_clear_cofactor(p));
+      break;
+    }
     // whole per-item stage bodies (tb_stages.h), used to count work per unit
     case TOP_STAGE_PK: {
       g1a a;
@@ -273,7 +284,9 @@ TB_HD TB_NOINLINE void test_op(int op, const uint8_t* in, uint8_t* out) {
       c.msg = in + 8;
       c.dst = in + 8 + 1024;
       g2a q;
-      tio_put_u32(out, stage_set_hash(c, q) ? 1u : 0u);
+      const bool ok = stage_set_hash(c, q);
+      tio_put_u32(out, ok ? 1u : 0u);
+      if (ok) g2_compress(out + 4, q, false);
       break;
     }
     case TOP_G2_JADD: {
