@@ -45,22 +45,28 @@ from teku_amd.dist import all_gather_partials, shard_bounds  # noqa: E402
 # Roofline: algorithmic work = Fp products (M) per unit,
 # counted by tools/count_muls.py on the host build of the same stage code,
 # x 300 32x32->64 MACs per M (12-limb CIOS Montgomery, 2*12^2 + 12).  Peak =
-# the measured v_mad_u64_u32 issue rate (tools/microbench/fp_rates.hip,
-# profiles/r01_microbench_fp_rates.json: 47.6 lane-ops/CU/clk) x CUs x 2.4 GHz.
-# The kernels' own 14 x 29-bit products issue 392 v_mad_u64_u32 per M (301
-# per squaring); "issue_frac" reports that instruction-level fraction too.
+# the measured v_mad_u64_u32 throughput of the whole chip at four waves per
+# SIMD (tools/microbench/mad_peak.hip, profiles/r04_microbench_mad_peak.json:
+# 3.39e13 MAD/s = 59.1 lane-ops/CU/clk at the 2.24 GHz the box ran; rounds 1-3
+# used 47.6 lane-ops/CU/clk x 2.4 GHz = 2.92e13 from a microbenchmark whose
+# inline-asm multiply-adds each got a hazard s_nop).  One wave per SIMD -- the
+# occupancy of every 512-register kernel -- issues at most 2.65e13 MAD/s
+# (47.1 lane-ops/CU/clk): "frac_1wave" reports the dominant kernel against
+# that ceiling.  The kernels' own 14 x 29-bit products issue 392
+# v_mad_u64_u32 per M (301 per squaring); "issue_frac" reports that
+# instruction-level fraction too.
 # ---------------------------------------------------------------------------
 MAC_PER_M = 300
-MAD_RATE_PER_CU_CLK = 47.6
-CLOCK_HZ = 2.4e9
+MAD_PEAK_PER_S = 3.3923e13  # 256 CUs, four waves per SIMD (measured)
+MAD_1WAVE_PER_S = 2.6492e13  # one wave per SIMD (measured)
 STAGES = ["pk_decompress", "set_pk", "set_sig", "set_hash", "g2_sum", "miller", "fp12_prod"]
 STAGE_KERNEL = {
     "pk_decompress": "k_pk_decompress",
-    "set_pk": "k_set_pk",
-    "set_sig": "k_sig_check",
-    "set_hash": "k_set_hash",
+    "set_pk": "k_set_pk_w2",
+    "set_sig": "k_sig_check_w2",
+    "set_hash": "k_set_hash_w2 + k_set_hash_fix",
     "g2_sum": "k_msm_bucket + k_msm_bucket_sum + k_msm_bitsum_pairs",
-    "miller": "k_miller_lines + k_miller_acc2",
+    "miller": "k_miller_lines_lds + k_miller_acc2",
     "fp12_prod": "k_fp12_prod_wave",
 }
 STAGE_UNITS = {"pk_decompress": "keys", "set_pk": "sets", "set_sig": "sets", "set_hash": "sets", "g2_sum": "sets", "miller": "pairs", "fp12_prod": "pairs"}
@@ -68,8 +74,10 @@ _MC = os.path.join(ROOT, "tools", "mul_counts.json")
 M_PER_UNIT = json.load(open(_MC)) if os.path.exists(_MC) else {}
 
 
-def peak_mac_per_s(device):
-    return MAD_RATE_PER_CU_CLK * torch.cuda.get_device_properties(device).multi_processor_count * CLOCK_HZ
+def peak_mac_per_s(device, one_wave=False):
+    """The measured chip-wide v_mad_u64_u32 rate, scaled to this device's CU count."""
+    cus = torch.cuda.get_device_properties(device).multi_processor_count
+    return (MAD_1WAVE_PER_S if one_wave else MAD_PEAK_PER_S) * cus / 256
 
 
 def acc_plan(S):
@@ -96,7 +104,7 @@ def plan_counts(S):
             mads["miller"] = round(mads["miller"] + d / 3 * mc.get("mads_per_fp2_mul", 980))
         mc["mads_per_unit"] = mads
     kern = dict(STAGE_KERNEL)
-    lines_k = "k_miller_lines" if os.environ.get("TBLS_LINES_LDS", "1") == "0" else "k_miller_lines_lds"
+    lines_k = "k_miller_lines_lds"
     if seg:
         kern["miller"] = f"{lines_k} + k_miller_accs"
     return mc, kern, {"per": per, "nseg": nseg, "kernel": "k_miller_accs" if seg else "k_miller_acc1/2"}
@@ -130,6 +138,8 @@ def roofline_entry(stage_ms, S, device, ms_per_step):
         "peak": peak / 1e12,
         "unit": "T MAC/s (32x32->64)",
         "frac": (achieved / peak) if achieved else None,
+        "peak_1wave": peak_mac_per_s(device, True) / 1e12,
+        "frac_1wave": (achieved / peak_mac_per_s(device, True)) if achieved else None,
         "traffic": traffic,
         "model": "SURVEY.md 8(d): Fp products per unit (tools/mul_counts.json) x 300 MAC",
         "units_per_launch": round(units[name]),
@@ -339,7 +349,7 @@ def extra_configs(device, stream, reps):
         "p50_ms_key_table": statistics.median(lat_tab),
         "sets_per_s_key_table": 64 / (statistics.median(lat_tab) * 1e-3),
         "aggregation_kernel": ("k_set_pk_wave (one 64-lane wave per set: strided mixed adds, LDS tree, [r] apk)"
-                               if os.environ.get("TBLS_AGG_COOP") == "0" else
+                               if os.environ.get("TBLS_COOP") == "0" else
                                "k_set_pk_agg_coop (32 coop rows per set: row sums of mixed adds, LDS tree, [r] apk by nibbles on "
                                "16 rows, -[r] g1 on row 17; critical path: the 60 doublings to 2^60 apk)"),
         "aggregation_ms": agg_ms,

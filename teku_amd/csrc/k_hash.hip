@@ -86,3 +86,27 @@ extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_MIN_WAVES)
   g2j h = hash_to_g2(c);
   g2_compress_jac(out + (size_t)i * 96, jac_mul_u256(h, sks + 4 * (size_t)i));
 }
+
+// The sets k_set_hash_w2 flagged (skip == 2: its branch-free cofactor chain met
+// an exceptional case or infinity) through the exact hash_to_G2 (tb_h2c.h
+// hash_to_g2 with g2_clear_cofactor).  One lane per set; unflagged sets return
+// at once.
+extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_MIN_WAVES)
+    k_set_hash_fix(const uint8_t* __restrict__ msgs, const uint32_t* __restrict__ msg_off, const uint8_t* __restrict__ dst,
+                   uint32_t dlen, uint32_t n, g2a* __restrict__ Q, uint8_t* __restrict__ skip) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || skip[i] != 2) return;
+  xmd_ctx c;
+  c.msg = msgs + msg_off[i];
+  c.mlen = msg_off[i + 1] - msg_off[i];
+  c.dst = dst;
+  c.dlen = dlen;
+  g2a a;
+  const bool ok = jac_to_aff(a, hash_to_g2(c));
+  if (!ok) {
+    a.x = fp2_zero();
+    a.y = fp2_zero();
+  }
+  Q[i] = a;
+  skip[i] = ok ? 0 : 1;
+}

@@ -52,16 +52,12 @@ __device__ TB_INLINE void hrow_sswu_body(uint32_t n, hrow_set* __restrict__ H, c
   const g2a q = crow::sswu(h.u[m & 1u], rb[g], K);
   if (d == 0) h.qm[m & 1u] = q;
 }
-// register bounds for 2 / 3 / 4 waves per SIMD (k_hrow_sswu: 228 / 168 + 148 B
-// scratch / 128 + 272 B); tb_lib.hip picks one (TBLS_HROW_WAVES)
-#define TB_HROW_SSWU(NAME, W)                                                                        \
-  extern "C" __global__ void __launch_bounds__(64, W) NAME(uint32_t n, hrow_set* __restrict__ H) { \
-    __shared__ crow::rowbuf rb[4];                                                                   \
-    hrow_sswu_body(n, H, rb);                                                                        \
-  }
-TB_HROW_SSWU(k_hrow_sswu, 2)
-TB_HROW_SSWU(k_hrow_sswu3, 3)
-TB_HROW_SSWU(k_hrow_sswu4, 4)
+// two waves per SIMD (228 registers; 3 and 4 waves, with spills, measured
+// neutral: 8.33 / 7.99 / 8.15 ms at 16,384 sets, round 3)
+extern "C" __global__ void __launch_bounds__(64, 2) k_hrow_sswu(uint32_t n, hrow_set* __restrict__ H) {
+  __shared__ crow::rowbuf rb[4];
+  hrow_sswu_body(n, H, rb);
+}
 
 extern "C" __global__ void __launch_bounds__(TB_BLOCK) k_hrow_iso(uint32_t n, hrow_set* __restrict__ H) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -122,15 +118,12 @@ __device__ TB_INLINE void hrow_cof_body(uint32_t n, const hrow_set* __restrict__
   }
 }
 
-// 2 / 3 waves per SIMD (256 + 236 B scratch / 168 + 656 B)
-#define TB_HROW_COF(NAME, W)                                                                                       \
-  extern "C" __global__ void __launch_bounds__(64, W)                                                              \
-      NAME(uint32_t n, const hrow_set* __restrict__ H, g2a* __restrict__ Q, uint8_t* __restrict__ skip, int force_fix) { \
-    __shared__ crow::rowbuf rb[4];                                                                                 \
-    hrow_cof_body(n, H, Q, skip, force_fix, rb);                                                                   \
-  }
-TB_HROW_COF(k_hrow_cof, 2)
-TB_HROW_COF(k_hrow_cof3, 3)
+// two waves per SIMD (256 registers + 236 B scratch)
+extern "C" __global__ void __launch_bounds__(64, 2)
+    k_hrow_cof(uint32_t n, const hrow_set* __restrict__ H, g2a* __restrict__ Q, uint8_t* __restrict__ skip, int force_fix) {
+  __shared__ crow::rowbuf rb[4];
+  hrow_cof_body(n, H, Q, skip, force_fix, rb);
+}
 
 extern "C" __global__ void __launch_bounds__(TB_BLOCK)
     k_hrow_fix(uint32_t n, const hrow_set* __restrict__ H, g2a* __restrict__ Q, uint8_t* __restrict__ skip) {

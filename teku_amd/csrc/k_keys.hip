@@ -1,6 +1,6 @@
 // Public keys: decompression + validity, per-set aggregation and [r] apk, the
 // pubkey-aggregation API, and sk -> pk.
-#include "tb_kdecl.h"
+#include "tb_kbody.h"
 #include "tb_comb.h"
 
 using namespace tb;
@@ -20,29 +20,6 @@ extern "C" __global__ void __launch_bounds__(TB_BLOCK, 2)
   pk_code[i] = (uint8_t)code;
 }
 
-// Two keys per thread: both square roots interleaved (g1_decompress2), then
-// each key's G1 check; same outputs as k_pk_decompress (TBLS_DEC2=0 selects it)
-extern "C" __global__ void __launch_bounds__(TB_BLOCK, 2)
-    k_pk_decompress2(const uint8_t* __restrict__ pks, uint32_t K, g1a* __restrict__ pk_aff, uint8_t* __restrict__ pk_code) {
-  const uint32_t i0 = 2 * (blockIdx.x * blockDim.x + threadIdx.x);
-  if (i0 >= K) return;
-  g1a a[2];
-  bool inf[2];
-  int code[2];
-  g1_decompress2(a, inf, code, pks + (size_t)i0 * 48, pks + (size_t)(i0 + 1 < K ? i0 + 1 : i0) * 48);
-  for (int j = 0; j < 2 && i0 + j < K; j++) {
-    int c = code[j];
-    if (c == TB_SUCCESS && inf[j]) c = TB_PK_IS_INFINITY;
-    if (c == TB_SUCCESS && !g1_in_group(jac_from_aff(a[j]))) c = TB_POINT_NOT_IN_GROUP;
-    if (c != TB_SUCCESS) {
-      a[j].x = fp_zero();
-      a[j].y = fp_zero();
-    }
-    pk_aff[i0 + j] = a[j];
-    pk_code[i0 + j] = (uint8_t)c;
-  }
-}
-
 // per set: aggregate keys (BlstPublicKey.aggregate semantics), P = [r] apk (affine);
 // key_idx (nullable): keys come from the device-resident table (pk_aff/pk_code =
 // the table, tab_n entries).  multi_wave: sets with more than one key are left
@@ -53,22 +30,9 @@ extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_MIN_WAVES)
              const uint64_t* __restrict__ rand, uint32_t n, g1a* __restrict__ P, uint8_t* __restrict__ set_code,
              uint32_t* __restrict__ n_bad, const uint32_t* __restrict__ key_idx, uint32_t tab_n, uint32_t multi_wave,
              g1a* __restrict__ P2, const g1a* __restrict__ comb) {
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const uint32_t b = pk_off[i], e = pk_off[i + 1];
-  // multi_wave & 3 == 1: multi-key sets go to k_set_pk_wave (P2 here), 2: to
-  // k_set_pk_agg_coop (P2 there too); bit 2: the batch's randomizers multiply
-  // H(m) on the G2 side (k_set_hash_coop), so P = apk
-  const uint32_t mw = multi_wave & 3u;
-  if (P2 && !(mw == 2 && e - b > 1)) P2[i] = neg_r_g1(comb, rand[i]);
-  if (mw && e - b > 1) return;
-  g1a out;
-  int code = stage_set_pk(pk_aff, pk_code, b, e, (multi_wave & 4u) ? 1ull : rand[i], out, key_idx, tab_n);
-  P[i] = out;
-  if (code != TB_SUCCESS) {
-    set_code[i] = (uint8_t)code;
-    atomicAdd(n_bad, 1u);
-  }
+  set_pk_body(i, pk_off, pk_aff, pk_code, rand, P, set_code, n_bad, key_idx, tab_n, multi_wave, P2, comb);
 }
 
 // Compaction of the multi-key sets (pk_off[i+1] - pk_off[i] > 1) into list[],

@@ -1,5 +1,6 @@
-// Split Miller loop kernels (k_miller_lines, k_miller_acc1/2): their own
-// translation unit so the device compiles run in parallel with k_miller.hip.
+// Split Miller loop kernels (k_miller_lines_lds, k_miller_acc1/2, the
+// segmented k_miller_accs): their own translation unit so the device compile
+// runs in parallel with the per-set stages'.
 #include "tb_kdecl.h"
 
 using namespace tb;
@@ -72,37 +73,6 @@ TB_HD TB_INLINE fp12 fp12_mul_by_line_i(const fp12& f, const fp2& A, const fp2& 
   return {c0, c1};
 }
 
-// f * l1 * l2 for two lines of one step (line = (A + B v) + (C v) w): the two
-// lines first (6 Fp2 products; the result L has w^0 coefficient X0 + X1 v +
-// X2 v^2 and w^1 coefficient Y1 v + Y2 v^2), then f * L in 17 (f0 L0 dense,
-// f1 L1 = v f1 (Y1 + Y2 v) sparse, Karatsuba middle term dense): 23 Fp2
-// products instead of 2 x 13.
-//   X0 = A1 A2 + xi C1 C2, X1 = A1 B2 + B1 A2, X2 = B1 B2,
-//   Y1 = A1 C2 + C1 A2,     Y2 = B1 C2 + C1 B2   (the cross terms by Karatsuba)
-TB_HD TB_INLINE fp12 fp12_mul_by_line_pair_i(const fp12& f, const line3& l1, const line3& l2) {
-  fp6 L0;
-  fp2 Y1, Y2;
-  {
-    const fp2 t0 = m2(l1.a, l2.a), t1 = m2(l1.b, l2.b), t2 = m2(l1.c, l2.c);
-    const fp2 s01 = m2(fp2_add(l1.a, l1.b), fp2_add(l2.a, l2.b));
-    const fp2 s02 = m2(fp2_add(l1.a, l1.c), fp2_add(l2.a, l2.c));
-    const fp2 s12 = m2(fp2_add(l1.b, l1.c), fp2_add(l2.b, l2.c));
-    L0 = {fp2_add(t0, fp2_mul_xi(t2)), fp2_sub(s01, fp2_add(t0, t1)), t1};
-    Y1 = fp2_sub(s02, fp2_add(t0, t2));
-    Y2 = fp2_sub(s12, fp2_add(t1, t2));
-  }
-  TB_FENCE();
-  const fp6 t1 = fp6_mul_v(fp6_mul_by_01_f(f.c1, Y1, Y2));  // f1 L1
-  const fp6 s = fp6_add(f.c0, f.c1);
-  const fp6 Ls = {L0.c0, fp2_add(L0.c1, Y1), fp2_add(L0.c2, Y2)};
-  TB_FENCE();
-  const fp6 u = fp6_mul_f(s, Ls);     // (f0 + f1)(L0 + L1)
-  const fp6 t0 = fp6_mul_f(f.c0, L0); // f0 L0
-  const fp6 c1 = fp6_sub(fp6_sub(u, t0), t1);
-  const fp6 c0 = fp6_add(t0, fp6_mul_v(t1));
-  return {c0, c1};
-}
-
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -126,12 +96,6 @@ TB_HD TB_INLINE fp12 fp12_mul_by_line_pair_i(const fp12& f, const line3& l1, con
 // step temporaries, and the Fp12 kernel holds f, one line and the product
 // temporaries.
 // ---------------------------------------------------------------------------
-#ifndef TB_SPREAD_EXTRA
-#define TB_SPREAD_EXTRA 0  // tb_lib.hip pair_plan: the bit-sum pairs run as wave Miller loops, no spread lines
-#endif
-#ifndef TB_ACC_COMPACT
-#define TB_ACC_COMPACT 1
-#endif
 #define TB_LINE_STEPS 68  // 63 doubling + 5 addition steps of |x| = 0xd201000000010000
 #define TB_LINE_G 18      // 16-byte groups per line (3 Fp2 = 72 words)
 
@@ -219,27 +183,10 @@ __device__ TB_INLINE line3 dbl_step_f(g2p& T, const g1a& P) {
 }
 }  // namespace
 
-#ifndef TB_LINES_WAVES
-#define TB_LINES_WAVES TB_MIN_WAVES  // A/B: 2 caps the line kernel at 256 registers
-#endif
-extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_LINES_WAVES)
-    k_miller_lines(const g1a* __restrict__ P, const g2a* __restrict__ Q, const uint8_t* __restrict__ skip,
-                   const uint8_t* __restrict__ code_a, const uint8_t* __restrict__ code_b, uint32_t n, uint4* __restrict__ lines) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  if (skip[i] != 0 || code_a[i] != 0 || code_b[i] != 0) return;  // k_miller_acc skips the pair too
-  const g1a p = P[i];
-  g2p T = {Q[i].x, Q[i].y, fp2_one()};
-  int s = 0;
-  TB_NOUNROLL for (int b = 62; b >= 0; --b) {
-    line_store(lines, n, i, s++, dbl_step_f(T, p));
-    if ((X_ABS >> b) & 1) line_store(lines, n, i, s++, add_step_f(T, Q[i], p));
-  }
-}
-
-// the same with the pair's G1 point and the twist point T in LDS (A/B
-// against scratch spills, TBLS_LINES_LDS=1)
-extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_LINES_WAVES)
+// One pair per thread, with the pair's G1 point and the twist point T in LDS
+// (round 3: scratch 612 -> 200 B per lane, fetch 2.0 -> 0.24 GB per 131k
+// launch, Miller stage 15.92 -> 15.64 ms against registers)
+extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_MIN_WAVES)
     k_miller_lines_lds(const g1a* __restrict__ P, const g2a* __restrict__ Q, const uint8_t* __restrict__ skip,
                        const uint8_t* __restrict__ code_a, const uint8_t* __restrict__ code_b, uint32_t n, uint4* __restrict__ lines) {
   __shared__ g1a psh[TB_BLOCK];
@@ -258,47 +205,26 @@ extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_LINES_WAVES)
   }
 }
 
-// Thread t accumulates the main pairs PER t .. PER t + PER - 1 (< n; their
-// lines in `lines`, stride n) and, at each step s, at most one line of the
-// n_extra pairs in `xlines` (stride n_extra; the signature side's bit-sum
-// pairs, whose lines k_miller_lines writes on the signature stream): extra
-// pair e goes to thread (s * n_extra + e) mod T at step s.  The product of all threads' f is the
-// same, since every thread applies the same squaring schedule after step s;
-// spreading the extra pairs one line at a time keeps every thread's work
-// within one line product (+0.5 %) instead of adding whole Miller loops to a
-// few threads (a tail as long as the kernel).
-template <int PER, bool EXTRA>
+// Thread t accumulates the pairs PER t .. PER t + PER - 1 (< n; their lines
+// in `lines`, stride n): per step one f^2 (paid once for the PER pairs) and
+// PER sparse line products.  One squaring site and one line-product site (the
+// PER pairs and the addition steps loop over them): a quarter of the unrolled
+// code, which fits the instruction cache better and keeps fewer values live.
+template <int PER>
 __device__ TB_INLINE void miller_acc_body(const uint4* __restrict__ lines, const uint8_t* __restrict__ skip,
                                           const uint8_t* __restrict__ code_a, const uint8_t* __restrict__ code_b, uint32_t n,
-                                          const uint4* __restrict__ xlines, const uint8_t* __restrict__ xskip, uint32_t n_extra,
                                           fp12* __restrict__ f_out) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t T = (n + PER - 1) / PER;
   const uint32_t i0 = PER * t;
   if (t >= T) return;
-  bool use[PER];
+  uint32_t usem = 0;
   TB_UNROLL for (int j = 0; j < PER; j++) {
     const uint32_t i = i0 + j;
-    use[j] = i < n && skip[i] == 0 && code_a[i] == 0 && code_b[i] == 0;
+    if (i < n && skip[i] == 0 && code_a[i] == 0 && code_b[i] == 0) usem |= 1u << j;
   }
   fp12 f = fp12_one();
   int s = 0;
-  // always_inline: an outlined call here (one per step) made the caller save
-  // and restore its live accumulator registers through scratch every step
-  auto extra = [&](int step) __attribute__((always_inline)) {
-    if (!EXTRA || !n_extra) return;
-    const uint32_t e = (t + T - (uint32_t)(step * n_extra) % T) % T;
-    if (e < n_extra && xskip[e] == 0) {
-      const line3 l = line_load(xlines, n_extra, e, step);
-      f = fp12_mul_by_line_i(f, l.a, l.b, l.c);
-    }
-  };
-#if TB_ACC_COMPACT
-  // one squaring site and one line-product site (the PER pairs and the
-  // addition steps loop over them): a quarter of the unrolled code, which
-  // fits the instruction cache better and keeps fewer values live
-  uint32_t usem = 0;
-  TB_UNROLL for (int j = 0; j < PER; j++) usem |= use[j] ? (1u << j) : 0u;
   TB_NOUNROLL for (int b = 62; b >= 0; --b) {
     const int reps = ((X_ABS >> b) & 1) ? 2 : 1;
     TB_NOUNROLL for (int r = 0; r < reps; r++) {
@@ -309,48 +235,22 @@ __device__ TB_INLINE void miller_acc_body(const uint4* __restrict__ lines, const
           f = fp12_mul_by_line_i(f, l.a, l.b, l.c);
         }
       }
-      extra(s);
       s++;
     }
   }
-#else
-  TB_NOUNROLL for (int b = 62; b >= 0; --b) {
-    if (b != 62) f = fp12_sqr_i(f);
-    TB_UNROLL for (int j = 0; j < PER; j++) {
-      if (use[j]) {
-        const line3 l = line_load(lines, n, i0 + j, s);
-        f = fp12_mul_by_line_i(f, l.a, l.b, l.c);
-      }
-    }
-    extra(s);
-    s++;
-    if ((X_ABS >> b) & 1) {
-      TB_UNROLL for (int j = 0; j < PER; j++) {
-        if (use[j]) {
-          const line3 l = line_load(lines, n, i0 + j, s);
-          f = fp12_mul_by_line_i(f, l.a, l.b, l.c);
-        }
-      }
-      extra(s);
-      s++;
-    }
-  }
-#endif
   f_out[t] = fp12_conj(f);
 }
 
 extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_MIN_WAVES)
     k_miller_acc1(const uint4* __restrict__ lines, const uint8_t* __restrict__ skip, const uint8_t* __restrict__ code_a,
-                  const uint8_t* __restrict__ code_b, uint32_t n, const uint4* __restrict__ xlines, const uint8_t* __restrict__ xskip,
-                  uint32_t n_extra, fp12* __restrict__ f) {
-  miller_acc_body<1, TB_SPREAD_EXTRA != 0>(lines, skip, code_a, code_b, n, xlines, xskip, n_extra, f);
+                  const uint8_t* __restrict__ code_b, uint32_t n, fp12* __restrict__ f) {
+  miller_acc_body<1>(lines, skip, code_a, code_b, n, f);
 }
 
 extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_MIN_WAVES)
     k_miller_acc2(const uint4* __restrict__ lines, const uint8_t* __restrict__ skip, const uint8_t* __restrict__ code_a,
-                  const uint8_t* __restrict__ code_b, uint32_t n, const uint4* __restrict__ xlines, const uint8_t* __restrict__ xskip,
-                  uint32_t n_extra, fp12* __restrict__ f) {
-  miller_acc_body<2, TB_SPREAD_EXTRA != 0>(lines, skip, code_a, code_b, n, xlines, xskip, n_extra, f);
+                  const uint8_t* __restrict__ code_b, uint32_t n, fp12* __restrict__ f) {
+  miller_acc_body<2>(lines, skip, code_a, code_b, n, f);
 }
 
 // ---------------------------------------------------------------------------
@@ -394,11 +294,9 @@ __device__ TB_INLINE bool step_is_dbl(int s) { return ((s < 64 ? (DBL_STEPS.lo >
 __device__ TB_INLINE fp12 line_fp12(const line3& l) { return {{l.a, l.b, fp2_zero()}, {fp2_zero(), l.c, fp2_zero()}}; }
 }  // namespace
 
-template <bool PAIRS, bool LDSF = false>
 __device__ TB_INLINE void miller_accs_body(const uint4* __restrict__ lines, const uint8_t* __restrict__ skip,
                                            const uint8_t* __restrict__ code_a, const uint8_t* __restrict__ code_b, uint32_t n, uint32_t per,
-                                           uint32_t nseg, uint32_t g_pad, fp12* __restrict__ f_out, uint32_t seg_stride,
-                                           fp12* fsh = nullptr) {
+                                           uint32_t nseg, uint32_t g_pad, fp12* __restrict__ f_out, uint32_t seg_stride) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t j = t / g_pad, g = t % g_pad;
   const uint32_t G = (n + per - 1) / per;
@@ -414,11 +312,9 @@ __device__ TB_INLINE void miller_accs_body(const uint4* __restrict__ lines, cons
     const uint32_t i = g + k * G;
     if (i < n && skip[i] == 0 && code_a[i] == 0 && code_b[i] == 0) usem |= 1u << k;
   }
-  fp12 freg;
-  fp12& f = LDSF ? fsh[threadIdx.x] : freg;  // LDSF: the accumulator lives in LDS, not in 144 registers
-  f = fp12_one();
+  fp12 f = fp12_one();
   bool fresh = true;  // f == 1
-  // the used pairs' offsets, packed 4 bits each (line products in pairs, TB_ACC_PAIRS)
+  // the used pairs' offsets, packed 4 bits each
   uint32_t uidx = 0, nu = 0;
   for (uint32_t k = 0; k < per; k++)
     if ((usem >> k) & 1u) uidx |= k << (4 * nu++);
@@ -429,13 +325,6 @@ __device__ TB_INLINE void miller_accs_body(const uint4* __restrict__ lines, cons
       f = line_fp12(line_load(lines, n, i0 + (uidx & 15u) * G, s));
       fresh = false;
       k = 1;
-    }
-    if (PAIRS) {
-      TB_NOUNROLL for (; k + 1 < nu; k += 2) {
-        const line3 l1 = line_load(lines, n, i0 + ((uidx >> (4 * k)) & 15u) * G, s);
-        const line3 l2 = line_load(lines, n, i0 + ((uidx >> (4 * k + 4)) & 15u) * G, s);
-        f = fp12_mul_by_line_pair_i(f, l1, l2);
-      }
     }
     TB_NOUNROLL for (; k < nu; k++) {
       const line3 l = line_load(lines, n, i0 + ((uidx >> (4 * k)) & 15u) * G, s);
@@ -449,25 +338,5 @@ extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_MIN_WAVES)
     k_miller_accs(const uint4* __restrict__ lines, const uint8_t* __restrict__ skip, const uint8_t* __restrict__ code_a,
                   const uint8_t* __restrict__ code_b, uint32_t n, uint32_t per, uint32_t nseg, uint32_t g_pad, fp12* __restrict__ f_out,
                   uint32_t seg_stride) {
-  miller_accs_body<false>(lines, skip, code_a, code_b, n, per, nseg, g_pad, f_out, seg_stride);
-}
-
-// the same with the step's lines multiplied two at a time (fp12_mul_by_line_pair_i)
-extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_MIN_WAVES)
-    k_miller_accs_pairs(const uint4* __restrict__ lines, const uint8_t* __restrict__ skip, const uint8_t* __restrict__ code_a,
-                        const uint8_t* __restrict__ code_b, uint32_t n, uint32_t per, uint32_t nseg, uint32_t g_pad, fp12* __restrict__ f_out,
-                        uint32_t seg_stride) {
-  miller_accs_body<true>(lines, skip, code_a, code_b, n, per, nseg, g_pad, f_out, seg_stride);
-}
-
-// the accumulator f in LDS (576 B per thread, 36.9 KB per 64-thread block;
-// four blocks per CU fit the 160 KB): the register file then holds only the
-// products' operands and temporaries (A/B against scratch spills,
-// TBLS_ACC_LDS=1)
-extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_MIN_WAVES)
-    k_miller_accs_lds(const uint4* __restrict__ lines, const uint8_t* __restrict__ skip, const uint8_t* __restrict__ code_a,
-                      const uint8_t* __restrict__ code_b, uint32_t n, uint32_t per, uint32_t nseg, uint32_t g_pad, fp12* __restrict__ f_out,
-                      uint32_t seg_stride) {
-  __shared__ fp12 fsh[TB_BLOCK];
-  miller_accs_body<false, true>(lines, skip, code_a, code_b, n, per, nseg, g_pad, f_out, seg_stride, fsh);
+  miller_accs_body(lines, skip, code_a, code_b, n, per, nseg, g_pad, f_out, seg_stride);
 }

@@ -1,6 +1,6 @@
 // Signatures: decompression + G2 check + [r] sig per set, the two-level G2 sum,
 // the signature-aggregation API and signature validation.
-#include "tb_kdecl.h"
+#include "tb_kbody.h"
 
 using namespace tb;
 
@@ -138,55 +138,15 @@ extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_MIN_WAVES) k_g1_comb_i
   comb[t] = out;
 }
 
-// Two sets per thread: both Fp2 square roots interleaved (g2_decompress2),
-// then each signature's G2 check; same outputs as k_sig_check (TBLS_DEC2=0
-// selects it)
-extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_MIN_WAVES)
-    k_sig_check2(const uint8_t* __restrict__ sigs, uint32_t n, g2a* __restrict__ sig_aff, uint8_t* __restrict__ sig_use,
-                 uint8_t* __restrict__ sig_code, uint32_t* __restrict__ n_bad, uint32_t skip_mode) {
-  const uint32_t i0 = 2 * (blockIdx.x * blockDim.x + threadIdx.x);
-  if (i0 >= n) return;
-  g2a a[2];
-  bool inf[2];
-  int code[2];
-  g2_decompress2(a, inf, code, sigs + (size_t)i0 * 96, sigs + (size_t)(i0 + 1 < n ? i0 + 1 : i0) * 96);
-  for (int j = 0; j < 2 && i0 + j < n; j++) {
-    const uint32_t i = i0 + j;
-    int c = code[j];
-    if (c == TB_SUCCESS && !inf[j] && !g2_in_group(jac_from_aff(a[j]))) c = TB_POINT_NOT_IN_GROUP;
-    const bool use = c == TB_SUCCESS && !inf[j];
-    if (!use) {
-      a[j].x = fp2_zero();
-      a[j].y = fp2_zero();
-    }
-    sig_aff[i] = a[j];
-    sig_use[i] = (use != (skip_mode != 0)) ? 1 : 0;
-    sig_code[i] = (uint8_t)c;
-    if (c != TB_SUCCESS) atomicAdd(n_bad, 1u);
-  }
-}
-
 // per set: decode + G2 check.  skip_mode = 0: sig_aff + sig_use (1 = valid and
 // finite: the bucket input); skip_mode = 1: sig_aff = Q of the set's signature
 // pair and sig_use = its skip flag (1 = no pair: infinite or invalid).
 extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_MIN_WAVES)
     k_sig_check(const uint8_t* __restrict__ sigs, uint32_t n, g2a* __restrict__ sig_aff, uint8_t* __restrict__ sig_use,
                 uint8_t* __restrict__ sig_code, uint32_t* __restrict__ n_bad, uint32_t skip_mode) {
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  g2a a;
-  bool inf;
-  int code = g2_decompress(a, inf, sigs + (size_t)i * 96);
-  if (code == TB_SUCCESS && !inf && !g2_in_group(jac_from_aff(a))) code = TB_POINT_NOT_IN_GROUP;
-  const bool use = code == TB_SUCCESS && !inf;
-  if (!use) {
-    a.x = fp2_zero();
-    a.y = fp2_zero();
-  }
-  sig_aff[i] = a;
-  sig_use[i] = (use != (skip_mode != 0)) ? 1 : 0;
-  sig_code[i] = (uint8_t)code;
-  if (code != TB_SUCCESS) atomicAdd(n_bad, 1u);
+  sig_check_body<false>(i, sigs, sig_aff, sig_use, sig_code, n_bad, skip_mode);
 }
 
 extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_MIN_WAVES)

@@ -18,7 +18,9 @@
 #include <hip/hip_runtime.h>
 #define TB_HD __host__ __device__
 #define TB_INLINE __forceinline__
+#ifndef TB_NOINLINE  // a TU may define it first (k_hash_w2.hip: everything inlined)
 #define TB_NOINLINE inline __attribute__((noinline))  // inline: one definition across TUs
+#endif
 #define TB_CONST static constexpr
 #else
 #define TB_HD

@@ -424,10 +424,15 @@ TB_HD TB_INLINE jac<F> jac_add_nx(const jac<F>& p, const jac<F>& q) {
 }
 
 // [|x|]P branch-free: the doubling runs of XRUN_DBL as one loop over the runs
-// (one doubling body and one addition body in the code: a ~180 KB leaf instead
-// of jac_mul_xabs's ~360 KB of unrolled runs), the additions jac_add_nx.
+// (one doubling body and one addition body in the code), the additions
+// jac_add_nx.  Inlined into its callers, which are kernels: as an outlined
+// function its ~270 KB loop exceeds the short-branch range (+-2^16 words), and
+// the compiler's long-branch expansion in a function uses s[30:31], the
+// return address, without saving it -- the return then loops forever
+// (observed with ROCm 7.2's clang; tests/test_long_branches.py checks every
+// built code object for it).
 template <typename F>
-TB_HD TB_NOINLINE jac<F> jac_mul_xabs_nx(const jac<F>& P) {
+TB_HD TB_INLINE jac<F> jac_mul_xabs_nx(const jac<F>& P) {
   jac<F> r = P;
   TB_NOUNROLL for (int k = 0; k < 6; k++) {
     const int nd = k == 0 ? 1 : k == 1 ? 2 : k == 2 ? 3 : k == 3 ? 9 : k == 4 ? 32 : 16;  // XRUN_DBL[k]
@@ -459,6 +464,16 @@ TB_HD TB_INLINE g1j g1_mul_x(const g1j& p) { return jac_neg(jac_mul_u64(p, X_ABS
 TB_HD TB_NOINLINE bool g2_in_group(const g2j& q) {
   if (jac_is_inf(q)) return true;
   return jac_eq(g2_psi(q), g2_mul_x(q));
+}
+
+// The same check with the branch-free [|x|] (jac_mul_xabs_nx).  For Q in G2 no
+// multiple [k]Q, 2 <= k < 2^64 < r, is +-Q or infinity, so the chain meets no
+// exceptional case and equals the exact one; a point outside G2 whose chain
+// meets one ends at Z = 0, which jac_eq finds unequal to the finite psi(Q):
+// rejected, as the exact check rejects it.  Same verdict for every finite Q.
+TB_HD TB_INLINE bool g2_in_group_nx(const g2j& q) {
+  if (jac_is_inf(q)) return true;
+  return jac_eq(g2_psi(q), jac_neg(jac_mul_xabs_nx(q)));
 }
 
 // Scott: P in G1 <=> phi(P) == [-x^2]P, phi(X,Y,Z) = (beta X, Y, Z)

@@ -14,12 +14,8 @@ struct hrow_set {
 extern "C" __global__ void k_hrow_field(const uint8_t* __restrict__ msgs, const uint32_t* __restrict__ msg_off,
                                         const uint8_t* __restrict__ dst, uint32_t dlen, uint32_t n, tb::hrow_set* __restrict__ H);
 extern "C" __global__ void k_hrow_sswu(uint32_t n, tb::hrow_set* __restrict__ H);
-extern "C" __global__ void k_hrow_sswu3(uint32_t n, tb::hrow_set* __restrict__ H);
-extern "C" __global__ void k_hrow_sswu4(uint32_t n, tb::hrow_set* __restrict__ H);
 extern "C" __global__ void k_hrow_iso(uint32_t n, tb::hrow_set* __restrict__ H);
 extern "C" __global__ void k_hrow_cof(uint32_t n, const tb::hrow_set* __restrict__ H, tb::g2a* __restrict__ Q,
                                       uint8_t* __restrict__ skip, int force_fix);
-extern "C" __global__ void k_hrow_cof3(uint32_t n, const tb::hrow_set* __restrict__ H, tb::g2a* __restrict__ Q,
-                                       uint8_t* __restrict__ skip, int force_fix);
 extern "C" __global__ void k_hrow_fix(uint32_t n, const tb::hrow_set* __restrict__ H, tb::g2a* __restrict__ Q,
                                       uint8_t* __restrict__ skip);

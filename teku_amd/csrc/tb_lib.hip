@@ -209,9 +209,6 @@ void place_one(placed& pl) {
 // bucket sum by randomizer byte with 2040 bucket pairs (k_msm_*, k_sigs.hip);
 // below it, one signature pair (-[r_i] g1, sig_i) per set.
 #define TB_MSM_MIN 32768u
-#ifndef TB_ORDER_DEFAULT
-#define TB_ORDER_DEFAULT 1  // measured 52.5 vs 53.3 ms per 131k step (2.71M vs 2.63M sigs/s with the key table)
-#endif
 #define TB_HASH_WAVE_MAX 512u  // k_set_hash_wave (one workgroup per set) up to this many sets: at 1024 its waves fill every SIMD and the key / signature stages can no longer run beside it (measured 9.8 vs 8.8 ms partial)
 #define TB_MSM_BUCKETS 2048u  // 8 windows x 256 digits (digit 0 unused)
 #define TB_MSM_NSUM 2040u     // 8 x 255 bucket sums (k_msm_bucket_sum)
@@ -223,11 +220,6 @@ void place_one(placed& pl) {
 // accumulator wave per SIMD: 1024 waves x 64 lanes x 2 pairs).
 #define TB_LINE_CHUNK 262144u
 #define TB_MILLER_PER2_MIN 131072u
-#define TB_MILLER1_MAX 4096u
-static bool miller_split() {
-  static const bool v = !(getenv("TBLS_MILLER_SPLIT") && getenv("TBLS_MILLER_SPLIT")[0] == '0');
-  return v;
-}
 // up to this many pairs, one pair per 64-lane workgroup (k_miller_wave);
 // TBLS_MILLER_WAVE_MAX overrides (tuning)
 static uint32_t miller_wave_max() {
@@ -240,25 +232,35 @@ static uint32_t miller_wave_max() {
 // pairs of the Miller kernels), else TB_MSM_XPAIRS bit-sum pairs.  With the
 // split Miller loop the bit-sum pairs run one 64-lane wave each (k_miller_wave,
 // n_xwave of them) on the bucket-sum stream, into the Miller values after the
-// accumulators' (TB_SPREAD_EXTRA=1: their lines spread over the accumulators,
-// k_lines.hip, the round-1/2 form).
-#ifndef TB_SPREAD_EXTRA
-#define TB_SPREAD_EXTRA 0
-#endif
+// accumulators'.
 // Segmented accumulator (k_lines.hip k_miller_accs): `per` pairs per thread,
 // the loop's 68 steps in `nseg` segments.  Chosen to minimize the modelled
 // accumulator time: per-thread latency (68 / nseg) (12 + 13 per) Fp2
 // products (one f^2, per sparse line products per step) times the wave rounds
 // (TB_ACC_FULL threads = one 64-lane wave per SIMD fill the GPU once); ties go
-// to fewer segments (smaller product tree).  TBLS_ACC_PER / TBLS_ACC_SEG
-// override (A/B); TBLS_ACC_SEG=0 selects the unsegmented k_miller_acc1/2.
+// to fewer segments (smaller product tree).  TBLS_ACC_PLAN="per,nseg"
+// overrides it (tuning; per in {1, 2, 4, 8}, nseg in 1..4; "0" selects the
+// unsegmented k_miller_acc1/2).  Every per divides TB_LINE_CHUNK, so the chunks
+// of a large batch fill contiguous group ranges (lo / per).
 #define TB_ACC_FULL 65536u
-static int acc_env(const char* name) {
-  const char* v = getenv(name);
-  return v ? atoi(v) : -1;
+// TBLS_ACC_PLAN: -1 / -1 (unset), 0 / 0 ("0": unsegmented), or per / nseg
+static void acc_env(int& e_per, int& e_seg) {
+  e_per = e_seg = -1;
+  const char* v = getenv("TBLS_ACC_PLAN");
+  if (!v) return;
+  if (v[0] == '0' && v[1] == 0) {
+    e_per = e_seg = 0;
+    return;
+  }
+  int p = 0, g = 0;
+  if (sscanf(v, "%d,%d", &p, &g) == 2 && (p == 1 || p == 2 || p == 4 || p == 8) && g >= 1 && g <= 4) {
+    e_per = p;
+    e_seg = g;
+  }
 }
 static void acc_plan(uint32_t n_main, uint32_t& per, uint32_t& nseg) {
-  static const int e_per = acc_env("TBLS_ACC_PER"), e_seg = acc_env("TBLS_ACC_SEG");
+  static int e_per = -2, e_seg = -2;
+  if (e_per == -2) acc_env(e_per, e_seg);
   if (e_seg == 0) {  // the unsegmented kernels
     per = n_main >= TB_MILLER_PER2_MIN ? 2u : 1u;
     nseg = 1;
@@ -267,8 +269,8 @@ static void acc_plan(uint32_t n_main, uint32_t& per, uint32_t& nseg) {
   double best = 0;
   per = 1;
   nseg = 1;
-  for (uint32_t p = 1; p <= 8; p++) {  // 1, 2, 4, 8 (an override may force any count up to 8)
-    if (e_per > 0 ? (int)p != e_per : (p & (p - 1)) != 0) continue;
+  for (uint32_t p = 1; p <= 8; p *= 2) {
+    if (e_per > 0 && (int)p != e_per) continue;
     for (uint32_t sg = 1; sg <= 4; sg++) {
       if (e_seg > 0 ? (int)sg != e_seg : sg == 3) continue;
       const double threads = (double)sg * ((n_main + p - 1) / p);
@@ -300,68 +302,23 @@ static uint32_t seg_dpack(uint32_t nseg) {
   return pack;
 }
 
-// the segmented accumulator kernel: TBLS_ACC_PAIRS=1 two lines per product
-// (fp12_mul_by_line_pair_i: 23 vs 26 Fp2 products, more registers)
-typedef void (*accs_fn)(const uint4*, const uint8_t*, const uint8_t*, const uint8_t*, uint32_t, uint32_t, uint32_t, uint32_t, fp12*,
-                        uint32_t);
-static accs_fn accs_kernel() {
-  static const bool pairs = getenv("TBLS_ACC_PAIRS") && getenv("TBLS_ACC_PAIRS")[0] == '1';
-  static const bool lds = getenv("TBLS_ACC_LDS") && getenv("TBLS_ACC_LDS")[0] == '1';
-  return pairs ? k_miller_accs_pairs : (lds ? k_miller_accs_lds : k_miller_accs);
-}
-
-// the line kernel: P and T in LDS (k_miller_lines_lds) unless TBLS_LINES_LDS=0
-typedef void (*lines_fn)(const g1a*, const g2a*, const uint8_t*, const uint8_t*, const uint8_t*, uint32_t, uint4*);
-static lines_fn lines_kernel() {
-  // default: P and T in LDS (round 3: fetch 2.0 -> 0.24 GB per 131k launch,
-  // Miller stage 15.92 -> 15.64 ms); TBLS_LINES_LDS=0 keeps them in registers
-  static const bool lds = !(getenv("TBLS_LINES_LDS") && getenv("TBLS_LINES_LDS")[0] == '0');
-  return lds ? k_miller_lines_lds : k_miller_lines;
-}
-
 struct pair_plan {
-  uint32_t n, n_extra, n_pairs, n_main, n_spread, n_xwave, per, nseg;
+  uint32_t n, n_extra, n_pairs, n_main, n_xwave, per, nseg;
   bool msm, wave, split;
   explicit pair_plan(uint32_t n_) : n(n_) {
     msm = n >= TB_MSM_MIN;
     n_extra = msm ? TB_MSM_XPAIRS : n;
     n_pairs = n + n_extra;
     wave = n_pairs <= miller_wave_max();
-    split = !wave && miller_split();
-    n_spread = split && msm && TB_SPREAD_EXTRA ? n_extra : 0u;  // pairs spread line by line
-    n_xwave = split && msm && !TB_SPREAD_EXTRA ? n_extra : 0u;  // pairs on their own waves
-    n_main = n_pairs - n_spread - n_xwave;                       // pairs owned by accumulator threads
+    split = !wave;
+    n_xwave = split && msm ? n_extra : 0u;  // bit-sum pairs on their own waves
+    n_main = n_pairs - n_xwave;             // pairs owned by accumulator threads
     nseg = 1;
-    if (wave)
-      per = 1;
-    else if (split)
-      acc_plan(std::min(n_main, TB_LINE_CHUNK), per, nseg);  // the chunks launch one after another: plan one chunk's fill
-    else
-      per = n_pairs <= TB_MILLER1_MAX ? 1u : 2u;
-    if (n_spread) nseg = 1;  // the spread extra lines need whole loops per thread
-    // TBLS_HALVES=1 (A/B; per-set signature pairs, below TB_MSM_MIN sets): the
-    // n signature pairs' Miller loops as a launch of their own, queued on the
-    // signature stream once the signatures and -[r] g1 exist -- beside
-    // hash_to_G2, which their pairs do not need -- and the n set pairs after
-    // the hash.  Measured and rejected (round 3, 16,384 sets): partial 12.88
-    // vs 12.91 ms (one plan for both halves), 13.47 ms (each half planned for
-    // n pairs): the set pairs' line chain after the hash is the critical path
-    // either way, and the side launch competes with the hash.
-    static const bool halves_env = getenv("TBLS_HALVES") && getenv("TBLS_HALVES")[0] == '1';
-    halves = halves_env && split && !msm && seg() && n_main == 2 * n;
-    if (halves) {  // each half is a launch of n pairs: plan its fill
-      uint32_t p2 = per, s2 = nseg;
-      acc_plan(n, p2, s2);
-      if (p2 > 2 || s2 > 1) {
-        per = p2;
-        nseg = s2;
-      }
-    }
+    per = 1;
+    if (split) acc_plan(std::min(n_main, TB_LINE_CHUNK), per, nseg);  // the chunks launch one after another: plan one chunk's fill
   }
-  bool halves = false;
   bool seg() const { return split && (nseg > 1 || per > 2); }  // k_miller_accs
-  uint32_t half_groups() const { return (n + per - 1) / per; }
-  uint32_t n_groups() const { return halves ? 2 * half_groups() : (n_main + per - 1) / per; }
+  uint32_t n_groups() const { return (n_main + per - 1) / per; }
   uint32_t n_f_main() const { return nseg * n_groups(); }
   uint32_t n_f() const { return n_f_main() + n_xwave; }  // Miller values: accumulators (segment-major), then the wave pairs'
   uint32_t line_pairs() const { return split ? std::min(n_main, TB_LINE_CHUNK) : 0u; }
@@ -387,7 +344,7 @@ static bool hash_pair(uint32_t n) {
 
 struct ws_layout {
   size_t pk_aff, pk_code, P, Q, skip, set_code, sig_code, f, fpart, fpart2, segv, n_bad, result;
-  size_t sig_aff, sig_use, msm_cnt, msm_off, msm_cur, msm_idx, msm_part, msm_sum, mlist, mcnt, lines, xlines, hrow, total;
+  size_t sig_aff, sig_use, msm_cnt, msm_off, msm_cur, msm_idx, msm_part, msm_sum, mlist, mcnt, lines, hrow, total;
   uint32_t nb_f;
   ws_layout() : total(0) {}
   ws_layout(const pair_plan& pp, uint32_t K) {
@@ -416,7 +373,6 @@ struct ws_layout {
     mcnt = o;     o = align_up(o + 4);
     hrow = o;     o = align_up(o + (hash_row(n) ? (size_t)n * sizeof(hrow_set) : 0));
     lines = o;    o = align_up(o + (size_t)pp.line_pairs() * TB_LINE_BYTES_PER_PAIR);
-    xlines = o;   o = align_up(o + (size_t)pp.n_spread * TB_LINE_BYTES_PER_PAIR);
     f = o;        o = align_up(o + (size_t)(nf ? nf : 1) * sizeof(fp12));
     fpart = o;    o = align_up(o + (size_t)nb_f * sizeof(fp12));
     fpart2 = o;   o = align_up(o + (size_t)((nb_f + TB_PROD_CHUNK - 1) / TB_PROD_CHUNK + pp.nseg) * sizeof(fp12));
@@ -440,8 +396,24 @@ struct ws_layout {
 // on aux[2] (high priority); all three join the caller's stream before the
 // Miller loops.  At large n
 // every stage fills the GPU; at small n (config 1) the three per-set chains
-// run side by side.  TBLS_SERIAL=1 (or `serial`) runs everything on the
+// run side by side.  `serial` (the stage-profile API) runs everything on the
 // caller's stream, for exclusive per-stage timings.
+
+// The large-batch one-lane kernels (hash, signature check, [r] apk) as their
+// two-waves-per-SIMD twins (k_w2_*.hip); TBLS_W2=0 selects the one-wave
+// kernels (A/B).
+static bool w2() {
+  static const bool v = !(getenv("TBLS_W2") && getenv("TBLS_W2")[0] == '0');
+  return v;
+}
+// Small batches (<= TB_HASH_WAVE_MAX sets) run the key, signature and hash
+// stages, and multi-key aggregation, on the lane-cooperative kernels
+// (k_kcoop.hip, k_hwave.hip k_set_hash_coop); TBLS_COOP=0 selects the
+// one-thread / one-wave kernels they replaced (A/B, fall-back).
+static bool coop() {
+  static const bool v = !(getenv("TBLS_COOP") && getenv("TBLS_COOP")[0] == '0');
+  return v;
+}
 
 // Per-set aggregate key and P_i = [r_i] apk_i on stream s.  Single-key sets:
 // one thread per set (k_set_pk).  When some set has several keys (n_entries >
@@ -450,22 +422,21 @@ struct ws_layout {
 // P2 (nullable): signature-pair points -[r_i] g1 (comb: the device's table).
 void launch_set_pk(hipStream_t s, uint32_t n, uint32_t n_entries, const uint32_t* pk_off, const g1a* aff, const uint8_t* code,
                    const uint64_t* rand, g1a* P, uint8_t* set_code, uint32_t* n_bad, const uint32_t* key_idx, uint32_t tab_n,
-                   uint32_t* mlist, uint32_t* mcnt, g1a* P2, const g1a* comb, bool r_on_g2 = false) {
+                   uint32_t* mlist, uint32_t* mcnt, g1a* P2, const g1a* comb) {
   if (!n) return;
   const dim3 blk(TB_BLOCK), g((n + TB_BLOCK - 1) / TB_BLOCK);
-  // lane-cooperative aggregation (16 rows per set, k_kcoop.hip, with the
-  // set's -[r] g1); TBLS_AGG_COOP=0 selects the one-wave-per-set kernel (A/B)
-  static const bool agg_coop = !(getenv("TBLS_AGG_COOP") && getenv("TBLS_AGG_COOP")[0] == '0');
-  const uint32_t multi = n_entries > n ? (agg_coop ? 2u : 1u) : 0u;
-  // r_on_g2: the randomizers multiply H(m) (k_set_hash_coop), P = apk here
-  hipLaunchKernelGGL(k_set_pk, g, blk, 0, s, pk_off, aff, code, rand, n, P, set_code, n_bad, key_idx, tab_n, multi | (r_on_g2 ? 4u : 0u), P2,
+  // multi-key sets: the lane-cooperative aggregation (32 rows per set,
+  // k_kcoop.hip, with the set's -[r] g1), or the one-wave-per-set kernel with
+  // TBLS_COOP=0
+  const uint32_t multi = n_entries > n ? (coop() ? 2u : 1u) : 0u;
+  hipLaunchKernelGGL(w2() ? k_set_pk_w2 : k_set_pk, g, blk, 0, s, pk_off, aff, code, rand, n, P, set_code, n_bad, key_idx, tab_n, multi, P2,
                      comb);
   if (!multi) return;
   (void)hipMemsetAsync(mcnt, 0, 4, s);
   hipLaunchKernelGGL(k_multi_list, g, blk, 0, s, pk_off, n, mlist, mcnt);
-  if (agg_coop)
+  if (multi == 2)
     hipLaunchKernelGGL(k_set_pk_agg_coop, dim3(std::min<uint32_t>(n, 4096u)), dim3(512), 0, s, pk_off, aff, code, rand,
-                       (const uint32_t*)mlist, (const uint32_t*)mcnt, P, set_code, n_bad, key_idx, tab_n, P2, comb, r_on_g2 ? 1u : 0u);
+                       (const uint32_t*)mlist, (const uint32_t*)mcnt, P, set_code, n_bad, key_idx, tab_n, P2, comb, 0u);
   else
     hipLaunchKernelGGL(k_set_pk_wave, dim3(std::min<uint32_t>(n, 4096u)), dim3(64), 0, s, pk_off, aff, code, rand,
                        (const uint32_t*)mlist, (const uint32_t*)mcnt, P, set_code, n_bad, key_idx, tab_n);
@@ -477,40 +448,14 @@ extern "C" __global__ void k_set_hash_wave(const uint8_t* __restrict__ msgs, con
 extern "C" __global__ void k_set_hash_coop(const uint8_t* __restrict__ msgs, const uint32_t* __restrict__ msg_off,
                                            const uint8_t* __restrict__ dst, uint32_t dlen, uint32_t n, g2a* __restrict__ Q,
                                            uint8_t* __restrict__ skip, const uint64_t* __restrict__ rand);  // k_hwave.hip (lane-cooperative, 256 threads)
-// small batches hash with the lane-cooperative kernel; TBLS_HASH_COOP=0 selects
-// the one-wave cofactor program (k_set_hash_wave) for A/B
-static bool hash_coop() {
-  static const bool v = !(getenv("TBLS_HASH_COOP") && getenv("TBLS_HASH_COOP")[0] == '0');
-  return v;
-}
 extern "C" __global__ void k_keys_coop(const uint8_t* __restrict__ pks, const uint32_t* __restrict__ pk_off, const g1a* __restrict__ tab_aff,
                                        const uint8_t* __restrict__ tab_code, const uint32_t* __restrict__ key_idx, uint32_t tab_n,
                                        const uint64_t* __restrict__ rand, uint32_t n, g1a* __restrict__ P, g1a* __restrict__ P2,
                                        uint8_t* __restrict__ set_code, uint32_t* __restrict__ n_bad, const g1a* __restrict__ comb);
 extern "C" __global__ void k_sig_check_coop(const uint8_t* __restrict__ sigs, uint32_t n, g2a* __restrict__ sig_aff, uint8_t* __restrict__ sig_use,
                                             uint8_t* __restrict__ sig_code, uint32_t* __restrict__ n_bad);  // k_kcoop.hip
-// small batches: lane-cooperative key and signature stages (k_kcoop.hip);
-// TBLS_KEYS_COOP=0 / TBLS_SIG_COOP=0 select the one-thread-per-item kernels (A/B)
-// two items per thread in the one-thread key / signature decompression
-// stages (k_pk_decompress2, k_sig_check2: both square-root chains
-// interleaved); TBLS_DEC2=1 selects them.  Measured and rejected as the
-// default (round 3, 131,072 sets): keys 3.47 -> 6.17 ms (spills, half the
-// waves), signatures 6.06 -> 6.00 ms; at 16,384 sets twice the latency.
-static bool dec2() {
-  static const bool v = getenv("TBLS_DEC2") && getenv("TBLS_DEC2")[0] == '1';
-  return v;
-}
-static bool keys_coop() {
-  static const bool v = !(getenv("TBLS_KEYS_COOP") && getenv("TBLS_KEYS_COOP")[0] == '0');
-  return v;
-}
-static bool sig_coop() {
-  static const bool v = !(getenv("TBLS_SIG_COOP") && getenv("TBLS_SIG_COOP")[0] == '0');
-  return v;
-}
-
 int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* partial_out, ws_layout& L,
-                   const uint8_t* dst, uint32_t dlen, hipEvent_t* ev = nullptr, bool serial_req = false,
+                   const uint8_t* dst, uint32_t dlen, hipEvent_t* ev = nullptr, bool serial = false,
                    const uint32_t* key_idx = nullptr) {
   const uint32_t n = b.n;
   const bool use_tab = key_idx != nullptr;  // keys = indices into the resident table: no decompression
@@ -523,19 +468,15 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
     if (c.ws.ensure(L.total)) return TBLS_DEVICE_ERROR;
   }
   uint8_t* w = c.ws.as<uint8_t>();
-  static const bool serial_env = getenv("TBLS_SERIAL") && getenv("TBLS_SERIAL")[0] == '1';
-  const bool serial = serial_env || serial_req;
-  // TBLS_ORDER=1 (default; large batches): the per-set stages in sequence on
-  // the caller's stream (signatures, keys, hash -- each kernel alone fills the
-  // GPU in whole wave rounds, no tail of lone hash waves), only the
-  // bucket-sum chain on a side stream; 0: the three per-set streams run
-  // concurrently (small batches always do).
-  static const int order_env = getenv("TBLS_ORDER") ? atoi(getenv("TBLS_ORDER")) : TB_ORDER_DEFAULT;
-  // TBLS_ORDER=2: hash then signatures on the caller's stream, the keys beside
-  // them on aux[0] (A/B).
-  const bool chain = !serial && pp.msm && (order_env == 1 || order_env == 2);
-  const bool hash_first = chain && order_env == 2;
-  hipStream_t sa = (serial || (chain && !hash_first)) ? s : c.aux[0], sb = serial ? s : c.aux[1], sh = (serial || chain) ? s : c.aux[2];
+  // `serial` (tbls_dev_batch_stage_profile): every stage on the caller's
+  // stream, for exclusive per-stage timings.  Large batches: the per-set
+  // stages in sequence on the caller's stream (signatures, keys, hash -- each
+  // kernel alone fills the GPU in whole wave rounds, no tail of lone hash
+  // waves), only the bucket-sum chain on a side stream (measured 52.5 vs 53.3
+  // ms per 131k step against three concurrent streams); small batches run the
+  // three per-set chains side by side.
+  const bool chain = !serial && pp.msm;
+  hipStream_t sa = (serial || chain) ? s : c.aux[0], sb = serial ? s : c.aux[1], sh = (serial || chain) ? s : c.aux[2];
   hipStream_t ssig = chain ? s : sb;
 #define TB_EV(i, st) \
   if (ev) HIPCHK(hipEventRecord(ev[i], st))
@@ -552,41 +493,6 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
     HIPCHK(hipStreamWaitEvent(sb, c.e_fork, 0));
     HIPCHK(hipStreamWaitEvent(sh, c.e_fork, 0));
   }
-  // TBLS_R_ON_G2=1 (A/B, multi-key batches of the coop-hash size): the
-  // randomizers multiply H(m) on the hash stream (k_set_hash_coop) instead of
-  // the aggregate keys.  Measured and rejected (round 3, 64 x 488 keys): the
-  // aggregation stage 1.06 -> 0.48 ms, but the coop G2 scalar multiplication
-  // lengthens the hash 1.82 -> 3.19 ms and the partial 4.70 -> 6.13 ms.
-  static const bool r_g2_env = getenv("TBLS_R_ON_G2") && getenv("TBLS_R_ON_G2")[0] == '1';
-  const bool r_on_g2 = r_g2_env && b.n_keys > n && n && n <= TB_HASH_WAVE_MAX && hash_coop();
-  auto launch_hash = [&]() -> int {
-    TB_EV(6, sh);
-    if (n && n <= TB_HASH_WAVE_MAX && hash_coop())  // one 256-thread workgroup per set: coop SSWU chains and cofactor program
-      hipLaunchKernelGGL(k_set_hash_coop, dim3(n), dim3(256), 0, sh, b.msgs, b.msg_off, dst, dlen, n, Q, skip, r_on_g2 ? b.rand : nullptr);
-    else if (n && n <= TB_HASH_WAVE_MAX)  // one workgroup per set: the cofactor clearing lane-parallel
-      hipLaunchKernelGGL(k_set_hash_wave, dim3(n), dim3(128), 0, sh, b.msgs, b.msg_off, dst, dlen, n, Q, skip);
-    else if (hash_row(n)) {  // one coop row per set (k_hrow.hip): five launches
-      static const int force_fix = getenv("TBLS_HROW_FORCE_FIX") && getenv("TBLS_HROW_FORCE_FIX")[0] == '1';
-      hrow_set* H = (hrow_set*)(w + L.hrow);
-      hipLaunchKernelGGL(k_hrow_field, g, blk, 0, sh, b.msgs, b.msg_off, dst, dlen, n, H);
-      // TBLS_HROW_WAVES: the coop kernels' register bound, waves per SIMD (A/B)
-      static const int hw = getenv("TBLS_HROW_WAVES") ? atoi(getenv("TBLS_HROW_WAVES")) : 2;
-      hipLaunchKernelGGL(hw >= 4 ? k_hrow_sswu4 : hw == 3 ? k_hrow_sswu3 : k_hrow_sswu, dim3((2 * n + 3) / 4), dim3(64), 0, sh, n, H);
-      hipLaunchKernelGGL(k_hrow_iso, g, blk, 0, sh, n, H);
-      hipLaunchKernelGGL(hw >= 3 ? k_hrow_cof3 : k_hrow_cof, dim3((n + 3) / 4), dim3(64), 0, sh, n, (const hrow_set*)H, Q, skip, force_fix);
-      hipLaunchKernelGGL(k_hrow_fix, g, blk, 0, sh, n, (const hrow_set*)H, Q, skip);
-    }
-    else if (hash_pair(n))
-      hipLaunchKernelGGL(k_set_hash_pair, dim3((2 * n + TB_BLOCK - 1) / TB_BLOCK), blk, 0, sh, b.msgs, b.msg_off, dst, dlen, n, Q, skip);
-    else if (n)
-      hipLaunchKernelGGL(k_set_hash, g, blk, 0, sh, b.msgs, b.msg_off, dst, dlen, n, Q, skip);
-    TB_EV(7, sh);
-    return TBLS_SUCCESS;
-  };
-  if (hash_first) {
-    const int rc = launch_hash();
-    if (rc != TBLS_SUCCESS) return rc;
-  }
   // --- stream b: signatures, then (large batches) the bucket sums -----------
   uint32_t* msm_cnt = (uint32_t*)(w + L.msm_cnt);
   uint32_t* msm_off = (uint32_t*)(w + L.msm_off);
@@ -600,20 +506,15 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
   }
   TB_EV(4, ssig);
   if (n) {
-    const dim3 g2((n + 1) / 2 / TB_BLOCK + 1);  // two sets per thread (k_sig_check2)
-    if (pp.msm && dec2())
-      hipLaunchKernelGGL(k_sig_check2, g2, blk, 0, ssig, b.sigs, n, (g2a*)(w + L.sig_aff), w + L.sig_use, w + L.sig_code,
-                         (uint32_t*)(w + L.n_bad), 0u);
-    else if (pp.msm)
-      hipLaunchKernelGGL(k_sig_check, g, blk, 0, ssig, b.sigs, n, (g2a*)(w + L.sig_aff), w + L.sig_use, w + L.sig_code,
-                         (uint32_t*)(w + L.n_bad), 0u);
-    else if (n <= TB_HASH_WAVE_MAX && sig_coop())  // the same, 4 sets per wave, lane-cooperative
+    if (pp.msm)
+      hipLaunchKernelGGL(w2() ? k_sig_check_w2 : k_sig_check, g, blk, 0, ssig, b.sigs, n, (g2a*)(w + L.sig_aff), w + L.sig_use,
+                         w + L.sig_code, (uint32_t*)(w + L.n_bad), 0u);
+    else if (n <= TB_HASH_WAVE_MAX && coop())  // the same, 4 sets per wave, lane-cooperative
       hipLaunchKernelGGL(k_sig_check_coop, dim3((n + 3) / 4), dim3(64), 0, ssig, b.sigs, n, (g2a*)(Q + n), skip + n, w + L.sig_code,
                          (uint32_t*)(w + L.n_bad));
-    else if (dec2())  // the set's signature pair: Q[n + i] = sig_i, skip[n + i] = infinite / invalid
-      hipLaunchKernelGGL(k_sig_check2, g2, blk, 0, ssig, b.sigs, n, Q + n, skip + n, w + L.sig_code, (uint32_t*)(w + L.n_bad), 1u);
-    else
-      hipLaunchKernelGGL(k_sig_check, g, blk, 0, ssig, b.sigs, n, Q + n, skip + n, w + L.sig_code, (uint32_t*)(w + L.n_bad), 1u);
+    else  // the set's signature pair: Q[n + i] = sig_i, skip[n + i] = infinite / invalid
+      hipLaunchKernelGGL(w2() ? k_sig_check_w2 : k_sig_check, g, blk, 0, ssig, b.sigs, n, Q + n, skip + n, w + L.sig_code,
+                         (uint32_t*)(w + L.n_bad), 1u);
   }
   TB_EV(5, ssig);
   if (chain) {  // the bucket sums need the decoded signatures
@@ -621,12 +522,11 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
     HIPCHK(hipStreamWaitEvent(sb, c.e_sig, 0));
   }
   // Large split batches: the main pairs' line kernel needs only the signature
-  // codes from this stream, not the bucket sums and the extra pairs' lines
-  // (one 64-lane launch of ~2.5 ms): it waits on e_sig, and only the
-  // accumulator launch that absorbs the extra lines waits on e_join[1].
+  // codes from this stream, not the bucket sums and the extra pairs' Miller
+  // loops (one 64-lane launch of ~2.5 ms): it waits on e_sig, and only the
+  // product tree waits on e_join[1].
   const bool late_join = !serial && pp.msm && pp.split;
-  const bool early_sig = !serial && pp.halves;  // the signature pairs' Miller loops on sb (pair_plan halves)
-  if ((late_join && !chain) || early_sig) HIPCHK(hipEventRecord(c.e_sig, sb));
+  if (late_join && !chain) HIPCHK(hipEventRecord(c.e_sig, sb));
   TB_EV(8, sb);
   if (pp.msm) {
     hipLaunchKernelGGL(k_msm_bucket, dim3(TB_MSM_PARTS / TB_BLOCK), blk, 0, sb, (const g2a*)(w + L.sig_aff), (const uint8_t*)(w + L.sig_use),
@@ -637,29 +537,12 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
     if (pp.n_xwave)  // their Miller loops, one wave each, on this stream: f[n_f_main ..)
       hipLaunchKernelGGL(k_miller_wave, dim3(pp.n_xwave), dim3(64), 0, sb, (const g1a*)P + n, (const g2a*)Q + n, (const uint8_t*)skip + n,
                          (const uint8_t*)(w + L.set_code + n), (const uint8_t*)(w + L.sig_code + n), pp.n_xwave, (fp12*)(w + L.f) + pp.n_f_main());
-    if (pp.n_spread)  // their lines now, on this stream (the main pairs' kernel would take a whole extra wave round)
-      hipLaunchKernelGGL(k_miller_lines, dim3(1), dim3(TB_MSM_XPAIRS), 0, sb, (const g1a*)P + n, (const g2a*)Q + n, (const uint8_t*)skip + n,
-                         w + L.set_code + n, w + L.sig_code + n, TB_MSM_XPAIRS, (uint4*)(w + L.xlines));
   }
   TB_EV(9, sb);
   HIPCHK(hipEventRecord(c.e_join[1], sb));
-  // one half of a halves plan: lines + segmented accumulator of m = n pairs
-  // from pair offset `off` into the group range [goff, goff + half_groups)
-  auto launch_half = [&](hipStream_t st, uint32_t off, uint32_t goff, uint4* lbuf) {
-    const uint8_t* ca = w + L.set_code;
-    const uint8_t* cb = w + L.sig_code;
-    const uint32_t m = n, mt = pp.half_groups();
-    hipLaunchKernelGGL(lines_kernel(), dim3((m + TB_BLOCK - 1) / TB_BLOCK), blk, 0, st, (const g1a*)P + off, (const g2a*)Q + off,
-                       (const uint8_t*)skip + off, ca + off, cb + off, m, lbuf);
-    const uint32_t g_pad = (mt + TB_BLOCK - 1) / TB_BLOCK * TB_BLOCK;
-    hipLaunchKernelGGL(accs_kernel(), dim3(pp.nseg * g_pad / TB_BLOCK), blk, 0, st, (const uint4*)lbuf, (const uint8_t*)skip + off,
-                       ca + off, cb + off, m, pp.per, pp.nseg, g_pad, (fp12*)(w + L.f) + goff, pp.n_groups());
-  };
-  uint4* lines_a = (uint4*)(w + L.lines);
-  uint4* lines_b = (uint4*)(w + L.lines + (size_t)n * TB_LINE_BYTES_PER_PAIR);
   // --- stream a: public keys, [r] apk (+ -[r] g1 for the signature pairs) -----
   TB_EV(0, sa);
-  if (b.n_keys == n && n && n <= TB_HASH_WAVE_MAX && keys_coop()) {
+  if (b.n_keys == n && n && n <= TB_HASH_WAVE_MAX && coop()) {
     // one kernel: decode + G1 check (wave 0) beside -[r] g1, then [r] pk (wave
     // 1); its time shows as stage 0.  As many keys as sets: one key per set
     // in every real batch (a set of several keys beside empty ones still
@@ -671,43 +554,52 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
     TB_EV(1, sa);
     TB_EV(2, sa);
   } else {
-    if (K && dec2())
-      hipLaunchKernelGGL(k_pk_decompress2, dim3(((K + 1) / 2 + TB_BLOCK - 1) / TB_BLOCK), blk, 0, sa, b.pks, K, (g1a*)(w + L.pk_aff), w + L.pk_code);
-    else if (K)
+    if (K)
       hipLaunchKernelGGL(k_pk_decompress, dim3((K + TB_BLOCK - 1) / TB_BLOCK), blk, 0, sa, b.pks, K, (g1a*)(w + L.pk_aff), w + L.pk_code);
     TB_EV(1, sa);
     TB_EV(2, sa);
     launch_set_pk(sa, n, b.n_keys, b.pk_off, use_tab ? c.tab_aff.as<const g1a>() : (const g1a*)(w + L.pk_aff),
                   use_tab ? c.tab_code.as<const uint8_t>() : (const uint8_t*)(w + L.pk_code), b.rand, P, w + L.set_code,
                   (uint32_t*)(w + L.n_bad), key_idx, use_tab ? c.tab_n : 0u, (uint32_t*)(w + L.mlist), (uint32_t*)(w + L.mcnt),
-                  pp.msm ? nullptr : P + n, c.comb.as<const g1a>(), r_on_g2);
+                  pp.msm ? nullptr : P + n, c.comb.as<const g1a>());
   }
   TB_EV(3, sa);
   HIPCHK(hipEventRecord(c.e_join[0], sa));
-  if (early_sig) {  // the signature pairs (-[r_i] g1, sig_i): keys' P2 + the signature stage, beside the hash
-    HIPCHK(hipStreamWaitEvent(sb, c.e_join[0], 0));
-    launch_half(sb, n, pp.half_groups(), lines_b);
-    HIPCHK(hipEventRecord(c.e_join[1], sb));
-  }
   // --- high-priority stream: hash_to_G2 per set -------------------------------
   // The longest per-set stage (2 wave rounds at 131k sets): with queue
   // priority its waves are dispatched first and the shorter key / signature
   // stages fill the SIMDs around them, instead of its last waves running
   // alone after the others finish.
-  if (!hash_first) {
-    const int rc = launch_hash();
-    if (rc != TBLS_SUCCESS) return rc;
-  }
+  TB_EV(6, sh);
+  if (n && n <= TB_HASH_WAVE_MAX && coop())  // one 256-thread workgroup per set: coop SSWU chains and cofactor program
+    hipLaunchKernelGGL(k_set_hash_coop, dim3(n), dim3(256), 0, sh, b.msgs, b.msg_off, dst, dlen, n, Q, skip, (const uint64_t*)nullptr);
+  else if (n && n <= TB_HASH_WAVE_MAX)  // one workgroup per set: the cofactor clearing lane-parallel
+    hipLaunchKernelGGL(k_set_hash_wave, dim3(n), dim3(128), 0, sh, b.msgs, b.msg_off, dst, dlen, n, Q, skip);
+  else if (hash_row(n)) {  // one coop row per set (k_hrow.hip): five launches
+    static const int force_fix = getenv("TBLS_HROW_FORCE_FIX") && getenv("TBLS_HROW_FORCE_FIX")[0] == '1';
+    hrow_set* H = (hrow_set*)(w + L.hrow);
+    hipLaunchKernelGGL(k_hrow_field, g, blk, 0, sh, b.msgs, b.msg_off, dst, dlen, n, H);
+    hipLaunchKernelGGL(k_hrow_sswu, dim3((2 * n + 3) / 4), dim3(64), 0, sh, n, H);
+    hipLaunchKernelGGL(k_hrow_iso, g, blk, 0, sh, n, H);
+    hipLaunchKernelGGL(k_hrow_cof, dim3((n + 3) / 4), dim3(64), 0, sh, n, (const hrow_set*)H, Q, skip, force_fix);
+    hipLaunchKernelGGL(k_hrow_fix, g, blk, 0, sh, n, (const hrow_set*)H, Q, skip);
+  } else if (hash_pair(n))
+    hipLaunchKernelGGL(k_set_hash_pair, dim3((2 * n + TB_BLOCK - 1) / TB_BLOCK), blk, 0, sh, b.msgs, b.msg_off, dst, dlen, n, Q, skip);
+  else if (n && w2()) {  // two waves per SIMD, then the exact formulas for the sets it flags (skip == 2)
+    hipLaunchKernelGGL(k_set_hash_w2, g, blk, 0, sh, b.msgs, b.msg_off, dst, dlen, n, Q, skip);
+    hipLaunchKernelGGL(k_set_hash_fix, g, blk, 0, sh, b.msgs, b.msg_off, dst, dlen, n, Q, skip);
+  } else if (n)
+    hipLaunchKernelGGL(k_set_hash, g, blk, 0, sh, b.msgs, b.msg_off, dst, dlen, n, Q, skip);
+  TB_EV(7, sh);
   if (!serial) {
     HIPCHK(hipEventRecord(c.e_join[2], sh));
     HIPCHK(hipStreamWaitEvent(s, c.e_join[2], 0));
   }
   HIPCHK(hipStreamWaitEvent(s, c.e_join[0], 0));
-  if (!late_join && !early_sig)
+  if (!late_join)
     HIPCHK(hipStreamWaitEvent(s, c.e_join[1], 0));
   else if (!chain)
     HIPCHK(hipStreamWaitEvent(s, c.e_sig, 0));  // the set pairs' lines read the signature codes
-  bool joined = !late_join && !early_sig;
   // --- Miller loops of all pairs (pairs of invalid sets contribute 1) ---------
   const uint32_t np = pp.n_pairs, nf = pp.n_f();
   TB_EV(10, s);
@@ -715,39 +607,28 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
     const uint8_t* ca = w + L.set_code;
     const uint8_t* cb = w + L.sig_code;
     fp12* f = (fp12*)(w + L.f);
-    if (pp.wave)
+    if (pp.wave) {
       hipLaunchKernelGGL(k_miller_wave, dim3(np), dim3(64), 0, s, (const g1a*)P, (const g2a*)Q, (const uint8_t*)skip, ca, cb, np, f);
-    else if (pp.halves) {  // the set pairs (after the hash); the signature pairs ran on sb (or run here when serial)
-      launch_half(s, 0, 0, lines_a);
-      if (!early_sig) launch_half(s, n, pp.half_groups(), lines_b);
-    } else if (pp.split) {
-      // chunks of the main pairs; the spread pairs' lines (xlines) are absorbed by the last chunk
+    } else {
+      // chunks of the main pairs: G2 lines (P and T in LDS), then the Fp12
+      // accumulator (segment-major values: segment j of group g at f[j * n_groups + g])
       uint4* lines = (uint4*)(w + L.lines);
       for (uint32_t lo = 0; lo < pp.n_main; lo += TB_LINE_CHUNK) {
         const uint32_t m = std::min(TB_LINE_CHUNK, pp.n_main - lo), mt = (m + pp.per - 1) / pp.per;
-        const uint32_t ex = lo + m == pp.n_main ? pp.n_spread : 0u;
-        hipLaunchKernelGGL(lines_kernel(), dim3((m + TB_BLOCK - 1) / TB_BLOCK), blk, 0, s, (const g1a*)P + lo, (const g2a*)Q + lo,
+        hipLaunchKernelGGL(k_miller_lines_lds, dim3((m + TB_BLOCK - 1) / TB_BLOCK), blk, 0, s, (const g1a*)P + lo, (const g2a*)Q + lo,
                            (const uint8_t*)skip + lo, ca + lo, cb + lo, m, lines);
-        if (ex && !joined) {  // this accumulator launch reads the extra pairs' lines and skip flags
-          HIPCHK(hipStreamWaitEvent(s, c.e_join[1], 0));
-          joined = true;
-        }
-        if (pp.seg()) {  // segment-major values: segment j of group g at f[j * n_groups + g]
+        if (pp.seg()) {
           const uint32_t g_pad = (mt + TB_BLOCK - 1) / TB_BLOCK * TB_BLOCK;
-          // TBLS_ACC_PAIRS=1: two lines per product (fp12_mul_by_line_pair_i: 23 vs 26 Fp2 products, more registers)
-          hipLaunchKernelGGL(accs_kernel(), dim3(pp.nseg * g_pad / TB_BLOCK), blk, 0, s, (const uint4*)lines, (const uint8_t*)skip + lo,
+          hipLaunchKernelGGL(k_miller_accs, dim3(pp.nseg * g_pad / TB_BLOCK), blk, 0, s, (const uint4*)lines, (const uint8_t*)skip + lo,
                              ca + lo, cb + lo, m, pp.per, pp.nseg, g_pad, f + lo / pp.per, pp.n_groups());
         } else {
           hipLaunchKernelGGL(pp.per == 2 ? k_miller_acc2 : k_miller_acc1, dim3((mt + TB_BLOCK - 1) / TB_BLOCK), blk, 0, s,
-                             (const uint4*)lines, (const uint8_t*)skip + lo, ca + lo, cb + lo, m, (const uint4*)(w + L.xlines),
-                             (const uint8_t*)skip + pp.n_main, ex, f + lo / pp.per);
+                             (const uint4*)lines, (const uint8_t*)skip + lo, ca + lo, cb + lo, m, f + lo / pp.per);
         }
       }
-    } else
-      hipLaunchKernelGGL(pp.per == 1 ? k_miller1 : k_miller2, dim3((nf + TB_BLOCK - 1) / TB_BLOCK), blk, 0, s, (const g1a*)P,
-                         (const g2a*)Q, (const uint8_t*)skip, ca, cb, np, f);
+    }
   }
-  if (!joined) HIPCHK(hipStreamWaitEvent(s, c.e_join[1], 0));  // every stream joins before ws_release
+  if (late_join) HIPCHK(hipStreamWaitEvent(s, c.e_join[1], 0));  // every stream joins before ws_release
   TB_EV(11, s);
   TB_EV(12, s);
   if (nf == 0) {  // no pairs at all: the partial product is 1

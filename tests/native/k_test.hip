@@ -11,11 +11,13 @@
 
 using namespace tb;
 
+// the field / tower / pairing half of the ops (test_op_a); k_test_b.hip has the other
 extern "C" __global__ void __launch_bounds__(TB_BLOCK) k_test_ops(int op, const uint8_t* in, uint8_t* out, uint32_t n) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  test_op(op, in + (size_t)i * TB_TEST_IN, out + (size_t)i * TB_TEST_OUT);
+  (void)test_op_a(op, in + (size_t)i * TB_TEST_IN, out + (size_t)i * TB_TEST_OUT);
 }
+extern "C" __global__ void k_test_ops_b(int op, const uint8_t* in, uint8_t* out, uint32_t n);  // k_test_b.hip
 
 // test hook: one final exponentiation per 64-lane block (tb_testops.h record layout)
 extern "C" __global__ void __launch_bounds__(64) k_test_final_exp_wave(const uint8_t* in, uint8_t* out) {
@@ -149,8 +151,10 @@ extern "C" int tbls_test_ops(int op, const uint8_t* in, uint8_t* out, size_t n) 
       hipLaunchKernelGGL(k_test_coop_timing, dim3(1), dim3(64), 0, 0, din, dout);
     else if (op == TOP_CLEAR_COF_PROG)
       hipLaunchKernelGGL(k_test_clear_cof_prog, dim3((uint32_t)n), dim3(64), 0, 0, din, dout);
-    else
+    else if (test_op_in_a(op))
       hipLaunchKernelGGL(k_test_ops, dim3((uint32_t)((n + TB_BLOCK - 1) / TB_BLOCK)), dim3(TB_BLOCK), 0, 0, op, din, dout, (uint32_t)n);
+    else
+      hipLaunchKernelGGL(k_test_ops_b, dim3((uint32_t)((n + TB_BLOCK - 1) / TB_BLOCK)), dim3(TB_BLOCK), 0, 0, op, din, dout, (uint32_t)n);
     if (hipGetLastError() == hipSuccess && hipDeviceSynchronize() == hipSuccess &&
         hipMemcpy(out, dout, n * TB_TEST_OUT, hipMemcpyDeviceToHost) == hipSuccess)
       rc = 0;

@@ -10,6 +10,8 @@
 //              force_fix != 0 sends every set through the one-lane k_hrow_fix
 //   variant 3  k_set_hash_coop     (256-thread workgroup per set; <= 512)
 //   variant 4  k_set_hash_wave     (64-lane cofactor program; the coop fall-back)
+//   variant 5  k_set_hash_w2 + k_set_hash_fix (two waves per SIMD; above 32,768,
+//              the default); force_fix != 0 flags every set for k_set_hash_fix
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -75,6 +77,11 @@ extern "C" int tbls_test_hash_variant(const char* product_so, int variant, const
       break;
     case 3: rc = launch(sym("k_set_hash_coop"), n32, 256, a_coop); break;
     case 4: rc = launch(sym("k_set_hash_wave"), n32, 128, a_set); break;
+    case 5:
+      rc = launch(sym("k_set_hash_w2"), g, BLK, a_set);
+      if (!rc && ff && hipMemset(dskip.p, 2, n) != hipSuccess) rc = -6;  // every set through the exact recomputation
+      if (!rc) rc = launch(sym("k_set_hash_fix"), g, BLK, a_set);
+      break;
     default: return -1;
   }
   if (rc) return rc;

@@ -2,12 +2,13 @@
 product trees + k_fp12_seg_combine_coop) computes the same Fp12 product as the
 unsegmented k_miller_acc1 / acc2: the partial record of a seeded batch, its
 12 coordinates canonicalized mod p, is identical under every accumulator plan
-(TBLS_ACC_SEG=0: the unsegmented kernels; forced pairs-per-thread x segment
-counts; the default plan; TBLS_ACC_PAIRS=1, the two-line products, with an
-odd pair count), on the per-set signature-pair path (3,000 sets) and
-the bucket-sum path with the wave bit-sum pairs in the last segment (40,000
-sets).  Each plan runs in its own process (the plan is read once per process);
-the verdicts also go through the final exponentiation."""
+(TBLS_ACC_PLAN=0: the unsegmented kernels; forced pairs-per-thread x segment
+counts "per,nseg"; the default plan), on the per-set signature-pair path
+(3,000 sets) and the bucket-sum path with the wave bit-sum pairs in the last
+segment (40,000 sets), and across line chunks (300,000 sets: more pairs than
+one 262,144-pair line chunk, so later chunks' groups start at lo / per).  Each
+plan runs in its own process (the plan is read once per process); the
+verdicts also go through the final exponentiation."""
 
 import json
 import os
@@ -20,10 +21,8 @@ pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
-PLANS = [{"TBLS_ACC_SEG": "0"}, {}, {"TBLS_ACC_PER": "8", "TBLS_ACC_SEG": "4"}, {"TBLS_ACC_PER": "1", "TBLS_ACC_SEG": "2"},
-         {"TBLS_ACC_PER": "4", "TBLS_ACC_SEG": "1"}, {"TBLS_ACC_PAIRS": "1"}, {"TBLS_ACC_PAIRS": "1", "TBLS_ACC_PER": "3", "TBLS_ACC_SEG": "2"},
-         {"TBLS_HALVES": "1"}, {"TBLS_HALVES": "1", "TBLS_ACC_PER": "3", "TBLS_ACC_SEG": "4"}, {"TBLS_ACC_PER": "3", "TBLS_ACC_SEG": "4"},
-         {"TBLS_ACC_LDS": "1", "TBLS_LINES_LDS": "1"}, {"TBLS_ACC_LDS": "1", "TBLS_ACC_PER": "2", "TBLS_ACC_SEG": "2"}]
+PLANS = [{"TBLS_ACC_PLAN": "0"}, {}, {"TBLS_ACC_PLAN": "8,4"}, {"TBLS_ACC_PLAN": "1,2"}, {"TBLS_ACC_PLAN": "4,1"},
+         {"TBLS_ACC_PLAN": "2,3"}, {"TBLS_ACC_PLAN": "8,2"}]
 
 
 def _record(n, env_extra, tamper=-1):
@@ -45,6 +44,17 @@ def test_segmented_accumulator_same_product(n):
 
 def test_segmented_accumulator_tampered():
     a = _record(3000, {}, tamper=1234)
-    b = _record(3000, {"TBLS_ACC_SEG": "0"}, tamper=1234)
+    b = _record(3000, {"TBLS_ACC_PLAN": "0"}, tamper=1234)
     assert a["ok"] == b["ok"] == 0
     assert a["coords"] == b["coords"]
+
+
+def test_segmented_accumulator_across_line_chunks():
+    """300,000 sets: 300,064 pairs in two line chunks (262,144 + 37,920); the
+    second chunk's groups follow the first's (a pairs-per-thread
+    count that does not divide the chunk would misplace them; the plan only
+    takes powers of two)."""
+    recs = [_record(300000, p) for p in ({"TBLS_ACC_PLAN": "0"}, {}, {"TBLS_ACC_PLAN": "8,4"}, {"TBLS_ACC_PLAN": "4,3"})]
+    for r in recs:
+        assert r["ok"] == 1 and r["n_bad"] == 0
+        assert r["coords"] == recs[0]["coords"]

@@ -128,3 +128,20 @@ def test_stage_set_hash_bytes(run):
         for m, out in zip(msgs, outs):
             assert u32(out[:4]) == 1
             assert out[4:100] == C.hash_to_g2(m, dst), m
+
+
+def test_g2_in_group_branch_free(run):
+    """g2_in_group_nx (the two-wave signature check's subgroup test) gives
+    g2_in_group's verdict on G2 points, random E2 points and small-order
+    points (whose [|x|] chain may meet P = +-Q)."""
+    import random as _r
+
+    from tests.test_gpu_kcoop import N2, _rand_e2, _torsion
+
+    rng = _r.Random(41)
+    g2 = [O.jac_to_affine(O.FP2, O.clear_cofactor_g2(O.jac_from_affine(O.FP2, _rand_e2(rng)))) for _ in range(4)]
+    other = [_rand_e2(rng) for _ in range(4)] + [_torsion(O.FP2, _rand_e2, m, N2, rng) for m in (13, 23, 299)]
+    recs = [enc_fp2(x) + enc_fp2(y) for x, y in g2 + other]
+    a = [u32(x) for x in run("G2_IN_GROUP_NX", recs)]
+    b = [u32(x) for x in run("G2_IN_GROUP", recs)]
+    assert a == b == [1] * len(g2) + [0] * len(other)

@@ -94,8 +94,10 @@ static float run(Kf k, T* d, int blocks, int iters) {
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0);
   (void)hipEventCreate(&e1);
+  fprintf(stderr, "launch %d blocks x %d iters\n", blocks, iters);
   hipLaunchKernelGGL(k, dim3(blocks), dim3(256), 0, 0, d, iters);
-  (void)hipDeviceSynchronize();
+  const hipError_t e = hipDeviceSynchronize();
+  if (e != hipSuccess) fprintf(stderr, "kernel error: %s\n", hipGetErrorString(e));
   float best = 1e30f;
   for (int r = 0; r < 3; r++) {
     (void)hipEventRecord(e0, 0);
@@ -120,6 +122,7 @@ int main() {
   // per SIMD: one wave (64 lanes) runs `it` iterations; cycles per op = ms * clk / (it * ops)
   auto report = [&](const char* what, float ms, double ops_per_iter) {
     printf("{\"what\": \"%s\", \"ms\": %.3f, \"cycles_per_op_at_max_clock\": %.1f}\n", what, ms, ms * 1e-3 * clk / (it * ops_per_iter));
+    fflush(stdout);
   };
   report("fp2_mul_lazy x1", run(k_fp2mul<1>, (fp2*)d, blocks, it), 1);
   report("fp2_mul_lazy x2", run(k_fp2mul<2>, (fp2*)d, blocks, it), 2);

@@ -1,7 +1,7 @@
 """Print the partial record (tbls_dev_batch_partial) of a seeded synthetic
 batch as JSON: the 12 Fp coordinates of the Miller product canonicalized mod p
 (hex) and the invalid count.  The accumulator plan follows the environment
-(TBLS_ACC_PER / TBLS_ACC_SEG / TBLS_MILLER_SPLIT), so tests/test_gpu_accseg.py
+(TBLS_ACC_PLAN), so tests/test_gpu_accseg.py
 runs it once per plan and compares the products.
 
     python tools/partial_record.py N [seed] [tamper_index]
