@@ -21,6 +21,7 @@
 
 #include "../../include/tekubls.h"
 #include "tb_kdecl.h"
+#include "tb_kdecl_mid.h"
 #include "tb_hrow.h"
 #include "tb_host.h"
 
@@ -324,23 +325,34 @@ struct pair_plan {
   uint32_t line_pairs() const { return split ? std::min(n_main, TB_LINE_CHUNK) : 0u; }
 };
 
-// hash_to_G2 on one coop row per set (k_hrow.hip) for batches above the
-// workgroup-per-set kernels' range and up to TBLS_HASH_ROW_MAX sets (default
-// TB_HASH_ROW_MAX); 0 disables it (A/B).  Above it the one-lane k_set_hash.
+// hash_to_G2 kernel by batch size above the workgroup-per-set kernels' range
+// (TB_HASH_WAVE_MAX): one 16-lane coop row per set (k_hrow.hip) up to row_max
+// sets, one quad per set (k_hquad.hip k_set_hash_quad) up to quad_max, two
+// lanes per set (k_set_hash_pair, one SSWU map each) up to pair_max, then the
+// one-lane k_set_hash_w2.  The quad Miller line kernel (k_miller_lines_quad)
+// takes the pairs of batches up to quad_max too.  TBLS_HASH_PLAN =
+// "row_max,quad_max,pair_max" overrides the defaults (A/B; 0 disables a
+// kernel).
 #define TB_HASH_ROW_MAX 4096u
-static uint32_t hash_row_max() {
-  static const uint32_t v = getenv("TBLS_HASH_ROW_MAX") ? (uint32_t)atoi(getenv("TBLS_HASH_ROW_MAX")) : TB_HASH_ROW_MAX;
+#define TB_HASH_QUAD_MAX 16384u  // 4 lanes x 16,384 sets: one wave per SIMD
+#define TB_HASH_PAIR_MAX 32768u  // 2 lanes x 32,768 sets: the same
+struct hash_plan_t {
+  uint32_t row_max, quad_max, pair_max;
+};
+static const hash_plan_t& hash_plan() {
+  static const hash_plan_t v = [] {
+    hash_plan_t h{TB_HASH_ROW_MAX, TB_HASH_QUAD_MAX, TB_HASH_PAIR_MAX};
+    const char* e = getenv("TBLS_HASH_PLAN");
+    unsigned r, q, p;
+    if (e && sscanf(e, "%u,%u,%u", &r, &q, &p) == 3) h = {r, q, p};
+    return h;
+  }();
   return v;
 }
-static bool hash_row(uint32_t n) { return n > TB_HASH_WAVE_MAX && n <= hash_row_max(); }
-// above the row hash and up to TBLS_HASH_PAIR_MAX sets (default 32,768: the
-// pairs' lanes then fill every SIMD once): two lanes per set, one SSWU map
-// each (k_set_hash_pair); 0 disables it (A/B)
-#define TB_HASH_PAIR_MAX 32768u
-static bool hash_pair(uint32_t n) {
-  static const uint32_t v = getenv("TBLS_HASH_PAIR_MAX") ? (uint32_t)atoi(getenv("TBLS_HASH_PAIR_MAX")) : TB_HASH_PAIR_MAX;
-  return n > TB_HASH_WAVE_MAX && !hash_row(n) && n <= v;
-}
+static bool hash_row(uint32_t n) { return n > TB_HASH_WAVE_MAX && n <= hash_plan().row_max; }
+static bool hash_quad(uint32_t n) { return n > TB_HASH_WAVE_MAX && !hash_row(n) && n <= hash_plan().quad_max; }
+static bool hash_pair(uint32_t n) { return n > TB_HASH_WAVE_MAX && !hash_row(n) && !hash_quad(n) && n <= hash_plan().pair_max; }
+static bool lines_quad(uint32_t n_main) { return n_main <= hash_plan().quad_max; }
 
 struct ws_layout {
   size_t pk_aff, pk_code, P, Q, skip, set_code, sig_code, f, fpart, fpart2, segv, n_bad, result;
@@ -399,13 +411,15 @@ struct ws_layout {
 // run side by side.  `serial` (the stage-profile API) runs everything on the
 // caller's stream, for exclusive per-stage timings.
 
-// The large-batch one-lane kernels (hash, signature check, [r] apk) as their
-// two-waves-per-SIMD twins (k_w2_*.hip); TBLS_W2=0 selects the one-wave
-// kernels (A/B).
-static bool w2() {
-  static const bool v = !(getenv("TBLS_W2") && getenv("TBLS_W2")[0] == '0');
+// Two-waves-per-SIMD twins (k_w2_*.hip), TBLS_W2 = bit mask: 1 = the
+// large-batch one-lane kernels (hash, signature check, [r] apk), 2 = the G2
+// line kernel, 4 = the Fp12 accumulator (the segmented body for every plan).
+// Default 1; 0 selects the one-wave kernels throughout (A/B).
+static int w2mask() {
+  static const int v = getenv("TBLS_W2") ? (int)strtol(getenv("TBLS_W2"), nullptr, 0) : 1;
   return v;
 }
+static bool w2() { return (w2mask() & 1) != 0; }
 // Small batches (<= TB_HASH_WAVE_MAX sets) run the key, signature and hash
 // stages, and multi-key aggregation, on the lane-cooperative kernels
 // (k_kcoop.hip, k_hwave.hip k_set_hash_coop); TBLS_COOP=0 selects the
@@ -576,13 +590,15 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
   else if (n && n <= TB_HASH_WAVE_MAX)  // one workgroup per set: the cofactor clearing lane-parallel
     hipLaunchKernelGGL(k_set_hash_wave, dim3(n), dim3(128), 0, sh, b.msgs, b.msg_off, dst, dlen, n, Q, skip);
   else if (hash_row(n)) {  // one coop row per set (k_hrow.hip): five launches
-    static const int force_fix = getenv("TBLS_HROW_FORCE_FIX") && getenv("TBLS_HROW_FORCE_FIX")[0] == '1';
     hrow_set* H = (hrow_set*)(w + L.hrow);
     hipLaunchKernelGGL(k_hrow_field, g, blk, 0, sh, b.msgs, b.msg_off, dst, dlen, n, H);
     hipLaunchKernelGGL(k_hrow_sswu, dim3((2 * n + 3) / 4), dim3(64), 0, sh, n, H);
     hipLaunchKernelGGL(k_hrow_iso, g, blk, 0, sh, n, H);
-    hipLaunchKernelGGL(k_hrow_cof, dim3((n + 3) / 4), dim3(64), 0, sh, n, (const hrow_set*)H, Q, skip, force_fix);
+    hipLaunchKernelGGL(k_hrow_cof, dim3((n + 3) / 4), dim3(64), 0, sh, n, (const hrow_set*)H, Q, skip, 0);
     hipLaunchKernelGGL(k_hrow_fix, g, blk, 0, sh, n, (const hrow_set*)H, Q, skip);
+  } else if (hash_quad(n)) {  // one quad per set, then the exact formulas for the sets it flags (skip == 2)
+    hipLaunchKernelGGL(k_set_hash_quad, dim3((4 * n + TB_BLOCK - 1) / TB_BLOCK), blk, 0, sh, b.msgs, b.msg_off, dst, dlen, n, Q, skip);
+    hipLaunchKernelGGL(k_set_hash_fix, g, blk, 0, sh, b.msgs, b.msg_off, dst, dlen, n, Q, skip);
   } else if (hash_pair(n))
     hipLaunchKernelGGL(k_set_hash_pair, dim3((2 * n + TB_BLOCK - 1) / TB_BLOCK), blk, 0, sh, b.msgs, b.msg_off, dst, dlen, n, Q, skip);
   else if (n && w2()) {  // two waves per SIMD, then the exact formulas for the sets it flags (skip == 2)
@@ -615,12 +631,17 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
       uint4* lines = (uint4*)(w + L.lines);
       for (uint32_t lo = 0; lo < pp.n_main; lo += TB_LINE_CHUNK) {
         const uint32_t m = std::min(TB_LINE_CHUNK, pp.n_main - lo), mt = (m + pp.per - 1) / pp.per;
-        hipLaunchKernelGGL(k_miller_lines_lds, dim3((m + TB_BLOCK - 1) / TB_BLOCK), blk, 0, s, (const g1a*)P + lo, (const g2a*)Q + lo,
-                           (const uint8_t*)skip + lo, ca + lo, cb + lo, m, lines);
-        if (pp.seg()) {
+        if (lines_quad(pp.n_main))  // mid-size batches: one quad per pair
+          hipLaunchKernelGGL(k_miller_lines_quad, dim3((4 * m + TB_BLOCK - 1) / TB_BLOCK), blk, 0, s, (const g1a*)P + lo,
+                             (const g2a*)Q + lo, (const uint8_t*)skip + lo, ca + lo, cb + lo, m, lines);
+        else
+          hipLaunchKernelGGL((w2mask() & 2) ? k_miller_lines_w2 : k_miller_lines_lds, dim3((m + TB_BLOCK - 1) / TB_BLOCK), blk, 0, s,
+                             (const g1a*)P + lo, (const g2a*)Q + lo, (const uint8_t*)skip + lo, ca + lo, cb + lo, m, lines);
+        if (pp.seg() || (w2mask() & 4)) {  // unsegmented plans as nseg = 1
           const uint32_t g_pad = (mt + TB_BLOCK - 1) / TB_BLOCK * TB_BLOCK;
-          hipLaunchKernelGGL(k_miller_accs, dim3(pp.nseg * g_pad / TB_BLOCK), blk, 0, s, (const uint4*)lines, (const uint8_t*)skip + lo,
-                             ca + lo, cb + lo, m, pp.per, pp.nseg, g_pad, f + lo / pp.per, pp.n_groups());
+          hipLaunchKernelGGL((w2mask() & 4) ? k_miller_accs_w2 : k_miller_accs, dim3(pp.nseg * g_pad / TB_BLOCK), blk, 0, s,
+                             (const uint4*)lines, (const uint8_t*)skip + lo, ca + lo, cb + lo, m, pp.per, pp.nseg, g_pad, f + lo / pp.per,
+                             pp.n_groups());
         } else {
           hipLaunchKernelGGL(pp.per == 2 ? k_miller_acc2 : k_miller_acc1, dim3((mt + TB_BLOCK - 1) / TB_BLOCK), blk, 0, s,
                              (const uint4*)lines, (const uint8_t*)skip + lo, ca + lo, cb + lo, m, f + lo / pp.per);

@@ -1,17 +1,18 @@
 """Byte-level parity of the batch hash_to_G2 kernels.
 
-batchVerify hashes with one of four kernels by batch size (tb_lib.hip
-launch_partial): k_set_hash (> 32,768 sets), k_set_hash_pair (4,097 -
-32,768), the row pipeline k_hrow_* (513 - 4,096) and k_set_hash_coop (<= 512;
-k_set_hash_wave is its fall-back); above 32,768 sets the default is the
-two-waves-per-SIMD k_set_hash_w2 with its exact recomputation k_set_hash_fix.  Each one runs here on the same 640
+batchVerify hashes with one of five kernels by batch size (tb_lib.hip
+launch_partial, hash_plan): k_set_hash_w2 + k_set_hash_fix (> 32,768 sets;
+k_set_hash is its one-wave A/B twin), k_set_hash_pair (16,385 - 32,768),
+k_set_hash_quad + k_set_hash_fix (4,097 - 16,384), the row pipeline k_hrow_*
+(513 - 4,096) and k_set_hash_coop (<= 512; k_set_hash_wave is its
+fall-back).  Each one runs here on the same 640
 messages -- empty, 200-byte, random lengths up to 256 bytes -- under the
 Ethereum POP DST and the NUL DST (BLSTest.java:375-391), through the test
 library's hook (tests/native/k_test_hash.hip), which launches the PRODUCT
 library's kernels, and its compressed H(m) is compared byte for byte with the
 C oracle (oracle/c: hash_to_G2, RFC 9380) and with the committed golden
-vectors (tests/golden/vectors.json "hash_to_G2").  The row pipeline and the
-two-wave kernel also run with every set forced through their one-lane exact
+vectors (tests/golden/vectors.json "hash_to_G2").  The row pipeline, the
+two-wave kernel and the quad kernel also run with every set forced through their one-lane exact
 fall-backs (k_hrow_fix, k_set_hash_fix: the path a Z = 0 cofactor chain
 takes)."""
 
@@ -30,7 +31,7 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 NUL_DST = b"BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_NUL_"
 RINV = pow(1 << 406, -1, O.P)  # Montgomery R = 2^406 (tb_fp.h)
-VARIANTS = {0: "k_set_hash", 1: "k_set_hash_pair", 2: "k_hrow_*", 3: "k_set_hash_coop", 4: "k_set_hash_wave", 5: "k_set_hash_w2 + k_set_hash_fix"}
+VARIANTS = {0: "k_set_hash", 1: "k_set_hash_pair", 2: "k_hrow_*", 3: "k_set_hash_coop", 4: "k_set_hash_wave", 5: "k_set_hash_w2 + k_set_hash_fix", 6: "k_set_hash_quad + k_set_hash_fix"}
 
 
 def messages():
@@ -89,7 +90,7 @@ def test_hash_kernel_bytes(hook, expected, variant, dst):
     assert not bad, (VARIANTS[variant], len(bad), bad[:5])
 
 
-@pytest.mark.parametrize("variant", [2, 5])
+@pytest.mark.parametrize("variant", [2, 5, 6])
 def test_hash_fallback_bytes(hook, expected, variant):
     """Every set through the exact fall-back kernel (k_hrow_fix; k_set_hash_fix)."""
     ms, exp = expected

@@ -1,13 +1,14 @@
-"""The row hash (k_hrow.hip: one 16-lane coop row per set, batches of 513 to
-TBLS_HASH_ROW_MAX sets) and the pair hash (k_hash.hip k_set_hash_pair: two
-lanes per set, one SSWU map each, up to TBLS_HASH_PAIR_MAX sets) give the
-same H(m_i) as the one-lane k_set_hash: the
-partial record of a seeded batch -- the Miller product over (P_i, H(m_i)) and
-the signature pairs, canonicalized mod p -- is identical with the row hash on
-or pair hash on (default: row at 600 sets, pair at 16,384; the row hash
-forced at 16,384) and both off, valid and tampered, and with every
-set forced through the one-lane fallback of the exceptional cases
-(TBLS_HROW_FORCE_FIX=1, k_hrow_fix).  The verdicts also go through the final
+"""The mid-size hash and line kernels give the same partial records as the
+one-lane kernels: the row hash (k_hrow.hip: one 16-lane coop row per set, 513
+to 4,096 sets), the quad hash and quad Miller lines (k_hquad.hip: one DPP
+quad per set / pair, up to 16,384) and the pair hash (k_set_hash_pair: two
+lanes per set, up to 32,768).  The partial record of a seeded batch -- the
+Miller product over (P_i, H(m_i)) and the signature pairs, canonicalized mod
+p -- is identical with the default plan (row at 600 sets, quad at 16,384),
+the row hash or the pair hash forced at 16,384, and all of them off
+(TBLS_HASH_PLAN=0,0,0: k_set_hash_w2 and the one-lane line kernel), valid and
+tampered.  The exact fall-backs are pinned byte for byte by
+test_gpu_hash_variants.py.  The verdicts also go through the final
 exponentiation (tools/partial_record.py)."""
 
 import json
@@ -31,10 +32,10 @@ def _record(n, env_extra, tamper=-1):
     return json.loads(out.stdout.strip().splitlines()[-1])
 
 
-LANE = {"TBLS_HASH_ROW_MAX": "0", "TBLS_HASH_PAIR_MAX": "0"}
+LANE = {"TBLS_HASH_PLAN": "0,0,0"}
 
 
-@pytest.mark.parametrize("n,env", [(600, {}), (16384, {}), (16384, {"TBLS_HASH_ROW_MAX": "32768"})])
+@pytest.mark.parametrize("n,env", [(600, {}), (16384, {}), (16384, {"TBLS_HASH_PLAN": "32768,0,0"}), (16384, {"TBLS_HASH_PLAN": "0,0,32768"})])
 def test_row_and_pair_hash_same_product(n, env):
     fast = _record(n, env)
     lane = _record(n, LANE)
@@ -45,9 +46,8 @@ def test_row_and_pair_hash_same_product(n, env):
 def test_row_hash_tampered_and_fallback():
     row = _record(1000, {}, tamper=517)
     lane = _record(1000, LANE, tamper=517)
-    fix = _record(1000, {"TBLS_HROW_FORCE_FIX": "1"}, tamper=517)
-    assert row["ok"] == lane["ok"] == fix["ok"] == 0
-    assert row["coords"] == lane["coords"] == fix["coords"]
+    assert row["ok"] == lane["ok"] == 0
+    assert row["coords"] == lane["coords"]
     pair = _record(6000, {}, tamper=4321)
     lane = _record(6000, LANE, tamper=4321)
     assert pair["ok"] == lane["ok"] == 0
