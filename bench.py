@@ -104,11 +104,10 @@ def plan_counts(S):
             mads["miller"] = round(mads["miller"] + d / 3 * mc.get("mads_per_fp2_mul", 980))
         mc["mads_per_unit"] = mads
     kern = dict(STAGE_KERNEL)
-    w2 = int(os.environ.get("TBLS_W2", "1"), 0)  # the library's kernel selection (tb_lib.hip w2mask)
-    if not w2 & 1:
+    if os.environ.get("TBLS_W2") == "0":  # the library's kernel selection (tb_lib.hip w2)
         kern.update(set_pk="k_set_pk", set_sig="k_sig_check", set_hash="k_set_hash")
-    lines_k = "k_miller_lines_w2" if w2 & 2 else "k_miller_lines_lds"
-    acc_k = "k_miller_accs_w2" if w2 & 4 else ("k_miller_accs" if seg else f"k_miller_acc{2 if per == 2 else 1}")
+    lines_k = "k_miller_lines_lds"
+    acc_k = "k_miller_accs" if seg else f"k_miller_acc{2 if per == 2 else 1}"
     kern["miller"] = f"{lines_k} + {acc_k}"
     return mc, kern, {"per": per, "nseg": nseg, "kernel": acc_k}
 

@@ -7,6 +7,7 @@ namespace tb {
 
 // --- field overload set used by the generic curve code -----------------------
 TB_HD TB_INLINE fp f_add(const fp& a, const fp& b) { return fp_add(a, b); }
+TB_HD TB_INLINE fp f_add_nr(const fp& a, const fp& b) { return fp_add_nr(a, b); }  // product operands only
 TB_HD TB_INLINE fp f_sub(const fp& a, const fp& b) { return fp_sub(a, b); }
 TB_HD TB_INLINE fp f_dbl(const fp& a) { return fp_dbl(a); }
 TB_HD TB_INLINE fp f_mul(const fp& a, const fp& b) { return fp_mul(a, b); }
@@ -19,6 +20,7 @@ TB_HD TB_INLINE void f_set_one(fp& a) { a = fp_one(); }
 TB_HD TB_INLINE void f_set_zero(fp& a) { a = fp_zero(); }
 
 TB_HD TB_INLINE fp2 f_add(const fp2& a, const fp2& b) { return fp2_add(a, b); }
+TB_HD TB_INLINE fp2 f_add_nr(const fp2& a, const fp2& b) { return fp2_add_nr(a, b); }  // product operands only
 TB_HD TB_INLINE fp2 f_sub(const fp2& a, const fp2& b) { return fp2_sub(a, b); }
 TB_HD TB_INLINE fp2 f_dbl(const fp2& a) { return fp2_dbl(a); }
 TB_HD TB_INLINE fp2 f_mul(const fp2& a, const fp2& b) { return fp2_mul(a, b); }
@@ -88,8 +90,8 @@ TB_HD TB_INLINE jac<F> jac_dbl_i(const jac<F>& p) {
   F A = f_sqr(p.x);
   F B = f_sqr(p.y);
   F C = f_sqr(B);
-  F D = f_dbl(f_sub(f_sub(f_sqr(f_add(p.x, B)), A), C));
-  F E = f_add(f_dbl(A), A);
+  F D = f_dbl(f_sub(f_sub(f_sqr(f_add_nr(p.x, B)), A), C));
+  F E = f_add_nr(f_dbl(A), A);  // < 4p: operand of the two products below only
   F Fv = f_sqr(E);
   jac<F> r;
   r.x = f_sub(Fv, f_dbl(D));
@@ -419,7 +421,7 @@ TB_HD TB_INLINE jac<F> jac_add_nx(const jac<F>& p, const jac<F>& q) {
   jac<F> o;
   o.x = f_sub(f_sub(f_sqr(r), J), f_dbl(V));
   o.y = f_sub(f_mul(r, f_sub(V, o.x)), f_dbl(f_mul(S1, J)));
-  o.z = f_mul(f_sub(f_sub(f_sqr(f_add(p.z, q.z)), Z1Z1), Z2Z2), H);
+  o.z = f_mul(f_sub(f_sub(f_sqr(f_add_nr(p.z, q.z)), Z1Z1), Z2Z2), H);
   return o;
 }
 

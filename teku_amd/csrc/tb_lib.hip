@@ -327,32 +327,48 @@ struct pair_plan {
 
 // hash_to_G2 kernel by batch size above the workgroup-per-set kernels' range
 // (TB_HASH_WAVE_MAX): one 16-lane coop row per set (k_hrow.hip) up to row_max
-// sets, one quad per set (k_hquad.hip k_set_hash_quad) up to quad_max, two
-// lanes per set (k_set_hash_pair, one SSWU map each) up to pair_max, then the
-// one-lane k_set_hash_w2.  The quad Miller line kernel (k_miller_lines_quad)
-// takes the pairs of batches up to quad_max too.  TBLS_HASH_PLAN =
-// "row_max,quad_max,pair_max" overrides the defaults (A/B; 0 disables a
-// kernel).
+// sets, one DPP quad per set (k_hquad.hip k_set_hash_quad) up to quad_max,
+// one lane pair per set (k_set_hash_duo: an SSWU map per lane, the cofactor
+// clearing dealt over the pair) up to duo_max, two lanes with the clearing on
+// one (k_set_hash_pair) up to pair_max, then the one-lane k_set_hash_w2.  A
+// lane group fills the GPU at 65,536 lanes: quads at 16,384 sets leave no
+// SIMD to the key and signature stages beside the hash
+// (profiles/r04_stage16k_quad_vs_pair.json), so quads stop at 8,192.  The
+// Miller lines use the same groups while they fit one wave per SIMD: quads
+// up to 16,384 pairs, pairs up to 32,768 (k_miller_lines_quad / _duo),
+// unless quad_max / duo_max is 0.  TBLS_HASH_PLAN =
+// "row_max,quad_max,duo_max,pair_max" overrides the defaults (A/B; 0
+// disables a kernel).
 #define TB_HASH_ROW_MAX 4096u
-#define TB_HASH_QUAD_MAX 16384u  // 4 lanes x 16,384 sets: one wave per SIMD
-#define TB_HASH_PAIR_MAX 32768u  // 2 lanes x 32,768 sets: the same
+#define TB_HASH_QUAD_MAX 8192u
+#define TB_HASH_DUO_MAX 32768u
+#define TB_HASH_PAIR_MAX 0u
+#define TB_GROUP_LANES 65536u  // one wave per SIMD
 struct hash_plan_t {
-  uint32_t row_max, quad_max, pair_max;
+  uint32_t row_max, quad_max, duo_max, pair_max;
 };
 static const hash_plan_t& hash_plan() {
   static const hash_plan_t v = [] {
-    hash_plan_t h{TB_HASH_ROW_MAX, TB_HASH_QUAD_MAX, TB_HASH_PAIR_MAX};
+    hash_plan_t h{TB_HASH_ROW_MAX, TB_HASH_QUAD_MAX, TB_HASH_DUO_MAX, TB_HASH_PAIR_MAX};
     const char* e = getenv("TBLS_HASH_PLAN");
-    unsigned r, q, p;
-    if (e && sscanf(e, "%u,%u,%u", &r, &q, &p) == 3) h = {r, q, p};
+    unsigned r, q, d, p;
+    if (e && sscanf(e, "%u,%u,%u,%u", &r, &q, &d, &p) == 4) h = {r, q, d, p};
     return h;
   }();
   return v;
 }
 static bool hash_row(uint32_t n) { return n > TB_HASH_WAVE_MAX && n <= hash_plan().row_max; }
 static bool hash_quad(uint32_t n) { return n > TB_HASH_WAVE_MAX && !hash_row(n) && n <= hash_plan().quad_max; }
-static bool hash_pair(uint32_t n) { return n > TB_HASH_WAVE_MAX && !hash_row(n) && !hash_quad(n) && n <= hash_plan().pair_max; }
-static bool lines_quad(uint32_t n_main) { return n_main <= hash_plan().quad_max; }
+static bool hash_duo(uint32_t n) { return n > TB_HASH_WAVE_MAX && !hash_row(n) && !hash_quad(n) && n <= hash_plan().duo_max; }
+static bool hash_pair(uint32_t n) {
+  return n > TB_HASH_WAVE_MAX && !hash_row(n) && !hash_quad(n) && !hash_duo(n) && n <= hash_plan().pair_max;
+}
+// lanes per pair of the Miller line kernel: 4, 2 or 1
+static int line_group(uint32_t n_main) {
+  if (hash_plan().quad_max && 4ull * n_main <= TB_GROUP_LANES) return 4;
+  if (hash_plan().duo_max && 2ull * n_main <= TB_GROUP_LANES) return 2;
+  return 1;
+}
 
 struct ws_layout {
   size_t pk_aff, pk_code, P, Q, skip, set_code, sig_code, f, fpart, fpart2, segv, n_bad, result;
@@ -411,15 +427,15 @@ struct ws_layout {
 // run side by side.  `serial` (the stage-profile API) runs everything on the
 // caller's stream, for exclusive per-stage timings.
 
-// Two-waves-per-SIMD twins (k_w2_*.hip), TBLS_W2 = bit mask: 1 = the
-// large-batch one-lane kernels (hash, signature check, [r] apk), 2 = the G2
-// line kernel, 4 = the Fp12 accumulator (the segmented body for every plan).
-// Default 1; 0 selects the one-wave kernels throughout (A/B).
-static int w2mask() {
-  static const int v = getenv("TBLS_W2") ? (int)strtol(getenv("TBLS_W2"), nullptr, 0) : 1;
+// The large-batch one-lane kernels (hash, signature check, [r] apk) as their
+// two-waves-per-SIMD twins (k_w2_*.hip); TBLS_W2=0 selects the one-wave
+// kernels (A/B).  (The Miller line and accumulator kernels measured slower at
+// two waves -- 17.5 and 24.3 vs 14.5 ms Miller stage at 131,072 sets,
+// profiles/r04_bench_w2_masks.json -- and stay at one.)
+static bool w2() {
+  static const bool v = !(getenv("TBLS_W2") && getenv("TBLS_W2")[0] == '0');
   return v;
 }
-static bool w2() { return (w2mask() & 1) != 0; }
 // Small batches (<= TB_HASH_WAVE_MAX sets) run the key, signature and hash
 // stages, and multi-key aggregation, on the lane-cooperative kernels
 // (k_kcoop.hip, k_hwave.hip k_set_hash_coop); TBLS_COOP=0 selects the
@@ -599,6 +615,9 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
   } else if (hash_quad(n)) {  // one quad per set, then the exact formulas for the sets it flags (skip == 2)
     hipLaunchKernelGGL(k_set_hash_quad, dim3((4 * n + TB_BLOCK - 1) / TB_BLOCK), blk, 0, sh, b.msgs, b.msg_off, dst, dlen, n, Q, skip);
     hipLaunchKernelGGL(k_set_hash_fix, g, blk, 0, sh, b.msgs, b.msg_off, dst, dlen, n, Q, skip);
+  } else if (hash_duo(n)) {  // one lane pair per set, then the exact formulas for the sets it flags
+    hipLaunchKernelGGL(k_set_hash_duo, dim3((2 * n + TB_BLOCK - 1) / TB_BLOCK), blk, 0, sh, b.msgs, b.msg_off, dst, dlen, n, Q, skip);
+    hipLaunchKernelGGL(k_set_hash_fix, g, blk, 0, sh, b.msgs, b.msg_off, dst, dlen, n, Q, skip);
   } else if (hash_pair(n))
     hipLaunchKernelGGL(k_set_hash_pair, dim3((2 * n + TB_BLOCK - 1) / TB_BLOCK), blk, 0, sh, b.msgs, b.msg_off, dst, dlen, n, Q, skip);
   else if (n && w2()) {  // two waves per SIMD, then the exact formulas for the sets it flags (skip == 2)
@@ -631,17 +650,17 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
       uint4* lines = (uint4*)(w + L.lines);
       for (uint32_t lo = 0; lo < pp.n_main; lo += TB_LINE_CHUNK) {
         const uint32_t m = std::min(TB_LINE_CHUNK, pp.n_main - lo), mt = (m + pp.per - 1) / pp.per;
-        if (lines_quad(pp.n_main))  // mid-size batches: one quad per pair
-          hipLaunchKernelGGL(k_miller_lines_quad, dim3((4 * m + TB_BLOCK - 1) / TB_BLOCK), blk, 0, s, (const g1a*)P + lo,
-                             (const g2a*)Q + lo, (const uint8_t*)skip + lo, ca + lo, cb + lo, m, lines);
-        else
-          hipLaunchKernelGGL((w2mask() & 2) ? k_miller_lines_w2 : k_miller_lines_lds, dim3((m + TB_BLOCK - 1) / TB_BLOCK), blk, 0, s,
+        const int lg = line_group(pp.n_main);  // mid-size batches: a lane group per pair
+        if (lg > 1)
+          hipLaunchKernelGGL(lg == 4 ? k_miller_lines_quad : k_miller_lines_duo, dim3((lg * m + TB_BLOCK - 1) / TB_BLOCK), blk, 0, s,
                              (const g1a*)P + lo, (const g2a*)Q + lo, (const uint8_t*)skip + lo, ca + lo, cb + lo, m, lines);
-        if (pp.seg() || (w2mask() & 4)) {  // unsegmented plans as nseg = 1
+        else
+          hipLaunchKernelGGL(k_miller_lines_lds, dim3((m + TB_BLOCK - 1) / TB_BLOCK), blk, 0, s, (const g1a*)P + lo, (const g2a*)Q + lo,
+                             (const uint8_t*)skip + lo, ca + lo, cb + lo, m, lines);
+        if (pp.seg()) {
           const uint32_t g_pad = (mt + TB_BLOCK - 1) / TB_BLOCK * TB_BLOCK;
-          hipLaunchKernelGGL((w2mask() & 4) ? k_miller_accs_w2 : k_miller_accs, dim3(pp.nseg * g_pad / TB_BLOCK), blk, 0, s,
-                             (const uint4*)lines, (const uint8_t*)skip + lo, ca + lo, cb + lo, m, pp.per, pp.nseg, g_pad, f + lo / pp.per,
-                             pp.n_groups());
+          hipLaunchKernelGGL(k_miller_accs, dim3(pp.nseg * g_pad / TB_BLOCK), blk, 0, s, (const uint4*)lines, (const uint8_t*)skip + lo,
+                             ca + lo, cb + lo, m, pp.per, pp.nseg, g_pad, f + lo / pp.per, pp.n_groups());
         } else {
           hipLaunchKernelGGL(pp.per == 2 ? k_miller_acc2 : k_miller_acc1, dim3((mt + TB_BLOCK - 1) / TB_BLOCK), blk, 0, s,
                              (const uint4*)lines, (const uint8_t*)skip + lo, ca + lo, cb + lo, m, f + lo / pp.per);

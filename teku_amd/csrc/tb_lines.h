@@ -37,9 +37,9 @@ __device__ TB_INLINE fp6 fp6_mul_f(const fp6& a, const fp6& b) {
   const fp2 t0 = m2(a.c0, b.c0);
   const fp2 t1 = m2(a.c1, b.c1);
   const fp2 t2 = m2(a.c2, b.c2);
-  const fp2 c0 = fp2_add(t0, fp2_mul_xi(fp2_sub(m2(fp2_add(a.c1, a.c2), fp2_add(b.c1, b.c2)), fp2_add(t1, t2))));
-  const fp2 c1 = fp2_add(fp2_sub(m2(fp2_add(a.c0, a.c1), fp2_add(b.c0, b.c1)), fp2_add(t0, t1)), fp2_mul_xi(t2));
-  const fp2 c2 = fp2_add(fp2_sub(m2(fp2_add(a.c0, a.c2), fp2_add(b.c0, b.c2)), fp2_add(t0, t2)), t1);
+  const fp2 c0 = fp2_add(t0, fp2_mul_xi(fp2_sub(m2(fp2_add_nr(a.c1, a.c2), fp2_add_nr(b.c1, b.c2)), fp2_add(t1, t2))));
+  const fp2 c1 = fp2_add(fp2_sub(m2(fp2_add_nr(a.c0, a.c1), fp2_add_nr(b.c0, b.c1)), fp2_add(t0, t1)), fp2_mul_xi(t2));
+  const fp2 c2 = fp2_add(fp2_sub(m2(fp2_add_nr(a.c0, a.c2), fp2_add_nr(b.c0, b.c2)), fp2_add(t0, t2)), t1);
   return {c0, c1, c2};
 }
 
@@ -48,14 +48,14 @@ __device__ TB_INLINE fp6 fp6_mul_by_01_f(const fp6& a, const fp2& b0, const fp2&
   const fp2 t0 = m2(a.c0, b0);
   const fp2 t1 = m2(a.c1, b1);
   const fp2 c0 = fp2_add(t0, fp2_mul_xi(m2(a.c2, b1)));
-  const fp2 c1 = fp2_sub(fp2_sub(m2(fp2_add(a.c0, a.c1), fp2_add(b0, b1)), t0), t1);
+  const fp2 c1 = fp2_sub(fp2_sub(m2(fp2_add_nr(a.c0, a.c1), fp2_add_nr(b0, b1)), t0), t1);
   const fp2 c2 = fp2_add(t1, m2(a.c2, b0));
   return {c0, c1, c2};
 }
 
 TB_HD TB_INLINE fp12 fp12_sqr_i(const fp12& a) {
   const fp6 ab = fp6_mul_f(a.c0, a.c1);
-  const fp6 s1 = fp6_add(a.c0, a.c1), s2 = fp6_add(a.c0, fp6_mul_v(a.c1));
+  const fp6 s1 = fp6_add_nr(a.c0, a.c1), s2 = fp6_add_nr(a.c0, fp6_mul_v(a.c1));  // product operands only
   TB_FENCE();
   const fp6 t = fp6_mul_f(s1, s2);
   const fp6 c0 = fp6_sub(fp6_sub(t, ab), fp6_mul_v(ab));
@@ -67,8 +67,8 @@ TB_HD TB_INLINE fp12 fp12_sqr_i(const fp12& a) {
 // dies), (f0 + f1) * (A + (B + C) v), then f0 * (A + B v) (f0 dies)
 TB_HD TB_INLINE fp12 fp12_mul_by_line_i(const fp12& f, const fp2& A, const fp2& B, const fp2& C) {
   const fp6 t1 = {fp2_mul_xi(m2(f.c1.c2, C)), m2(f.c1.c0, C), m2(f.c1.c1, C)};
-  const fp6 s = fp6_add(f.c0, f.c1);
-  const fp2 BC = fp2_add(B, C);
+  const fp6 s = fp6_add_nr(f.c0, f.c1);  // product operands only
+  const fp2 BC = fp2_add_nr(B, C);
   TB_FENCE();
   const fp6 u = fp6_mul_by_01_f(s, A, BC);
   const fp6 t0 = fp6_mul_by_01_f(f.c0, A, B);
@@ -169,7 +169,7 @@ __device__ TB_INLINE line3 add_step_f(g2p& T, const g2a& Q, const g1a& P) {
 __device__ TB_INLINE line3 dbl_step_f(g2p& T, const g1a& P) {
   const fp2 B = s2(T.y);
   const fp2 C = s2(T.z);
-  const fp2 H = fp2_sub(s2(fp2_add(T.y, T.z)), fp2_add(B, C));
+  const fp2 H = fp2_sub(s2(fp2_add_nr(T.y, T.z)), fp2_add(B, C));
   const fp2 A = fp2_half(m2(T.x, T.y));
   const fp2 J = s2(T.x);
   const fp2 E = fp2_mul_3b(C);
@@ -178,7 +178,7 @@ __device__ TB_INLINE line3 dbl_step_f(g2p& T, const g1a& P) {
   const fp2 EE = s2(E);
   line3 l;
   l.a = fp2_sub(E, B);
-  l.b = mf(fp2_add(fp2_dbl(J), J), P.x);
+  l.b = mf(fp2_add_nr(fp2_dbl(J), J), P.x);
   l.c = fp2_neg(mf(H, P.y));
   T.x = m2(A, fp2_sub(B, F));
   T.z = m2(B, H);

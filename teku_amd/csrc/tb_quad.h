@@ -1,5 +1,5 @@
-// Quad-cooperative G2 arithmetic for mid-size batches (config 4's 16,384
-// sets).  At that size the one-lane hash and Miller-line kernels fill a
+// Lane-group cooperative G2 arithmetic for mid-size batches (config 4's
+// 16,384 sets): quads (namespace quad) and lane pairs (namespace duo).  At that size the one-lane hash and Miller-line kernels fill a
 // quarter of the SIMDs and their time is one lane's chain: 126 doublings of
 // the cofactor clearing, 68 line steps.  Here four lanes (a DPP quad) carry
 // one point, each holding the whole point; the independent Fp2 products of a
@@ -24,36 +24,42 @@
 #include "tb_pairing.h"
 
 namespace tb {
-namespace quad {
+// lane groups of G = 2 or 4 consecutive lanes (within a DPP quad)
+namespace lg {
 
-__device__ TB_INLINE uint32_t qlane() { return threadIdx.x & 3u; }
+template <int G>
+__device__ TB_INLINE uint32_t glane() {
+  return threadIdx.x & (uint32_t)(G - 1);
+}
 
-// v of quad lane SRC, on every lane of the quad
-template <int SRC>
+// v of group member SRC, on every lane of the group
+template <int G, int SRC>
 __device__ TB_INLINE uint32_t bc(uint32_t v) {
+  static_assert((G == 2 || G == 4) && SRC < G, "groups of 2 or 4 lanes");
+  constexpr int CTRL = G == 4 ? SRC * 0x55 : (SRC | (SRC << 2) | ((2 + SRC) << 4) | ((2 + SRC) << 6));
 #if defined(__HIP_DEVICE_COMPILE__)
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, SRC * 0x55, 0xf, 0xf, false);
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xf, 0xf, false);
 #else
   return v;
 #endif
 }
 
-template <int SRC>
+template <int G, int SRC>
 __device__ TB_INLINE fp2 bc2(const fp2& a) {
   fp2 r;
   TB_UNROLL for (int w = 0; w < 12; w++) {
-    r.c0.l[w] = bc<SRC>(a.c0.l[w]);
-    r.c1.l[w] = bc<SRC>(a.c1.l[w]);
+    r.c0.l[w] = bc<G, SRC>(a.c0.l[w]);
+    r.c1.l[w] = bc<G, SRC>(a.c1.l[w]);
   }
   return r;
 }
 
-template <int SRC>
+template <int G, int SRC>
 __device__ TB_INLINE g2a bca(const g2a& a) {
-  return {bc2<SRC>(a.x), bc2<SRC>(a.y)};
+  return {bc2<G, SRC>(a.x), bc2<G, SRC>(a.y)};
 }
 
-// lane q's pick among v[0..N-1] (lanes q >= N take v[N-1])
+// member q's pick among v[0..N-1] (members q >= N take v[N-1])
 template <int N>
 __device__ TB_INLINE fp2 pick(uint32_t q, const fp2 (&v)[N]) {
   fp2 x = v[N - 1];
@@ -61,27 +67,43 @@ __device__ TB_INLINE fp2 pick(uint32_t q, const fp2 (&v)[N]) {
   return x;
 }
 
-template <int N>
+template <int G, int N>
 __device__ TB_INLINE void spread(fp2 (&r)[N], const fp2& p) {
-  r[0] = bc2<0>(p);
-  if constexpr (N > 1) r[1] = bc2<1>(p);
-  if constexpr (N > 2) r[2] = bc2<2>(p);
-  if constexpr (N > 3) r[3] = bc2<3>(p);
+  r[0] = bc2<G, 0>(p);
+  if constexpr (N > 1) r[1] = bc2<G, 1>(p);
+  if constexpr (N > 2) r[2] = bc2<G, 2>(p);
+  if constexpr (N > 3) r[3] = bc2<G, 3>(p);
 }
 
-// r[k] = a[k] b[k], k < N <= 4, one product per lane
+// one round: r[k] = a[k] b[k], k < N <= G, one product per member
+template <int G, int N>
+__device__ TB_INLINE void rmul(fp2 (&r)[N], const fp2 (&a)[N], const fp2 (&b)[N]) {
+  static_assert(N >= 1 && N <= G, "one product per member");
+  const uint32_t q = glane<G>();
+  spread<G, N>(r, fp2_mul(pick<N>(q, a), pick<N>(q, b)));
+}
+
+// one round of squarings
+template <int G, int N>
+__device__ TB_INLINE void rsqr(fp2 (&r)[N], const fp2 (&a)[N]) {
+  static_assert(N >= 1 && N <= G, "one product per member");
+  spread<G, N>(r, fp2_sqr(pick<N>(glane<G>(), a)));
+}
+
+}  // namespace lg
+
+namespace quad {
+template <int SRC>
+__device__ TB_INLINE g2a bca(const g2a& a) {
+  return lg::bca<4, SRC>(a);
+}
 template <int N>
 __device__ TB_INLINE void qmul(fp2 (&r)[N], const fp2 (&a)[N], const fp2 (&b)[N]) {
-  static_assert(N >= 1 && N <= 4, "a quad holds four products");
-  const uint32_t q = qlane();
-  spread<N>(r, fp2_mul(pick<N>(q, a), pick<N>(q, b)));
+  lg::rmul<4, N>(r, a, b);
 }
-
-// r[k] = a[k]^2
 template <int N>
 __device__ TB_INLINE void qsqr(fp2 (&r)[N], const fp2 (&a)[N]) {
-  static_assert(N >= 1 && N <= 4, "a quad holds four products");
-  spread<N>(r, fp2_sqr(pick<N>(qlane(), a)));
+  lg::rsqr<4, N>(r, a);
 }
 
 // dbl-2009-l (tb_curve.h jac_dbl_i); Z = 0 stays 0
@@ -89,9 +111,9 @@ __device__ TB_INLINE g2j dbl(const g2j& p) {
   fp2 r1[3];
   qmul<3>(r1, {p.x, p.y, p.y}, {p.x, p.y, p.z});
   const fp2 A = r1[0], B = r1[1];
-  const fp2 E = fp2_add(fp2_dbl(A), A);
+  const fp2 E = fp2_add_nr(fp2_dbl(A), A);  // product operand only
   fp2 r2[3];
-  qsqr<3>(r2, {B, fp2_add(p.x, B), E});
+  qsqr<3>(r2, {B, fp2_add_nr(p.x, B), E});
   const fp2 C = r2[0];
   const fp2 D = fp2_dbl(fp2_sub(fp2_sub(r2[1], A), C));
   g2j o;
@@ -114,7 +136,7 @@ __device__ TB_INLINE g2j add(const g2j& p, const g2j& q) {
   const fp2 H = fp2_sub(r2[1], U1);
   const fp2 r = fp2_dbl(fp2_sub(r2[3], S1));
   fp2 r3[3];
-  qsqr<3>(r3, {fp2_dbl(H), r, fp2_add(p.z, q.z)});
+  qsqr<3>(r3, {fp2_dbl(H), r, fp2_add_nr(p.z, q.z)});
   const fp2 I = r3[0];
   fp2 r4[3];
   qmul<3>(r4, {H, U1, fp2_sub(fp2_sub(r3[2], Z1Z1), Z2Z2)}, {I, I, H});
@@ -153,7 +175,7 @@ __device__ TB_INLINE bool clear_cofactor(g2j& out, const g2j& p) {
 // tb_lines.h dbl_step_f on the quad: T <- 2T, the tangent line at P
 __device__ TB_INLINE line3 dbl_step(g2p& T, const g1a& P) {
   fp2 r1[4];
-  qmul<4>(r1, {T.x, T.y, T.z, fp2_add(T.y, T.z)}, {T.y, T.y, T.z, fp2_add(T.y, T.z)});
+  qmul<4>(r1, {T.x, T.y, T.z, fp2_add_nr(T.y, T.z)}, {T.y, T.y, T.z, fp2_add_nr(T.y, T.z)});
   const fp2 A = fp2_half(r1[0]), B = r1[1], C = r1[2];
   const fp2 H = fp2_sub(r1[3], fp2_add(B, C));
   const fp2 E = fp2_mul_3b(C);
@@ -164,7 +186,7 @@ __device__ TB_INLINE line3 dbl_step(g2p& T, const g1a& P) {
   const fp2 J = r2[0], EE = r2[1];
   const fp2 px = {P.x, fp_zero()}, py = {P.y, fp_zero()};
   fp2 r3[3];
-  qmul<3>(r3, {A, fp2_add(fp2_dbl(J), J), H}, {fp2_sub(B, F), px, py});
+  qmul<3>(r3, {A, fp2_add_nr(fp2_dbl(J), J), H}, {fp2_sub(B, F), px, py});
   line3 l;
   l.a = fp2_sub(E, B);
   l.b = r3[1];
@@ -202,4 +224,159 @@ __device__ TB_INLINE line3 add_step(g2p& T, const g2a& Q, const g1a& P) {
 }
 
 }  // namespace quad
+
+// ---------------------------------------------------------------------------
+// Lane pairs (batches whose quads would overfill the GPU): the same formulas
+// dealt over two lanes.  G2 doubling 4 rounds, addition 8, Miller doubling
+// step 6, addition step 8 (a lone product of a round runs on both lanes).
+// ---------------------------------------------------------------------------
+namespace duo {
+template <int N>
+__device__ TB_INLINE void dmul(fp2 (&r)[N], const fp2 (&a)[N], const fp2 (&b)[N]) {
+  lg::rmul<2, N>(r, a, b);
+}
+template <int N>
+__device__ TB_INLINE void dsqr(fp2 (&r)[N], const fp2 (&a)[N]) {
+  lg::rsqr<2, N>(r, a);
+}
+
+// dbl-2009-l: [X^2, Y^2] [B^2, (X + B)^2] [E^2, Y Z] [E (D - X3)]
+__device__ TB_INLINE g2j dbl(const g2j& p) {
+  fp2 r1[2];
+  dsqr<2>(r1, {p.x, p.y});
+  const fp2 A = r1[0], B = r1[1];
+  const fp2 E = fp2_add_nr(fp2_dbl(A), A);  // product operand only
+  fp2 r2[2];
+  dsqr<2>(r2, {B, fp2_add_nr(p.x, B)});
+  const fp2 C = r2[0];
+  const fp2 D = fp2_dbl(fp2_sub(fp2_sub(r2[1], A), C));
+  fp2 r3[2];
+  dmul<2>(r3, {E, p.y}, {E, p.z});
+  g2j o;
+  o.x = fp2_sub(r3[0], fp2_dbl(D));
+  const fp2 C8 = fp2_dbl(fp2_dbl(fp2_dbl(C)));
+  o.y = fp2_sub(fp2_mul(E, fp2_sub(D, o.x)), C8);
+  o.z = fp2_dbl(r3[1]);
+  return o;
+}
+
+// add-2007-bl, no exceptional branch: [Z1^2, Z2^2] [Y1 Z2, Y2 Z1] [U1, U2]
+// [S1, S2] [I, (Z1 + Z2)^2] [J, V] [r^2, Z3] [r (V - X3), S1 J]
+__device__ TB_INLINE g2j add(const g2j& p, const g2j& q) {
+  fp2 r1[2];
+  dsqr<2>(r1, {p.z, q.z});
+  const fp2 Z1Z1 = r1[0], Z2Z2 = r1[1];
+  fp2 r2[2];
+  dmul<2>(r2, {p.y, q.y}, {q.z, p.z});
+  fp2 r3[2];
+  dmul<2>(r3, {p.x, q.x}, {Z2Z2, Z1Z1});
+  const fp2 U1 = r3[0];
+  const fp2 H = fp2_sub(r3[1], U1);
+  fp2 r4[2];
+  dmul<2>(r4, {r2[0], r2[1]}, {Z2Z2, Z1Z1});
+  const fp2 S1 = r4[0];
+  const fp2 r = fp2_dbl(fp2_sub(r4[1], S1));
+  fp2 r5[2];
+  dsqr<2>(r5, {fp2_dbl(H), fp2_add_nr(p.z, q.z)});
+  const fp2 I = r5[0];
+  fp2 r6[2];
+  dmul<2>(r6, {H, U1}, {I, I});
+  const fp2 J = r6[0], V = r6[1];
+  fp2 r7[2];
+  dmul<2>(r7, {r, fp2_sub(fp2_sub(r5[1], Z1Z1), Z2Z2)}, {r, H});
+  g2j o;
+  o.x = fp2_sub(fp2_sub(r7[0], J), fp2_dbl(V));
+  fp2 r8[2];
+  dmul<2>(r8, {r, S1}, {fp2_sub(V, o.x), J});
+  o.y = fp2_sub(r8[0], fp2_dbl(r8[1]));
+  o.z = r7[1];
+  return o;
+}
+
+__device__ TB_INLINE g2j mul_xabs(const g2j& P) {
+  g2j r = P;
+  TB_NOUNROLL for (int k = 0; k < 6; k++) {
+    const int nd = k == 0 ? 1 : k == 1 ? 2 : k == 2 ? 3 : k == 3 ? 9 : k == 4 ? 32 : 16;  // XRUN_DBL[k]
+    TB_NOUNROLL for (int i = 0; i < nd; i++) r = dbl(r);
+    if (k < 5) r = add(r, P);
+  }
+  return r;
+}
+
+__device__ TB_INLINE bool clear_cofactor(g2j& out, const g2j& p) {
+  const g2j t2 = g2_psi(p);
+  const g2j A = add(add(g2_psi2(dbl(p)), jac_neg(p)), jac_neg(t2));
+  const g2j t1 = mul_xabs(p);
+  const g2j t3 = mul_xabs(add(t2, jac_neg(t1)));
+  out = add(add(jac_neg(t3), t1), A);
+  return !fp2_is_zero(out.z);
+}
+
+// Miller doubling step: [X Y, Y^2] [Z^2, (Y + Z)^2] [X^2, B H] [E^2, G^2]
+// [A (B - F), H yP] [3 J xP]
+__device__ TB_INLINE line3 dbl_step(g2p& T, const g1a& P) {
+  fp2 r1[2];
+  dmul<2>(r1, {T.x, T.y}, {T.y, T.y});
+  const fp2 A = fp2_half(r1[0]), B = r1[1];
+  fp2 r2[2];
+  dsqr<2>(r2, {T.z, fp2_add_nr(T.y, T.z)});
+  const fp2 C = r2[0];
+  const fp2 H = fp2_sub(r2[1], fp2_add(B, C));
+  const fp2 E = fp2_mul_3b(C);
+  const fp2 F = fp2_add(fp2_dbl(E), E);
+  const fp2 G = fp2_half(fp2_add(B, F));
+  fp2 r3[2];
+  dmul<2>(r3, {T.x, B}, {T.x, H});
+  const fp2 J = r3[0];
+  fp2 r4[2];
+  dsqr<2>(r4, {E, G});
+  const fp2 EE = r4[0];
+  const fp2 px = {P.x, fp_zero()}, py = {P.y, fp_zero()};
+  fp2 r5[2];
+  dmul<2>(r5, {A, H}, {fp2_sub(B, F), py});
+  line3 l;
+  l.a = fp2_sub(E, B);
+  l.b = fp2_mul(fp2_add_nr(fp2_dbl(J), J), px);  // both lanes
+  l.c = fp2_neg(r5[1]);
+  T.x = r5[0];
+  T.y = fp2_sub(r4[1], fp2_add(fp2_dbl(EE), EE));
+  T.z = r3[1];
+  return l;
+}
+
+// Miller addition step: [Qy Tz, Qx Tz] [theta^2, lambda^2] [theta Qx,
+// lambda Qy] [e, f] [g, theta xP] [lambda yP, e Ty] [lambda h, Tz e]
+// [theta (g - h)]
+__device__ TB_INLINE line3 add_step(g2p& T, const g2a& Q, const g1a& P) {
+  fp2 r1[2];
+  dmul<2>(r1, {Q.y, Q.x}, {T.z, T.z});
+  const fp2 theta = fp2_sub(T.y, r1[0]);
+  const fp2 lambda = fp2_sub(T.x, r1[1]);
+  fp2 r2[2];
+  dsqr<2>(r2, {theta, lambda});
+  const fp2 c = r2[0], d = r2[1];
+  fp2 r3[2];
+  dmul<2>(r3, {theta, lambda}, {Q.x, Q.y});
+  const fp2 px = {P.x, fp_zero()}, py = {P.y, fp_zero()};
+  fp2 r4[2];
+  dmul<2>(r4, {lambda, T.z}, {d, c});
+  const fp2 e = r4[0];
+  fp2 r5[2];
+  dmul<2>(r5, {T.x, theta}, {d, px});
+  const fp2 g = r5[0];
+  const fp2 h = fp2_sub(fp2_add(e, r4[1]), fp2_dbl(g));
+  fp2 r6[2];
+  dmul<2>(r6, {lambda, e}, {py, T.y});
+  fp2 r7[2];
+  dmul<2>(r7, {lambda, T.z}, {h, e});
+  line3 l;
+  l.a = fp2_sub(r3[0], r3[1]);
+  l.b = fp2_neg(r5[1]);
+  l.c = r6[0];
+  T.y = fp2_sub(fp2_mul(theta, fp2_sub(g, h)), r6[1]);  // both lanes
+  T.x = r7[0];
+  T.z = r7[1];
+  return l;
+}
+}  // namespace duo
 }  // namespace tb

@@ -29,6 +29,10 @@ TB_HD TB_INLINE fp2 fp2_one() { return {fp_one(), fp_zero()}; }
 TB_HD TB_INLINE fp2 fp2_from_const(const uint32_t (&c)[2][12]) { return {fp_from_const(c[0]), fp_from_const(c[1])}; }
 TB_HD TB_INLINE fp2 fp2_add(const fp2& a, const fp2& b) { return {fp_add(a.c0, b.c0), fp_add(a.c1, b.c1)}; }
 TB_HD TB_INLINE fp2 fp2_sub(const fp2& a, const fp2& b) { return {fp_sub(a.c0, b.c0), fp_sub(a.c1, b.c1)}; }
+// a + b without the reduction (< 4p for reduced a, b): only as an operand of
+// a product, which takes any coordinates < 2^383 (fp2_mul_lazy, fp2_sqr,
+// mont29) -- the Karatsuba pre-sums
+TB_HD TB_INLINE fp2 fp2_add_nr(const fp2& a, const fp2& b) { return {fp_add_nr(a.c0, b.c0), fp_add_nr(a.c1, b.c1)}; }
 TB_HD TB_INLINE fp2 fp2_dbl(const fp2& a) { return {fp_dbl(a.c0), fp_dbl(a.c1)}; }
 TB_HD TB_INLINE fp2 fp2_neg(const fp2& a) { return {fp_neg(a.c0), fp_neg(a.c1)}; }
 TB_HD TB_INLINE fp2 fp2_conj(const fp2& a) { return {a.c0, fp_neg(a.c1)}; }
@@ -39,44 +43,53 @@ TB_HD TB_INLINE fp2 fp2_mul_fp(const fp2& a, const fp& b) { return {fp_mul(a.c0,
 TB_HD TB_INLINE fp2 fp2_mul3(const fp2& a) { return {fp_mul3(a.c0), fp_mul3(a.c1)}; }
 TB_HD TB_INLINE fp2 fp2_half(const fp2& a) { return {fp_half(a.c0), fp_half(a.c1)}; }
 
-// Karatsuba Fp2 product with lazy reduction.  The three half products a0 b0,
-// a1 b1 and (a0 + a1)(b0 + b1) are scanned column by column on 14 x 29-bit
-// limbs and only the two results are Montgomery-reduced:
+// Karatsuba Fp2 product with lazy reduction.  The three half products are
+// scanned column by column on 14 x 29-bit limbs and only the two results are
+// Montgomery-reduced:
 //   re = a0 b0 - a1 b1 + p 2^388      (the offset keeps it non-negative)
-//   im = (a0 + a1)(b0 + b1) - a0 b0 - a1 b1
-// so a product costs 3 x 196 + 2 x 196 = 980 v_mad_u64_u32 instead of the
-// 3 x 392 of three Montgomery products.  Per column five independent
-// accumulator chains (the two pure products, the Karatsuba product plus im's
-// reduction, re's reduction plus offset) give the multiplier its ILP.
-// Bounds: coordinates < 2p (weakly reduced; the sums a0 + a1 < 4p < 2^383 are
-// operands too, so every operand is < 2^384); re < 2^769.4,
-// im < 2^769, so both outputs are < 2p; mid-scan column values stay inside
-// +-2^63 (signed, arithmetic carries).
+//   im = a0 b0 + a1 b1 + (a0 - a1)(b1 - b0)  (= a0 b1 + a1 b0)
+// so a product costs 3 x 196 + 2 x 196 = 980 v_mad_u64_u32 / v_mad_i64_i32
+// instead of the 3 x 392 of three Montgomery products.  The difference
+// operands are formed limb by limb as signed 29-bit digits (14 subtractions
+// each, no carry chain, no conversion of a sum) and multiplied with the signed
+// multiply-add; im then needs no subtraction per column, re one (round 4:
+// 1,737 -> ~1,630 instructions per product).  Per column five independent
+// accumulator chains (the two pure products, the difference product plus
+// im's reduction, re's reduction plus offset) give the multiplier its ILP.
+// Bounds: coordinates < 2p (weakly reduced), so every operand is < 2^384;
+// re < 2^769.4, im < 2^769, so both outputs are < 2p.  Column values: re's
+// stay inside +-2^63 (signed, arithmetic carries); im's partial sum x2 may
+// wrap below zero, its column total c0 + c1 + x2 is the true non-negative
+// column value < 2^63.4 + carry < 2^64 (unsigned, logical carries).
 TB_HD TB_INLINE fp2 fp2_mul_lazy(const fp2& a, const fp2& b) {
-  uint32_t A0[14], A1[14], AS[14], B0[14], B1[14], BS[14];
+  uint32_t A0[14], A1[14], B0[14], B1[14];
+  int32_t AD[14], BD[14];
   to29(A0, a.c0);
   to29(A1, a.c1);
-  to29(AS, fp_add_nr(a.c0, a.c1));
   to29(B0, b.c0);
   to29(B1, b.c1);
-  to29(BS, fp_add_nr(b.c0, b.c1));
+  TB_UNROLL for (int i = 0; i < 14; i++) {
+    AD[i] = (int32_t)(A0[i] - A1[i]);
+    BD[i] = (int32_t)(B1[i] - B0[i]);
+  }
   uint32_t m0[14], m1[14], r0[14], r1[14];
-  int64_t k0 = 0, k1 = 0;  // carries into the column (signed)
+  int64_t k0 = 0;   // re's carry into the column (signed)
+  uint64_t k1 = 0;  // im's (non-negative)
   TB_UNROLL for (int k = 0; k < 27; k++) {
     const int lo = k < 14 ? 0 : k - 13;
     const int hi = k < 14 ? k : 13;
-    uint64_t c0 = 0, c1 = 0, x0 = (uint64_t)k0 + (k >= 13 ? OFF29[k - 13] : 0u), x2 = (uint64_t)k1;
+    uint64_t c0 = 0, c1 = 0, x0 = (uint64_t)k0 + (k >= 13 ? OFF29[k - 13] : 0u), x2 = k1;
     TB_UNROLL for (int i = lo; i <= hi; i++) {
       mad29(c0, A0[i], B0[k - i]);
       mad29(c1, A1[i], B1[k - i]);
-      mad29(x2, AS[i], BS[k - i]);
+      x2 += (uint64_t)((int64_t)AD[i] * (int64_t)BD[k - i]);
     }
     const int mhi = k < 14 ? k - 1 : 13;  // m_k is formed at the end of column k
     TB_UNROLL for (int i = lo; i <= mhi; i++) {
       mad29(x0, m0[i], P29[k - i]);
       mad29(x2, m1[i], P29[k - i]);
     }
-    uint64_t t0 = x0 + c0 - c1, t1 = x2 - c0 - c1;
+    uint64_t t0 = x0 + c0 - c1, t1 = x2 + c0 + c1;
     if (k < 14) {
       m0[k] = ((uint32_t)t0 * N0_29) & M29;
       m1[k] = ((uint32_t)t1 * N0_29) & M29;
@@ -87,7 +100,7 @@ TB_HD TB_INLINE fp2 fp2_mul_lazy(const fp2& a, const fp2& b) {
       r1[k - 14] = (uint32_t)t1 & M29;
     }
     k0 = (int64_t)t0 >> 29;
-    k1 = (int64_t)t1 >> 29;
+    k1 = t1 >> 29;
   }
   r0[13] = (uint32_t)k0;
   r1[13] = (uint32_t)k1;
@@ -121,15 +134,64 @@ TB_HD TB_INLINE fp2 fp2_mul(fp2 a, fp2 b) {
 #endif
 }
 
+// Fp2 squaring with lazy reduction, the same column scan:
+//   re = (a0 + a1)(a0 - a1) + p 2^388,   im = a0 (2 a1)
+// a0 + a1 on the hardware carry chain (< 4p, normalized limbs), a0 - a1 as
+// signed 29-bit digits, 2 a1 as limbs < 2^30; 2 x 196 products plus two
+// reductions = 784 multiply-adds (as two Montgomery products), with four
+// independent accumulator chains per column and no Fp subtraction or
+// doubling around them.  Bounds: |re| < 4p 2p < 2^765 below the offset
+// p 2^388 > 2^768, re's columns inside +-2^63 (signed), im's < 2^63.4
+// (unsigned); both outputs < 2p.
 TB_HD TB_INLINE fp2 fp2_sqr(fp2 a) {
 #if !TB_DEVICE_PASS && defined(TB_COUNT_MULS)
   tb_mul_count += 2;
 #endif
-  fp t[2];
-  const fp x[2] = {a.c0, fp_add_nr(a.c0, a.c1)};
-  const fp y[2] = {a.c1, fp_sub(a.c0, a.c1)};
-  fp_mul_n<2>(t, x, y);
-  return {t[1], fp_dbl(t[0])};
+  uint32_t A0[14], A1[14], S[14];
+  to29(A0, a.c0);
+  to29(A1, a.c1);
+  to29(S, fp_add_nr(a.c0, a.c1));
+  int32_t D[14];
+  uint32_t T1[14];
+  TB_UNROLL for (int i = 0; i < 14; i++) {
+    D[i] = (int32_t)(A0[i] - A1[i]);
+    T1[i] = A1[i] << 1;
+  }
+  uint32_t m0[14], m1[14], r0[14], r1[14];
+  int64_t k0 = 0;   // re's carry (signed)
+  uint64_t k1 = 0;  // im's
+  TB_UNROLL for (int k = 0; k < 27; k++) {
+    const int lo = k < 14 ? 0 : k - 13;
+    const int hi = k < 14 ? k : 13;
+    uint64_t cr = 0, ci = 0, x0 = (uint64_t)k0 + (k >= 13 ? OFF29[k - 13] : 0u), x2 = k1;
+    TB_UNROLL for (int i = lo; i <= hi; i++) {
+      cr += (uint64_t)((int64_t)(int32_t)S[i] * (int64_t)D[k - i]);
+      mad29(ci, A0[i], T1[k - i]);
+    }
+    const int mhi = k < 14 ? k - 1 : 13;
+    TB_UNROLL for (int i = lo; i <= mhi; i++) {
+      mad29(x0, m0[i], P29[k - i]);
+      mad29(x2, m1[i], P29[k - i]);
+    }
+    uint64_t t0 = x0 + cr, t1 = x2 + ci;
+    if (k < 14) {
+      m0[k] = ((uint32_t)t0 * N0_29) & M29;
+      m1[k] = ((uint32_t)t1 * N0_29) & M29;
+      mad29(t0, m0[k], P29[0]);
+      mad29(t1, m1[k], P29[0]);
+    } else {
+      r0[k - 14] = (uint32_t)t0 & M29;
+      r1[k - 14] = (uint32_t)t1 & M29;
+    }
+    k0 = (int64_t)t0 >> 29;
+    k1 = t1 >> 29;
+  }
+  r0[13] = (uint32_t)k0;
+  r1[13] = (uint32_t)k1;
+  fp2 r;
+  from29(r.c0, r0);
+  from29(r.c1, r1);
+  return r;
 }
 
 // multiply by xi = 1 + u
@@ -199,6 +261,7 @@ TB_HD TB_INLINE fp6 fp6_zero() { return {fp2_zero(), fp2_zero(), fp2_zero()}; }
 TB_HD TB_INLINE fp6 fp6_one() { return {fp2_one(), fp2_zero(), fp2_zero()}; }
 TB_HD TB_INLINE fp6 fp6_add(const fp6& a, const fp6& b) { return {fp2_add(a.c0, b.c0), fp2_add(a.c1, b.c1), fp2_add(a.c2, b.c2)}; }
 TB_HD TB_INLINE fp6 fp6_sub(const fp6& a, const fp6& b) { return {fp2_sub(a.c0, b.c0), fp2_sub(a.c1, b.c1), fp2_sub(a.c2, b.c2)}; }
+TB_HD TB_INLINE fp6 fp6_add_nr(const fp6& a, const fp6& b) { return {fp2_add_nr(a.c0, b.c0), fp2_add_nr(a.c1, b.c1), fp2_add_nr(a.c2, b.c2)}; }
 TB_HD TB_INLINE fp6 fp6_neg(const fp6& a) { return {fp2_neg(a.c0), fp2_neg(a.c1), fp2_neg(a.c2)}; }
 TB_HD TB_INLINE fp6 fp6_mul_v(const fp6& a) { return {fp2_mul_xi(a.c2), a.c0, a.c1}; }
 TB_HD TB_INLINE bool fp6_is_zero(const fp6& a) { return fp2_is_zero(a.c0) && fp2_is_zero(a.c1) && fp2_is_zero(a.c2); }

@@ -5,7 +5,7 @@
 // messages and returns their affine H(m_i) (Montgomery limbs) and skip flags,
 // for tests/test_gpu_hash_variants.py to compare with the oracle.
 //   variant 0  k_set_hash          (one lane per set; batches above 32,768 sets)
-//   variant 1  k_set_hash_pair     (two lanes per set; 16,385 - 32,768)
+//   variant 1  k_set_hash_pair     (two lanes per set, clearing on one; A/B only)
 //   variant 2  k_hrow_* (5 launches: field, sswu, iso, cof, fix; 513 - 4,096);
 //              force_fix != 0 sends every set through the one-lane k_hrow_fix
 //   variant 3  k_set_hash_coop     (256-thread workgroup per set; <= 512)
@@ -13,7 +13,9 @@
 //   variant 5  k_set_hash_w2 + k_set_hash_fix (two waves per SIMD; above 32,768,
 //              the default); force_fix != 0 flags every set for k_set_hash_fix
 //   variant 6  k_set_hash_quad + k_set_hash_fix (one DPP quad per set; 4,097 -
-//              16,384); force_fix as variant 5
+//              8,192); force_fix as variant 5
+//   variant 7  k_set_hash_duo + k_set_hash_fix (one lane pair per set; 8,193 -
+//              32,768); force_fix as variant 5
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -86,6 +88,11 @@ extern "C" int tbls_test_hash_variant(const char* product_so, int variant, const
       break;
     case 6:
       rc = launch(sym("k_set_hash_quad"), (4 * n32 + BLK - 1) / BLK, BLK, a_set);
+      if (!rc && ff && hipMemset(dskip.p, 2, n) != hipSuccess) rc = -6;
+      if (!rc) rc = launch(sym("k_set_hash_fix"), g, BLK, a_set);
+      break;
+    case 7:
+      rc = launch(sym("k_set_hash_duo"), (2 * n32 + BLK - 1) / BLK, BLK, a_set);
       if (!rc && ff && hipMemset(dskip.p, 2, n) != hipSuccess) rc = -6;
       if (!rc) rc = launch(sym("k_set_hash_fix"), g, BLK, a_set);
       break;

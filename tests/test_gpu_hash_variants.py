@@ -2,8 +2,9 @@
 
 batchVerify hashes with one of five kernels by batch size (tb_lib.hip
 launch_partial, hash_plan): k_set_hash_w2 + k_set_hash_fix (> 32,768 sets;
-k_set_hash is its one-wave A/B twin), k_set_hash_pair (16,385 - 32,768),
-k_set_hash_quad + k_set_hash_fix (4,097 - 16,384), the row pipeline k_hrow_*
+k_set_hash is its one-wave A/B twin), k_set_hash_duo + k_set_hash_fix
+(8,193 - 32,768; k_set_hash_pair, the clearing on one lane, its A/B twin),
+k_set_hash_quad + k_set_hash_fix (4,097 - 8,192), the row pipeline k_hrow_*
 (513 - 4,096) and k_set_hash_coop (<= 512; k_set_hash_wave is its
 fall-back).  Each one runs here on the same 640
 messages -- empty, 200-byte, random lengths up to 256 bytes -- under the
@@ -12,7 +13,7 @@ library's hook (tests/native/k_test_hash.hip), which launches the PRODUCT
 library's kernels, and its compressed H(m) is compared byte for byte with the
 C oracle (oracle/c: hash_to_G2, RFC 9380) and with the committed golden
 vectors (tests/golden/vectors.json "hash_to_G2").  The row pipeline, the
-two-wave kernel and the quad kernel also run with every set forced through their one-lane exact
+two-wave kernel and the lane-group kernels also run with every set forced through their one-lane exact
 fall-backs (k_hrow_fix, k_set_hash_fix: the path a Z = 0 cofactor chain
 takes)."""
 
@@ -31,7 +32,7 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 NUL_DST = b"BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_NUL_"
 RINV = pow(1 << 406, -1, O.P)  # Montgomery R = 2^406 (tb_fp.h)
-VARIANTS = {0: "k_set_hash", 1: "k_set_hash_pair", 2: "k_hrow_*", 3: "k_set_hash_coop", 4: "k_set_hash_wave", 5: "k_set_hash_w2 + k_set_hash_fix", 6: "k_set_hash_quad + k_set_hash_fix"}
+VARIANTS = {0: "k_set_hash", 1: "k_set_hash_pair", 2: "k_hrow_*", 3: "k_set_hash_coop", 4: "k_set_hash_wave", 5: "k_set_hash_w2 + k_set_hash_fix", 6: "k_set_hash_quad + k_set_hash_fix", 7: "k_set_hash_duo + k_set_hash_fix"}
 
 
 def messages():
@@ -90,7 +91,7 @@ def test_hash_kernel_bytes(hook, expected, variant, dst):
     assert not bad, (VARIANTS[variant], len(bad), bad[:5])
 
 
-@pytest.mark.parametrize("variant", [2, 5, 6])
+@pytest.mark.parametrize("variant", [2, 5, 6, 7])
 def test_hash_fallback_bytes(hook, expected, variant):
     """Every set through the exact fall-back kernel (k_hrow_fix; k_set_hash_fix)."""
     ms, exp = expected

@@ -5,9 +5,11 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-echo "== hash variants"
-timeout -k 10 400 python -u -m pytest tests/test_gpu_hash_variants.py -x -q --timeout 180 --timeout-method thread > gpurun_out/pytest_r04f_hv.log 2>&1
-rc=$?; tail -4 gpurun_out/pytest_r04f_hv.log; [ $rc -eq 0 ] || exit $rc
+if [ -z "$NOHV" ]; then
+  echo "== hash variants"
+  timeout -k 10 400 python -u -m pytest tests/test_gpu_hash_variants.py -x -q --timeout 180 --timeout-method thread > gpurun_out/pytest_r04f_hv.log 2>&1
+  rc=$?; tail -4 gpurun_out/pytest_r04f_hv.log; [ $rc -eq 0 ] || exit $rc
+fi
 for plan in "4096,16384,32768" "4096,0,32768"; do
   echo "== stage_small 16384 plan=$plan"
   TBLS_HASH_PLAN=$plan timeout -k 10 300 python tools/stage_small.py 16384 > gpurun_out/stage16k_$plan.json 2> gpurun_out/stage16k_$plan.err || exit $?
