@@ -428,13 +428,18 @@ struct ws_layout {
 // caller's stream, for exclusive per-stage timings.
 
 // The large-batch one-lane kernels (hash, signature check, [r] apk) as their
-// two-waves-per-SIMD twins (k_w2_*.hip); TBLS_W2=0 selects the one-wave
-// kernels (A/B).  (The Miller line and accumulator kernels measured slower at
-// two waves -- 17.5 and 24.3 vs 14.5 ms Miller stage at 131,072 sets,
-// profiles/r04_bench_w2_masks.json -- and stay at one.)
-static bool w2() {
+// two-waves-per-SIMD twins (k_w2_*.hip) from TB_MSM_MIN sets, where each
+// stage fills the GPU alone (throughput); TBLS_W2=0 selects the one-wave
+// kernels (A/B).  Below it the stages run side by side and each is a
+// latency chain: the one-wave kernels spill less, and a wave that holds the
+// whole register file keeps its SIMD to itself instead of sharing it with
+// another stage's two-wave waves (profiles/r04_stage16k_*).  (The Miller
+// line and accumulator kernels measured slower at two waves -- 17.5 and 24.3
+// vs 14.5 ms Miller stage at 131,072 sets, profiles/r04_bench_w2_masks.json
+// -- and stay at one.)
+static bool w2(uint32_t n) {
   static const bool v = !(getenv("TBLS_W2") && getenv("TBLS_W2")[0] == '0');
-  return v;
+  return v && n >= TB_MSM_MIN;
 }
 // Small batches (<= TB_HASH_WAVE_MAX sets) run the key, signature and hash
 // stages, and multi-key aggregation, on the lane-cooperative kernels
@@ -459,7 +464,7 @@ void launch_set_pk(hipStream_t s, uint32_t n, uint32_t n_entries, const uint32_t
   // k_kcoop.hip, with the set's -[r] g1), or the one-wave-per-set kernel with
   // TBLS_COOP=0
   const uint32_t multi = n_entries > n ? (coop() ? 2u : 1u) : 0u;
-  hipLaunchKernelGGL(w2() ? k_set_pk_w2 : k_set_pk, g, blk, 0, s, pk_off, aff, code, rand, n, P, set_code, n_bad, key_idx, tab_n, multi, P2,
+  hipLaunchKernelGGL(w2(n) ? k_set_pk_w2 : k_set_pk, g, blk, 0, s, pk_off, aff, code, rand, n, P, set_code, n_bad, key_idx, tab_n, multi, P2,
                      comb);
   if (!multi) return;
   (void)hipMemsetAsync(mcnt, 0, 4, s);
@@ -537,13 +542,13 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
   TB_EV(4, ssig);
   if (n) {
     if (pp.msm)
-      hipLaunchKernelGGL(w2() ? k_sig_check_w2 : k_sig_check, g, blk, 0, ssig, b.sigs, n, (g2a*)(w + L.sig_aff), w + L.sig_use,
+      hipLaunchKernelGGL(w2(n) ? k_sig_check_w2 : k_sig_check, g, blk, 0, ssig, b.sigs, n, (g2a*)(w + L.sig_aff), w + L.sig_use,
                          w + L.sig_code, (uint32_t*)(w + L.n_bad), 0u);
     else if (n <= TB_HASH_WAVE_MAX && coop())  // the same, 4 sets per wave, lane-cooperative
       hipLaunchKernelGGL(k_sig_check_coop, dim3((n + 3) / 4), dim3(64), 0, ssig, b.sigs, n, (g2a*)(Q + n), skip + n, w + L.sig_code,
                          (uint32_t*)(w + L.n_bad));
     else  // the set's signature pair: Q[n + i] = sig_i, skip[n + i] = infinite / invalid
-      hipLaunchKernelGGL(w2() ? k_sig_check_w2 : k_sig_check, g, blk, 0, ssig, b.sigs, n, Q + n, skip + n, w + L.sig_code,
+      hipLaunchKernelGGL(w2(n) ? k_sig_check_w2 : k_sig_check, g, blk, 0, ssig, b.sigs, n, Q + n, skip + n, w + L.sig_code,
                          (uint32_t*)(w + L.n_bad), 1u);
   }
   TB_EV(5, ssig);
@@ -620,7 +625,7 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
     hipLaunchKernelGGL(k_set_hash_fix, g, blk, 0, sh, b.msgs, b.msg_off, dst, dlen, n, Q, skip);
   } else if (hash_pair(n))
     hipLaunchKernelGGL(k_set_hash_pair, dim3((2 * n + TB_BLOCK - 1) / TB_BLOCK), blk, 0, sh, b.msgs, b.msg_off, dst, dlen, n, Q, skip);
-  else if (n && w2()) {  // two waves per SIMD, then the exact formulas for the sets it flags (skip == 2)
+  else if (n && w2(n)) {  // two waves per SIMD, then the exact formulas for the sets it flags (skip == 2)
     hipLaunchKernelGGL(k_set_hash_w2, g, blk, 0, sh, b.msgs, b.msg_off, dst, dlen, n, Q, skip);
     hipLaunchKernelGGL(k_set_hash_fix, g, blk, 0, sh, b.msgs, b.msg_off, dst, dlen, n, Q, skip);
   } else if (n)
