@@ -104,9 +104,9 @@ extern "C" __global__ void k_final_verify_recs(const uint8_t* __restrict__ recs,
 #define TB_CFE_THREADS 256
 extern "C" __global__ void k_final_verify_recs_coop(const uint8_t* __restrict__ recs, uint32_t g, int* __restrict__ result);
 extern "C" __global__ void k_final_verify_coop(const fp12* __restrict__ f, uint32_t g, const uint32_t* __restrict__ n_bad, int* __restrict__ result);
-// TBLS_FINAL_COOP=0 selects the one-wave final exponentiation (A/B)
+// TBLS_COOP=0 selects the one-wave final exponentiation too (A/B, fall-back)
 inline bool tb_final_coop() {
-  static const bool v = !(getenv("TBLS_FINAL_COOP") && getenv("TBLS_FINAL_COOP")[0] == '0');
+  static const bool v = !(getenv("TBLS_COOP") && getenv("TBLS_COOP")[0] == '0');
   return v;
 }
 // the final verification of g partial records on stream s (*result in device memory)
