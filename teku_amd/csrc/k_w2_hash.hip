@@ -11,7 +11,8 @@
 // 256-register bound too, and a second wave per SIMD hides the latency the
 // one-wave kernels stall on (MAD issue: 5.4 cycles per wave64 instruction at
 // one wave per SIMD, 4.5 at two, tools/microbench/mad_peak.hip).  The cofactor
-// clearing is the branch-free g2_clear_cofactor_nx; a set whose chain meets an
+// clearing is the branch-free g2_clear_cofactor_nx_stash (one point parked in
+// LDS across the second [|x|] chain); a set whose chain meets an
 // exceptional case (Z = 0) is flagged skip = 2 and recomputed with the exact
 // formulas by k_set_hash_fix (k_hash.hip) on the same stream, so the results
 // are k_set_hash's.
@@ -19,9 +20,32 @@
 
 using namespace tb;
 
+namespace {
+// g2_clear_cofactor_nx in an order that keeps one point besides the loop
+// state live across each [|x|] chain: t1 = [|x|]P first (its base P is live
+// anyway), then u = psi(P) - t1 and w = t1 + A, w parked in *stash (the
+// caller's LDS slot) while t3 = [|x|]u runs; out = w - t3.  The same point
+// (the group law is associative); an exceptional case anywhere ends at Z = 0
+// as in g2_clear_cofactor_nx.  (The throughput hash: the chains' live
+// points beside the doubling temporaries were spilled every iteration,
+// profiles/pmc_traffic.json.)
+__device__ TB_INLINE bool g2_clear_cofactor_nx_stash(g2j& out, const g2j& p, g2j* stash) {
+  const g2j t1 = jac_mul_xabs_nx(p);
+  const g2j t2 = g2_psi(p);
+  const g2j u = jac_add_nx(t2, jac_neg(t1));
+  const g2j A = jac_add_nx(jac_add_nx(g2_psi2(jac_dbl_i(p)), jac_neg(p)), jac_neg(t2));
+  *stash = jac_add_nx(t1, A);
+  const g2j t3 = jac_mul_xabs_nx(u);
+  out = jac_add_nx(jac_neg(t3), *stash);
+  return !fp2_is_zero(out.z);
+}
+
+}  // namespace
+
 extern "C" __global__ void __launch_bounds__(TB_BLOCK, 2)
     k_set_hash_w2(const uint8_t* __restrict__ msgs, const uint32_t* __restrict__ msg_off, const uint8_t* __restrict__ dst,
                   uint32_t dlen, uint32_t n, g2a* __restrict__ Q, uint8_t* __restrict__ skip) {
+  __shared__ g2j stash[TB_BLOCK];  // 288 B per lane: 147 KB per CU at two waves per SIMD
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   xmd_ctx c;
@@ -35,7 +59,7 @@ extern "C" __global__ void __launch_bounds__(TB_BLOCK, 2)
   map_to_curve_sswu2(q0, q1, u0, u1);
   const g2j p = iso_map_jac(e2p_add_aff_aff(q0, q1));
   g2j h;
-  if (!g2_clear_cofactor_nx(h, p)) {
+  if (!g2_clear_cofactor_nx_stash(h, p, &stash[threadIdx.x])) {
     skip[i] = 2;  // k_set_hash_fix: the exact formulas
     return;
   }

@@ -332,6 +332,39 @@ TB_HD TB_NOINLINE jac<F> jac_mul_u64_aff(const aff<F>& P, uint64_t k) {
   return r;
 }
 
+// [k]P for G1, P affine and finite, k != 0: fixed 2-bit windows over the
+// affine table {P, 2P, 3P} (2P and 3P normalized with one shared inversion).
+// Every lane of a wave takes the same path -- two doublings and one mixed
+// addition per window -- where the bitwise form's per-lane "add if bit set"
+// makes a wave of random 64-bit scalars run the addition at every step:
+// 62 doublings + 32 additions instead of, in effect, 63 + 63 (the [r] apk
+// stage).  A window digit of 0 adds nothing (its lanes are masked off the
+// addition); the exceptional cases stay with jac_add_aff_i's branch.
+TB_HD TB_INLINE g1j g1_mul_u64_aff_w2(const g1a& P, uint64_t k) {
+  const g1j P2j = jac_dbl_i(jac_from_aff(P));
+  const g1j P3j = jac_add_aff_i(P2j, P);
+  // one inversion for both: 1 / (Z2 Z3)
+  const fp zz = fp_mul(P2j.z, P3j.z);
+  const fp iz = fp_inv(zz);
+  const fp i2 = fp_mul(iz, P3j.z), i3 = fp_mul(iz, P2j.z);
+  const fp i22 = fp_sqr(i2), i33 = fp_sqr(i3);
+  const g1a T2 = {fp_mul(P2j.x, i22), fp_mul(fp_mul(P2j.y, i22), i2)};
+  const g1a T3 = {fp_mul(P3j.x, i33), fp_mul(fp_mul(P3j.y, i33), i3)};
+  const int top = 63 - __builtin_clzll(k);
+  int w = top >> 1;  // the top window holds bits 2w + 1, 2w
+  uint32_t d = (uint32_t)(k >> (2 * w)) & 3u;  // != 0
+  g1j r = jac_from_aff(d == 1 ? P : d == 2 ? T2 : T3);
+  TB_NOUNROLL for (--w; w >= 0; --w) {
+    r = jac_dbl_i(jac_dbl_i(r));
+    d = (uint32_t)(k >> (2 * w)) & 3u;
+    if (d) {
+      const g1a t = {fp_sel(d == 1, P.x, fp_sel(d == 2, T2.x, T3.x)), fp_sel(d == 1, P.y, fp_sel(d == 2, T2.y, T3.y))};
+      r = jac_add_aff_i(r, t);
+    }
+  }
+  return r;
+}
+
 // [k]P for Jacobian P.  G2 (Fp2 coordinates): the addition is an outlined
 // call -- the G2 scalars here are |x| (5 additions in 63 steps: the cofactor
 // clearing, the subgroup checks), and an inlined addition's ~11 Fp2
@@ -446,10 +479,11 @@ TB_HD TB_INLINE jac<F> jac_mul_xabs_nx(const jac<F>& P) {
 
 // [x]P with x = -0xd201000000010000
 // TB_G1_XRUNS=1: the same for G1 (g1_mul_x, the key subgroup check): its
-// doubling loop loses 18 scratch accesses per step; built and CPU-tested, not
-// yet measured on the GPU, so off by default.
+// doubling loop loses 18 scratch accesses per step; measured in round 4 (key
+// decompression at 131,072 keys 3.45 -> 3.31 ms, profiles/r04_bench_g1x.json),
+// so on by default (0: the general jac_mul_u64, A/B).
 #ifndef TB_G1_XRUNS
-#define TB_G1_XRUNS 0
+#define TB_G1_XRUNS 1
 #endif
 #if TB_G2_XRUNS
 TB_HD TB_INLINE g2j g2_mul_x(const g2j& p) { return jac_neg(jac_mul_xabs(p)); }
@@ -475,7 +509,8 @@ TB_HD TB_NOINLINE bool g2_in_group(const g2j& q) {
 // rejected, as the exact check rejects it.  Same verdict for every finite Q.
 TB_HD TB_INLINE bool g2_in_group_nx(const g2j& q) {
   if (jac_is_inf(q)) return true;
-  return jac_eq(g2_psi(q), jac_neg(jac_mul_xabs_nx(q)));
+  const g2j t = jac_mul_xabs_nx(q);  // first: psi(Q) is not live across the chain
+  return jac_eq(g2_psi(q), jac_neg(t));
 }
 
 // Scott: P in G1 <=> phi(P) == [-x^2]P, phi(X,Y,Z) = (beta X, Y, Z)

@@ -49,7 +49,8 @@ TB_HD TB_INLINE int stage_set_pk(const g1a* pk_aff, const uint8_t* pk_code, uint
     uint32_t k;
     if (!set_key(idx, tab_n, b, k)) return TB_BAD_ENCODING;
     if (pk_code[k] != TB_SUCCESS) return TB_PK_IS_INFINITY;
-    g1j rp = jac_mul_u64_aff(pk_aff[k], r);
+    if (r == 0) return TB_PK_IS_INFINITY;  // [0] apk (a caller's randomizer is never 0)
+    g1j rp = g1_mul_u64_aff_w2(pk_aff[k], r);
     if (!jac_to_aff(P, rp)) code = TB_PK_IS_INFINITY;
     return code;
   }

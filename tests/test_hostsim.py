@@ -145,3 +145,26 @@ def test_g2_in_group_branch_free(run):
     a = [u32(x) for x in run("G2_IN_GROUP_NX", recs)]
     b = [u32(x) for x in run("G2_IN_GROUP", recs)]
     assert a == b == [1] * len(g2) + [0] * len(other)
+
+
+def test_stage_set_pk_windowed(run):
+    """tb_stages.h stage_set_pk for one key: P = [r] pk affine by the fixed
+    2-bit-window form (tb_curve.h g1_mul_u64_aff_w2) -- random 64-bit r and
+    the edge scalars (1, 2, 3, 4, a lone top bit, all ones, zero windows
+    between set ones), against the oracle; r = 0 reports infinity."""
+    rng = random.Random(17)
+    g = O.jac_from_affine(O.FP, O.G1_GEN)
+    pts = [O.jac_to_affine(O.FP, O.jac_mul(O.FP, g, rng.randrange(1, O.R))) for _ in range(6)]
+    rs = [1, 2, 3, 4, 5, 7, 1 << 63, (1 << 64) - 1, 0x8000000000000001, 0x5555555555555555, 0xC000000000000003, 0x100000000]
+    rs += [rng.getrandbits(64) | 1 for _ in range(30)]
+    recs, want = [], []
+    for i, r in enumerate(rs):
+        pt = pts[i % len(pts)]
+        recs.append(enc_fp(pt[0]) + enc_fp(pt[1]) + (r & 0xFFFFFFFF).to_bytes(4, "little") + (r >> 32).to_bytes(4, "little"))
+        want.append(O.jac_to_affine(O.FP, O.jac_mul(O.FP, O.jac_from_affine(O.FP, pt), r)))
+    out = run("STAGE_SET_PK", recs)
+    for o, w in zip(out, want):
+        assert u32(o) == 0
+        assert (dec_fp(o[4:52]), dec_fp(o[52:100])) == w
+    z = run("STAGE_SET_PK", [enc_fp(pts[0][0]) + enc_fp(pts[0][1]) + bytes(8)])
+    assert u32(z[0]) != 0
