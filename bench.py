@@ -66,7 +66,7 @@ STAGE_KERNEL = {
     "set_sig": "k_sig_check_w2",
     "set_hash": "k_set_hash_w2 + k_set_hash_fix",
     "g2_sum": "k_msm_bucket + k_msm_bucket_sum + k_msm_bitsum_pairs",
-    "miller": "k_miller_lines_lds + k_miller_acc2",
+    "miller": "k_miller_lines_w2 + k_miller_acc2",
     "fp12_prod": "k_fp12_prod_wave",
 }
 STAGE_UNITS = {"pk_decompress": "keys", "set_pk": "sets", "set_sig": "sets", "set_hash": "sets", "g2_sum": "sets", "miller": "pairs", "fp12_prod": "pairs"}
@@ -106,7 +106,7 @@ def plan_counts(S):
     kern = dict(STAGE_KERNEL)
     if os.environ.get("TBLS_W2") == "0":  # the library's kernel selection (tb_lib.hip w2)
         kern.update(set_pk="k_set_pk", set_sig="k_sig_check", set_hash="k_set_hash")
-    lines_k = "k_miller_lines_lds"
+    lines_k = "k_miller_lines_w2"
     acc_k = "k_miller_accs" if seg else f"k_miller_acc{2 if per == 2 else 1}"
     kern["miller"] = f"{lines_k} + {acc_k}"
     return mc, kern, {"per": per, "nseg": nseg, "kernel": acc_k}

@@ -45,7 +45,7 @@ extern "C" __global__ void __launch_bounds__(TB_BLOCK, 1)
   }
 }
 
-// k_miller_lines_lds with lanes 4i .. 4i + 3 per pair: the same 68 lines
+// k_miller_lines_w2 with lanes 4i .. 4i + 3 per pair: the same 68 lines
 // (tb_quad.h dbl_step / add_step), stored by lane 0 in the same layout.
 extern "C" __global__ void __launch_bounds__(TB_BLOCK, 1)
     k_miller_lines_quad(const g1a* __restrict__ P, const g2a* __restrict__ Q, const uint8_t* __restrict__ skip,
@@ -101,7 +101,7 @@ extern "C" __global__ void __launch_bounds__(TB_BLOCK, 1)
   }
 }
 
-// k_miller_lines_lds with lanes 2i, 2i + 1 per pair (duo::dbl_step /
+// k_miller_lines_w2 with lanes 2i, 2i + 1 per pair (duo::dbl_step /
 // add_step), lines stored by lane 2i in the same layout.
 extern "C" __global__ void __launch_bounds__(TB_BLOCK, 1)
     k_miller_lines_duo(const g1a* __restrict__ P, const g2a* __restrict__ Q, const uint8_t* __restrict__ skip,

@@ -1,16 +1,10 @@
-// Split Miller loop kernels (k_miller_lines_lds, k_miller_acc1/2, the
-// segmented k_miller_accs) at one wave per SIMD; device code in tb_lines.h.
+// Split Miller loop accumulator kernels (k_miller_acc1/2, the segmented
+// k_miller_accs) at one wave per SIMD; device code in tb_lines.h.  The line
+// kernels: k_w2_lines.hip (one lane per pair, two waves per SIMD),
+// k_hquad.hip (lane groups, mid-size batches).
 #include "tb_lines.h"
 
 using namespace tb;
-
-extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_MIN_WAVES)
-    k_miller_lines_lds(const g1a* __restrict__ P, const g2a* __restrict__ Q, const uint8_t* __restrict__ skip,
-                       const uint8_t* __restrict__ code_a, const uint8_t* __restrict__ code_b, uint32_t n, uint4* __restrict__ lines) {
-  __shared__ g1a psh[TB_BLOCK];
-  __shared__ g2p tsh[TB_BLOCK];
-  miller_lines_body(P, Q, skip, code_a, code_b, n, lines, psh, tsh);
-}
 
 extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_MIN_WAVES)
     k_miller_acc1(const uint4* __restrict__ lines, const uint8_t* __restrict__ skip, const uint8_t* __restrict__ code_a,

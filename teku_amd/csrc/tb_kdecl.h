@@ -13,7 +13,7 @@
 //                     large batches: bucket sums by randomizer byte, one pair
 //                     (-(d 2^(8w)) g1, B[w][d]) per bucket (k_msm_*, k_sigs.hip)
 //   k_miller_wave     per pair, one 64-lane wave (small batches)
-//   k_miller_lines_lds + k_miller_acc*   larger batches: G2 line precompute, then the Fp12 accumulation
+//   k_miller_lines_w2 / _quad / _duo + k_miller_acc*   larger batches: G2 line precompute, then the Fp12 accumulation
 //   k_fp12_prod_wave  F = prod f_i  (chunked wave-parallel levels; the per-GPU partial, 576 B)
 //   k_final_verify    final_exp(F) == 1 && no invalid set
 //
@@ -86,7 +86,6 @@ extern "C" __global__ void k_aggregate_sigs_many(const uint8_t* __restrict__ sig
 extern "C" __global__ void k_verify_each(const g1a* __restrict__ P, const g2a* __restrict__ Q, const uint8_t* __restrict__ skip, const uint8_t* __restrict__ set_code, const g2a* __restrict__ sig_aff, const uint8_t* __restrict__ sig_use, const uint8_t* __restrict__ sig_code, uint32_t n, uint8_t* __restrict__ ok);
 extern "C" __global__ void k_hash_to_g2(const uint8_t* __restrict__ msgs, const uint32_t* __restrict__ msg_off, const uint8_t* __restrict__ dst, uint32_t dlen, uint32_t n, uint8_t* __restrict__ out);
 extern "C" __global__ void k_sign(const uint64_t* __restrict__ sks, const uint8_t* __restrict__ msgs, const uint32_t* __restrict__ msg_off, const uint8_t* __restrict__ dst, uint32_t dlen, uint32_t n, uint8_t* __restrict__ out);
-extern "C" __global__ void k_miller_lines_lds(const g1a* __restrict__ P, const g2a* __restrict__ Q, const uint8_t* __restrict__ skip, const uint8_t* __restrict__ code_a, const uint8_t* __restrict__ code_b, uint32_t n, uint4* __restrict__ lines);
 extern "C" __global__ void k_miller_acc1(const uint4* __restrict__ lines, const uint8_t* __restrict__ skip, const uint8_t* __restrict__ code_a, const uint8_t* __restrict__ code_b, uint32_t n, fp12* __restrict__ f);
 extern "C" __global__ void k_miller_acc2(const uint4* __restrict__ lines, const uint8_t* __restrict__ skip, const uint8_t* __restrict__ code_a, const uint8_t* __restrict__ code_b, uint32_t n, fp12* __restrict__ f);
 extern "C" __global__ void k_miller_accs(const uint4* __restrict__ lines, const uint8_t* __restrict__ skip, const uint8_t* __restrict__ code_a, const uint8_t* __restrict__ code_b, uint32_t n, uint32_t per, uint32_t nseg, uint32_t g_pad, fp12* __restrict__ f_out, uint32_t seg_stride);

@@ -660,8 +660,8 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
           hipLaunchKernelGGL(lg == 4 ? k_miller_lines_quad : k_miller_lines_duo, dim3((lg * m + TB_BLOCK - 1) / TB_BLOCK), blk, 0, s,
                              (const g1a*)P + lo, (const g2a*)Q + lo, (const uint8_t*)skip + lo, ca + lo, cb + lo, m, lines);
         else
-          hipLaunchKernelGGL(k_miller_lines_lds, dim3((m + TB_BLOCK - 1) / TB_BLOCK), blk, 0, s, (const g1a*)P + lo, (const g2a*)Q + lo,
-                             (const uint8_t*)skip + lo, ca + lo, cb + lo, m, lines);
+          hipLaunchKernelGGL(k_miller_lines_w2, dim3((m + TB_BLOCK - 1) / TB_BLOCK), blk, 0, s,
+                             (const g1a*)P + lo, (const g2a*)Q + lo, (const uint8_t*)skip + lo, ca + lo, cb + lo, m, lines);
         if (pp.seg()) {
           const uint32_t g_pad = (mt + TB_BLOCK - 1) / TB_BLOCK * TB_BLOCK;
           hipLaunchKernelGGL(k_miller_accs, dim3(pp.nseg * g_pad / TB_BLOCK), blk, 0, s, (const uint4*)lines, (const uint8_t*)skip + lo,

@@ -187,25 +187,6 @@ __device__ TB_INLINE line3 dbl_step_f(g2p& T, const g1a& P) {
 }
 }  // namespace
 
-// One pair per thread, with the pair's G1 point and the twist point T in LDS
-// (round 3: scratch 612 -> 200 B per lane, fetch 2.0 -> 0.24 GB per 131k
-// launch, Miller stage 15.92 -> 15.64 ms against registers)
-__device__ TB_INLINE void miller_lines_body(const g1a* __restrict__ P, const g2a* __restrict__ Q, const uint8_t* __restrict__ skip,
-                                            const uint8_t* __restrict__ code_a, const uint8_t* __restrict__ code_b, uint32_t n,
-                                            uint4* __restrict__ lines, g1a* psh, g2p* tsh) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  if (skip[i] != 0 || code_a[i] != 0 || code_b[i] != 0) return;
-  g1a& p = psh[threadIdx.x];
-  g2p& T = tsh[threadIdx.x];
-  p = P[i];
-  T = {Q[i].x, Q[i].y, fp2_one()};
-  int s = 0;
-  TB_NOUNROLL for (int b = 62; b >= 0; --b) {
-    line_store(lines, n, i, s++, dbl_step_f(T, p));
-    if ((X_ABS >> b) & 1) line_store(lines, n, i, s++, add_step_f(T, Q[i], p));
-  }
-}
 
 // Thread t accumulates the pairs PER t .. PER t + PER - 1 (< n; their lines
 // in `lines`, stride n): per step one f^2 (paid once for the PER pairs) and
