@@ -71,10 +71,24 @@ extern "C" __global__ void __launch_bounds__(64)
 
 // Horner over the segment products of the segmented accumulator (k_lines.hip
 // k_miller_accs): R = v_0, then R = R^(2^d_j) v_j for j = 1 .. nseg - 1 (d_j =
-// doubling steps of segment j, byte j - 1 of dpack); one 256-thread coop
-// workgroup (tb_cfe.h products, general squaring as mul(x, x)).
+// doubling steps of segment j, the 68-step loop split as k_miller_accs splits
+// it: steps 68 j / nseg .. 68 (j + 1) / nseg - 1); one 256-thread coop
+// workgroup (tb_cfe.h products, general squaring as mul(x, x)).  (`dpack` is
+// unused: d_j is counted here, for any nseg.)
+__device__ __forceinline__ uint32_t seg_doublings(uint32_t j, uint32_t nseg) {
+  const int lo = (int)(68u * j / nseg), hi = (int)(68u * (j + 1) / nseg);
+  int s = 0;
+  uint32_t d = 0;
+  for (int b = 62; b >= 0; --b) {
+    d += (s >= lo && s < hi) ? 1u : 0u;  // step s: a doubling
+    s++;
+    if ((X_ABS >> b) & 1) s++;  // an addition step
+  }
+  return d;
+}
 extern "C" __global__ void __launch_bounds__(CFE_THREADS)
     k_fp12_seg_combine_coop(const fp12* __restrict__ vals, uint32_t nseg, uint32_t dpack, fp12* __restrict__ out) {
+  (void)dpack;
   __shared__ cfe_lds L;
   tb_latency_prio();
   cfe::init(L);
@@ -82,7 +96,7 @@ extern "C" __global__ void __launch_bounds__(CFE_THREADS)
   cfe::regs_load(R, L);
   cfe::load_coords(L.F, reinterpret_cast<const fp*>(vals));
   for (uint32_t j = 1; j < nseg; j++) {
-    const uint32_t d = (dpack >> (8 * (j - 1))) & 255u;
+    const uint32_t d = seg_doublings(j, nseg);
     for (uint32_t k = 0; k < d; k++) cfe::mul(L.F, L.F, L.F, L, R);
     cfe::load_coords(L.X, reinterpret_cast<const fp*>(vals + j));
     cfe::mul(L.F, L.F, L.X, L, R);

@@ -238,12 +238,18 @@ static uint32_t miller_wave_max() {
 // the loop's 68 steps in `nseg` segments.  Chosen to minimize the modelled
 // accumulator time: per-thread latency (68 / nseg) (12 + 13 per) Fp2
 // products (one f^2, per sparse line products per step) times the wave rounds
-// (TB_ACC_FULL threads = one 64-lane wave per SIMD fill the GPU once); ties go
-// to fewer segments (smaller product tree).  TBLS_ACC_PLAN="per,nseg"
-// overrides it (tuning; per in {1, 2, 4, 8}, nseg in 1..4; "0" selects the
-// unsegmented k_miller_acc1/2).  Every per divides TB_LINE_CHUNK, so the chunks
-// of a large batch fill contiguous group ranges (lo / per).
+// (TB_ACC_FULL threads = one 64-lane wave per SIMD fill the GPU once), plus
+// the Horner tail of the segment products (k_fp12_seg_combine_coop: ~63 (1 -
+// 1/nseg) Fp12 squarings, about one Fp2-product latency each); ties go to
+// fewer segments (smaller product tree).  TBLS_ACC_PLAN="per,nseg" overrides
+// it (tuning; per and nseg powers of two up to TB_ACC_PER_MAX /
+// TB_ACC_NSEG_MAX; "0" selects the unsegmented k_miller_acc1/2).  Every per
+// divides TB_LINE_CHUNK, so the chunks of a large batch fill contiguous group
+// ranges (lo / per).  (Round 4: per up to 32 and nseg up to 16 -- 32 x 16 at
+// 131,072 pairs, 8 x 16 at config 4's 32,768 -- where round 3 stopped at 8 x 4.)
 #define TB_ACC_FULL 65536u
+#define TB_ACC_PER_MAX 32
+#define TB_ACC_NSEG_MAX 16
 // TBLS_ACC_PLAN: -1 / -1 (unset), 0 / 0 ("0": unsegmented), or per / nseg
 static void acc_env(int& e_per, int& e_seg) {
   e_per = e_seg = -1;
@@ -254,7 +260,7 @@ static void acc_env(int& e_per, int& e_seg) {
     return;
   }
   int p = 0, g = 0;
-  if (sscanf(v, "%d,%d", &p, &g) == 2 && (p == 1 || p == 2 || p == 4 || p == 8) && g >= 1 && g <= 4) {
+  if (sscanf(v, "%d,%d", &p, &g) == 2 && p >= 1 && p <= TB_ACC_PER_MAX && (p & (p - 1)) == 0 && g >= 1 && g <= TB_ACC_NSEG_MAX) {
     e_per = p;
     e_seg = g;
   }
@@ -270,13 +276,13 @@ static void acc_plan(uint32_t n_main, uint32_t& per, uint32_t& nseg) {
   double best = 0;
   per = 1;
   nseg = 1;
-  for (uint32_t p = 1; p <= 8; p *= 2) {
+  for (uint32_t p = 1; p <= (uint32_t)TB_ACC_PER_MAX; p *= 2) {
     if (e_per > 0 && (int)p != e_per) continue;
-    for (uint32_t sg = 1; sg <= 4; sg++) {
-      if (e_seg > 0 ? (int)sg != e_seg : sg == 3) continue;
+    for (uint32_t sg = 1; sg <= (uint32_t)TB_ACC_NSEG_MAX; sg++) {
+      if (e_seg > 0 ? (int)sg != e_seg : (sg & (sg - 1)) != 0) continue;
       const double threads = (double)sg * ((n_main + p - 1) / p);
       const double rounds = std::max(1.0, std::ceil(threads / TB_ACC_FULL));
-      const double cost = rounds * (68.0 / sg) * (12.0 + 13.0 * p);
+      const double cost = rounds * (68.0 / sg) * (12.0 + 13.0 * p) + (sg > 1 ? 63.0 * (1.0 - 1.0 / sg) : 0.0);
       if (best == 0 || cost < best * 0.999) {
         best = cost;
         per = p;
@@ -285,24 +291,6 @@ static void acc_plan(uint32_t n_main, uint32_t& per, uint32_t& nseg) {
     }
   }
 }
-// Horner exponents of the segment products: byte j - 1 = doubling steps in
-// segment j (j >= 1) of the 68-step loop split as k_miller_accs splits it
-static uint32_t seg_dpack(uint32_t nseg) {
-  int dbl[68];
-  int s = 0;
-  for (int b = 62; b >= 0; --b) {
-    dbl[s++] = 1;
-    if ((X_ABS >> b) & 1) dbl[s++] = 0;
-  }
-  uint32_t pack = 0;
-  for (uint32_t j = 1; j < nseg; j++) {
-    uint32_t d = 0;
-    for (uint32_t t = 68 * j / nseg; t < 68 * (j + 1) / nseg; t++) d += (uint32_t)dbl[t];
-    pack |= d << (8 * (j - 1));
-  }
-  return pack;
-}
-
 struct pair_plan {
   uint32_t n, n_extra, n_pairs, n_main, n_xwave, per, nseg;
   bool msm, wave, split;
@@ -704,7 +692,7 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
         lvl++;
       }
       hipLaunchKernelGGL(k_fp12_seg_combine_coop, dim3(1), dim3(TB_CFE_THREADS), 0, s, (const fp12*)(w + L.segv), pp.nseg,
-                         seg_dpack(pp.nseg), (fp12*)partial_out);
+                         0u, (fp12*)partial_out);
     } else
     for (;;) {
       const uint32_t nout = (cnt + TB_PROD_CHUNK - 1) / TB_PROD_CHUNK;

@@ -285,21 +285,19 @@ __device__ TB_INLINE void miller_accs_body(const uint4* __restrict__ lines, cons
   }
   fp12 f = fp12_one();
   bool fresh = true;  // f == 1
-  // the used pairs' offsets, packed 4 bits each
-  uint32_t uidx = 0, nu = 0;
-  for (uint32_t k = 0; k < per; k++)
-    if ((usem >> k) & 1u) uidx |= k << (4 * nu++);
+  // (per <= 32: usem is one bit per owned pair; with every pair valid the
+  // lanes of a wave take the same path)
   TB_NOUNROLL for (int s = s_lo; s < s_hi; s++) {
     if (!fresh && step_is_dbl(s)) f = fp12_sqr_i(f);
-    uint32_t k = 0;
-    if (fresh && nu) {
-      f = line_fp12(line_load(lines, n, i0 + (uidx & 15u) * G, s));
-      fresh = false;
-      k = 1;
-    }
-    TB_NOUNROLL for (; k < nu; k++) {
-      const line3 l = line_load(lines, n, i0 + ((uidx >> (4 * k)) & 15u) * G, s);
-      f = fp12_mul_by_line_i(f, l.a, l.b, l.c);
+    TB_NOUNROLL for (uint32_t k = 0; k < per; k++) {
+      if (!((usem >> k) & 1u)) continue;
+      const line3 l = line_load(lines, n, i0 + k * G, s);
+      if (fresh) {
+        f = line_fp12(l);
+        fresh = false;
+      } else {
+        f = fp12_mul_by_line_i(f, l.a, l.b, l.c);
+      }
     }
   }
   f_out[(size_t)j * seg_stride + g] = fp12_conj(f);

@@ -206,6 +206,15 @@ def check(rc, what):
         raise NativeError(rc, what)
 
 
+def acc_plan(n_sets):
+    """The Miller accumulator plan the library runs for a batch of n_sets
+    single-key sets (tbls_acc_plan; no device needed): (per, nseg, split)."""
+    L = load_library() if _lib is None else _lib
+    per, nseg, split = ctypes.c_uint32(0), ctypes.c_uint32(0), ctypes.c_int(0)
+    check(L.tbls_acc_plan(n_sets, ctypes.byref(per), ctypes.byref(nseg), ctypes.byref(split)), "acc_plan")
+    return per.value, nseg.value, split.value
+
+
 def place_plan(n, n_pks=None, n_devices=8, n_gpus=0, load=None, rr=0, shard_min=None):
     """The library's device placement of a batch (tbls_place_plan; no device
     needed): returns (devices, cuts) -- device devices[k] verifies sets

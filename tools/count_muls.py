@@ -97,7 +97,7 @@ def main():
     # a segment skips its first step's squaring (f = 1) and takes its first
     # line as f.  MILLER2 (two pairs per accumulator, 62 squarings) minus its
     # accumulator share plus the plan's; the segment products' Horner tail (<= 49
-    # Fp12 squarings per batch) is below 0.01 M per pair at 131,072 pairs.
+    # Fp12 squarings per batch, <= 59 at 16 segments) is below 0.01 M per pair at 131,072 pairs.
     X_ABS = 0xD201000000010000
     dbl = []
     for b in range(62, -1, -1):
@@ -106,7 +106,7 @@ def main():
             dbl.append(0)
     SQR12, LINE12 = 36, 39
     acc2 = (62 * SQR12) / 2 + 68 * LINE12
-    for per, nseg in ((1, 4), (2, 4), (4, 2), (4, 4), (8, 2), (8, 4)):
+    for per, nseg in ((1, 4), (2, 4), (4, 2), (4, 4), (8, 2), (8, 4), (1, 16), (2, 16), (4, 16), (8, 16), (16, 16), (32, 8), (32, 16)):
         sq_ = sum(sum(dbl[68 * j // nseg:68 * (j + 1) // nseg]) - dbl[68 * j // nseg] for j in range(nseg))
         accs = (sq_ * SQR12 + (per * 68 - nseg) * LINE12) / per
         res[f"miller_seg_{per}x{nseg}"] = res["miller"] - acc2 + accs
