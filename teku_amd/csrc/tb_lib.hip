@@ -245,10 +245,11 @@ static uint32_t miller_wave_max() {
 // it (tuning; per and nseg powers of two up to TB_ACC_PER_MAX /
 // TB_ACC_NSEG_MAX; "0" selects the unsegmented k_miller_acc1/2).  Every per
 // divides TB_LINE_CHUNK, so the chunks of a large batch fill contiguous group
-// ranges (lo / per).  (Round 4: per up to 32 and nseg up to 16 -- 32 x 16 at
-// 131,072 pairs, 8 x 16 at config 4's 32,768 -- where round 3 stopped at 8 x 4.)
+// ranges (lo / per).  (Round 4: per up to 16 and nseg up to 16 -- 16 x 8 at
+// 131,072 pairs, 8 x 16 at config 4's 32,768 -- where round 3 stopped at 8 x 4;
+// profiles/r04_bench_accplans.json.)
 #define TB_ACC_FULL 65536u
-#define TB_ACC_PER_MAX 32
+#define TB_ACC_PER_MAX 16  // 32 x 16 measured slower than 16 x 8 at 131,072 pairs (13.9 vs 13.3 ms Miller stage)
 #define TB_ACC_NSEG_MAX 16
 // TBLS_ACC_PLAN: -1 / -1 (unset), 0 / 0 ("0": unsegmented), or per / nseg
 static void acc_env(int& e_per, int& e_seg) {

@@ -106,7 +106,7 @@ def main():
             dbl.append(0)
     SQR12, LINE12 = 36, 39
     acc2 = (62 * SQR12) / 2 + 68 * LINE12
-    for per, nseg in ((1, 4), (2, 4), (4, 2), (4, 4), (8, 2), (8, 4), (1, 16), (2, 16), (4, 16), (8, 16), (16, 16), (32, 8), (32, 16)):
+    for per, nseg in ((1, 4), (2, 4), (4, 2), (4, 4), (8, 2), (8, 4), (1, 16), (2, 16), (4, 16), (8, 16), (16, 4), (16, 8), (16, 16), (32, 8), (32, 16)):
         sq_ = sum(sum(dbl[68 * j // nseg:68 * (j + 1) // nseg]) - dbl[68 * j // nseg] for j in range(nseg))
         accs = (sq_ * SQR12 + (per * 68 - nseg) * LINE12) / per
         res[f"miller_seg_{per}x{nseg}"] = res["miller"] - acc2 + accs
