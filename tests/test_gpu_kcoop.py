@@ -186,3 +186,28 @@ def test_dev_batch_uneven_sets_fallback(hip, sets):
 
     assert run(pks[1]) == 1
     assert run(bad_keys()["order 11"]) == 2
+
+
+def test_multi_key_batch_keys_outside_g1_quad(hip):
+    """Multi-key batches decompress their keys on a DPP quad per key
+    (k_w2_pk.hip k_pk_decompress_quad, more keys than sets, up to 32,768
+    keys): the subgroup check's branch-free [x^2] chain on four lanes must
+    reject every outside-G1 key -- random non-G1 points and points of order
+    3, 11, 33, whose multiples meet the exceptional addition cases -- at
+    several positions of a 16 sets x 20 keys batch, and accept the clean
+    batch."""
+    from teku_amd import synth
+
+    bls = hip[0]
+    keys, msgs, sigs = synth.multi_key(16, 20, first_key=3000, seed=9)
+    rands = [random.getrandbits(64) | 1 for _ in sigs]
+
+    def run(ks):
+        return bls.batch_verify_raw([(b"".join(k), len(k), m, s) for k, m, s in zip(ks, msgs, sigs)], rands)
+
+    assert run(keys) is True
+    for name, bad in bad_keys().items():
+        for s_i, k_i in ((0, 0), (3, 1), (7, 2), (15, 19)):
+            ks = [list(k) for k in keys]
+            ks[s_i][k_i] = bad
+            assert run(ks) is False, (name, s_i, k_i)
