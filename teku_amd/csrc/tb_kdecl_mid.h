@@ -9,4 +9,3 @@ extern "C" __global__ void k_miller_lines_quad(const g1a* __restrict__ P, const 
 extern "C" __global__ void k_set_hash_duo(const uint8_t* __restrict__ msgs, const uint32_t* __restrict__ msg_off, const uint8_t* __restrict__ dst, uint32_t dlen, uint32_t n, g2a* __restrict__ Q, uint8_t* __restrict__ skip);
 extern "C" __global__ void k_miller_lines_duo(const g1a* __restrict__ P, const g2a* __restrict__ Q, const uint8_t* __restrict__ skip, const uint8_t* __restrict__ code_a, const uint8_t* __restrict__ code_b, uint32_t n, uint4* __restrict__ lines);
 extern "C" __global__ void k_miller_lines_w2(const g1a* __restrict__ P, const g2a* __restrict__ Q, const uint8_t* __restrict__ skip, const uint8_t* __restrict__ code_a, const uint8_t* __restrict__ code_b, uint32_t n, uint4* __restrict__ lines);  // k_w2_lines.hip
-extern "C" __global__ void k_pk_decompress_quad(const uint8_t* __restrict__ pks, uint32_t K, g1a* __restrict__ pk_aff, uint8_t* __restrict__ pk_code);  // k_w2_pk.hip

@@ -426,11 +426,6 @@ struct ws_layout {
 // line and accumulator kernels measured slower at two waves -- 17.5 and 24.3
 // vs 14.5 ms Miller stage at 131,072 sets, profiles/r04_bench_w2_masks.json
 // -- and stay at one.)
-// Multi-key batches up to this many keys decompress them on a quad per key
-// (k_w2_pk.hip k_pk_decompress_quad: the subgroup check's doublings dealt
-// over four lanes; 4 x 32,768 lanes fill one two-wave round).  TBLS_COOP=0
-// keeps the one-lane kernel.
-#define TB_KEYS_QUAD_MAX 32768u
 static bool w2(uint32_t n) {
   static const bool v = !(getenv("TBLS_W2") && getenv("TBLS_W2")[0] == '0');
   return v && n >= TB_MSM_MIN;
@@ -583,10 +578,7 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
     TB_EV(1, sa);
     TB_EV(2, sa);
   } else {
-    if (K && K > n && K <= TB_KEYS_QUAD_MAX && coop())  // multi-key batches (configs 2/3): a quad per key
-      hipLaunchKernelGGL(k_pk_decompress_quad, dim3((4 * K + TB_BLOCK - 1) / TB_BLOCK), blk, 0, sa, b.pks, K, (g1a*)(w + L.pk_aff),
-                         w + L.pk_code);
-    else if (K)
+    if (K)
       hipLaunchKernelGGL(k_pk_decompress, dim3((K + TB_BLOCK - 1) / TB_BLOCK), blk, 0, sa, b.pks, K, (g1a*)(w + L.pk_aff), w + L.pk_code);
     TB_EV(1, sa);
     TB_EV(2, sa);

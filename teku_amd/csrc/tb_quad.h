@@ -91,37 +91,6 @@ __device__ TB_INLINE void rsqr(fp2 (&r)[N], const fp2 (&a)[N]) {
 }
 
 
-// the same for Fp (G1)
-template <int G, int SRC>
-__device__ TB_INLINE fp bc1(const fp& a) {
-  fp r;
-  TB_UNROLL for (int w = 0; w < 12; w++) r.l[w] = bc<G, SRC>(a.l[w]);
-  return r;
-}
-template <int N>
-__device__ TB_INLINE fp pick1(uint32_t q, const fp (&v)[N]) {
-  fp x = v[N - 1];
-  TB_UNROLL for (int k = N - 2; k >= 0; k--) x = fp_sel(q == (uint32_t)k, v[k], x);
-  return x;
-}
-template <int G, int N>
-__device__ TB_INLINE void spread1(fp (&r)[N], const fp& p) {
-  r[0] = bc1<G, 0>(p);
-  if constexpr (N > 1) r[1] = bc1<G, 1>(p);
-  if constexpr (N > 2) r[2] = bc1<G, 2>(p);
-  if constexpr (N > 3) r[3] = bc1<G, 3>(p);
-}
-template <int G, int N>
-__device__ TB_INLINE void rmul1(fp (&r)[N], const fp (&a)[N], const fp (&b)[N]) {
-  static_assert(N >= 1 && N <= G, "one product per member");
-  const uint32_t q = glane<G>();
-  spread1<G, N>(r, fp_mul(pick1<N>(q, a), pick1<N>(q, b)));
-}
-template <int G, int N>
-__device__ TB_INLINE void rsqr1(fp (&r)[N], const fp (&a)[N]) {
-  static_assert(N >= 1 && N <= G, "one product per member");
-  spread1<G, N>(r, fp_sqr(pick1<N>(glane<G>(), a)));
-}
 }  // namespace lg
 
 namespace quad {
@@ -412,82 +381,4 @@ __device__ TB_INLINE line3 add_step(g2p& T, const g2a& Q, const g1a& P) {
 }
 }  // namespace duo
 
-// ---------------------------------------------------------------------------
-// G1 on a quad (the key subgroup check of multi-key batches): the G2 rounds
-// above on Fp coordinates.
-// ---------------------------------------------------------------------------
-namespace quad1 {
-template <int N>
-__device__ TB_INLINE void qmul(fp (&r)[N], const fp (&a)[N], const fp (&b)[N]) {
-  lg::rmul1<4, N>(r, a, b);
-}
-template <int N>
-__device__ TB_INLINE void qsqr(fp (&r)[N], const fp (&a)[N]) {
-  lg::rsqr1<4, N>(r, a);
-}
-
-// dbl-2009-l (tb_curve.h jac_dbl_i for G1): [X^2, Y^2, Y Z] [B^2, (X + B)^2, E^2] [E (D - X3)]
-__device__ TB_INLINE g1j dbl(const g1j& p) {
-  fp r1[3];
-  qmul<3>(r1, {p.x, p.y, p.y}, {p.x, p.y, p.z});
-  const fp A = r1[0], B = r1[1];
-  const fp E = fp_add_nr(fp_dbl(A), A);  // product operand only
-  fp r2[3];
-  qsqr<3>(r2, {B, fp_add_nr(p.x, B), E});
-  const fp C = r2[0];
-  const fp D = fp_dbl(fp_sub(fp_sub(r2[1], A), C));
-  g1j o;
-  o.x = fp_sub(r2[2], fp_dbl(D));
-  const fp C8 = fp_dbl(fp_dbl(fp_dbl(C)));
-  o.y = fp_sub(fp_mul(E, fp_sub(D, o.x)), C8);
-  o.z = fp_dbl(r1[2]);
-  return o;
-}
-
-// add-2007-bl without the exceptional branch (Z3 = 0 on P == +-Q or infinity)
-__device__ TB_INLINE g1j add(const g1j& p, const g1j& q) {
-  fp r1[4];
-  qmul<4>(r1, {p.z, q.z, p.y, q.y}, {p.z, q.z, q.z, p.z});
-  const fp Z1Z1 = r1[0], Z2Z2 = r1[1];
-  fp r2[4];
-  qmul<4>(r2, {p.x, q.x, r1[2], r1[3]}, {Z2Z2, Z1Z1, Z2Z2, Z1Z1});
-  const fp U1 = r2[0], S1 = r2[2];
-  const fp H = fp_sub(r2[1], U1);
-  const fp r = fp_dbl(fp_sub(r2[3], S1));
-  fp r3[3];
-  qsqr<3>(r3, {fp_dbl(H), r, fp_add_nr(p.z, q.z)});
-  const fp I = r3[0];
-  fp r4[3];
-  qmul<3>(r4, {H, U1, fp_sub(fp_sub(r3[2], Z1Z1), Z2Z2)}, {I, I, H});
-  const fp J = r4[0], V = r4[1];
-  g1j o;
-  o.x = fp_sub(fp_sub(r3[1], J), fp_dbl(V));
-  fp r5[2];
-  qmul<2>(r5, {r, S1}, {fp_sub(V, o.x), J});
-  o.y = fp_sub(r5[0], fp_dbl(r5[1]));
-  o.z = r4[2];
-  return o;
-}
-
-__device__ TB_INLINE g1j mul_xabs(const g1j& P) {
-  g1j r = P;
-  TB_NOUNROLL for (int k = 0; k < 6; k++) {
-    const int nd = k == 0 ? 1 : k == 1 ? 2 : k == 2 ? 3 : k == 3 ? 9 : k == 4 ? 32 : 16;  // XRUN_DBL[k]
-    TB_NOUNROLL for (int i = 0; i < nd; i++) r = dbl(r);
-    if (k < 5) r = add(r, P);
-  }
-  return r;
-}
-
-// Scott's G1 test phi(P) == [-x^2]P (tb_curve.h g1_in_group) with the
-// branch-free chains: a point of G1 meets no exceptional case below its order
-// (exact), a point outside whose chain meets one ends at Z = 0, unequal to the
-// finite phi(P) -- rejected, as the exact test rejects it
-__device__ TB_INLINE bool in_group(const g1j& p) {
-  if (jac_is_inf(p)) return true;
-  const g1j t = mul_xabs(mul_xabs(p));
-  const g1j phi = {fp_mul(p.x, fp_from_const(BETA)), p.y, p.z};
-  return jac_eq(phi, jac_neg(t));
-}
-}  // namespace quad1
 }  // namespace tb

@@ -189,13 +189,14 @@ def test_dev_batch_uneven_sets_fallback(hip, sets):
 
 
 def test_multi_key_batch_keys_outside_g1_quad(hip):
-    """Multi-key batches decompress their keys on a DPP quad per key
-    (k_w2_pk.hip k_pk_decompress_quad, more keys than sets, up to 32,768
-    keys): the subgroup check's branch-free [x^2] chain on four lanes must
-    reject every outside-G1 key -- random non-G1 points and points of order
-    3, 11, 33, whose multiples meet the exceptional addition cases -- at
-    several positions of a 16 sets x 20 keys batch, and accept the clean
-    batch."""
+    """Multi-key batches (k_pk_decompress, then the multi-key aggregation):
+    every outside-G1 key -- random non-G1 points and points of order 3, 11,
+    33, whose multiples meet the exceptional addition cases of the [x^2]
+    chain -- at several positions of a 16 sets x 20 keys batch makes the
+    batch fail, and the clean batch verifies.  (Round 4 measured a
+    quad-per-key decompression kernel here: configs 2/3 p50 5.48 -> 5.80 ms,
+    its 4 x 31,232 lanes fill the chip where the one-lane kernel's chains
+    run a quarter-full GPU, so it was removed.)"""
     from teku_amd import synth
 
     bls = hip[0]
