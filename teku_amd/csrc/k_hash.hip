@@ -20,44 +20,6 @@ extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_MIN_WAVES)
   skip[i] = ok ? 0 : 1;
 }
 
-// Two lanes per set (mid-size batches, tb_lib.hip hash_pair): lanes 2i and
-// 2i + 1 both run expand_message_xmd / hash_to_field (0.16 ms), then ONE SSWU
-// map each -- two instruction streams where k_set_hash interleaves both maps
-// on one lane (map_to_curve_sswu2, ~1.6 of the 6.4 ms chain at 16,384 sets) --
-// lane 2i takes its partner's image through two lane shuffles per word, adds,
-// maps through the isogeny and clears the cofactor.  Same Q_i and skip_i.
-extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_MIN_WAVES)
-    k_set_hash_pair(const uint8_t* __restrict__ msgs, const uint32_t* __restrict__ msg_off, const uint8_t* __restrict__ dst,
-                    uint32_t dlen, uint32_t n, g2a* __restrict__ Q, uint8_t* __restrict__ skip) {
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x, i = t >> 1, j = t & 1u;
-  if (i >= n) return;  // both lanes of a pair leave together
-  xmd_ctx c;
-  c.msg = msgs + msg_off[i];
-  c.mlen = msg_off[i + 1] - msg_off[i];
-  c.dst = dst;
-  c.dlen = dlen;
-  fp2 u0, u1;
-  hash_to_field_fp2(u0, u1, c);
-  const g2a q = map_to_curve_sswu(j ? u1 : u0);
-  g2a o;  // the partner lane's image
-  const uint32_t* qw = &q.x.c0.l[0];
-  uint32_t* ow = &o.x.c0.l[0];
-  static_assert(sizeof(g2a) == 48 * 4, "g2a is 48 words");
-  TB_UNROLL for (int k = 0; k < 48; k++) ow[k] = (uint32_t)__shfl_xor((int)qw[k], 1);
-  if (j) return;
-  const g2j p = iso_map_jac(e2p_add_aff_aff(q, o));
-  g2j h;
-  if (!g2_clear_cofactor_nx(h, p)) h = g2_clear_cofactor(p);  // exceptional chain or infinity: exact (tb_stages.h stage_set_hash)
-  g2a a;
-  const bool ok = jac_to_aff(a, h);
-  if (!ok) {
-    a.x = fp2_zero();
-    a.y = fp2_zero();
-  }
-  Q[i] = a;
-  skip[i] = ok ? 0 : 1;
-}
-
 // per item: compressed hash_to_G2 of message i
 extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_MIN_WAVES)
     k_hash_to_g2(const uint8_t* __restrict__ msgs, const uint32_t* __restrict__ msg_off, const uint8_t* __restrict__ dst,

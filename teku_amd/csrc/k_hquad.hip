@@ -70,7 +70,7 @@ extern "C" __global__ void __launch_bounds__(TB_BLOCK, 1)
 }
 
 // Q_i = hash_to_G2(m_i) with lanes 2i, 2i + 1 (batches whose quads would
-// overfill the GPU): k_set_hash_pair's split -- one SSWU map per lane, the
+// overfill the GPU): round 3's pair split -- one SSWU map per lane, the
 // images exchanged -- with the cofactor clearing on the lane pair too
 // (tb_quad.h duo::clear_cofactor) instead of on lane 2i alone; the chain's
 // exceptional cases flag skip = 2 for k_set_hash_fix.

@@ -318,30 +318,29 @@ struct pair_plan {
 // (TB_HASH_WAVE_MAX): one 16-lane coop row per set (k_hrow.hip) up to row_max
 // sets, one DPP quad per set (k_hquad.hip k_set_hash_quad) up to quad_max,
 // one lane pair per set (k_set_hash_duo: an SSWU map per lane, the cofactor
-// clearing dealt over the pair) up to duo_max, two lanes with the clearing on
-// one (k_set_hash_pair) up to pair_max, then the one-lane k_set_hash_w2.  A
-// lane group fills the GPU at 65,536 lanes: quads at 16,384 sets leave no
-// SIMD to the key and signature stages beside the hash
+// clearing dealt over the pair) up to duo_max, then the one-lane
+// k_set_hash_w2.  A lane group fills the GPU at 65,536 lanes: quads at 16,384
+// sets leave no SIMD to the key and signature stages beside the hash
 // (profiles/r04_stage16k_quad_vs_pair.json), so quads stop at 8,192.  The
 // Miller lines use the same groups while they fit one wave per SIMD: quads
 // up to 16,384 pairs, pairs up to 32,768 (k_miller_lines_quad / _duo),
-// unless quad_max / duo_max is 0.  TBLS_HASH_PLAN =
-// "row_max,quad_max,duo_max,pair_max" overrides the defaults (A/B; 0
-// disables a kernel).
+// unless quad_max / duo_max is 0.  TBLS_HASH_PLAN = "row_max,quad_max,duo_max"
+// overrides the defaults (A/B; 0 disables a kernel).  (Round 3's pair kernel,
+// the SSWU maps on two lanes and the clearing on one, was removed once the
+// duo kernel replaced it: 16,384-set hash stage 5.10 -> 3.65 ms.)
 #define TB_HASH_ROW_MAX 4096u
 #define TB_HASH_QUAD_MAX 8192u
 #define TB_HASH_DUO_MAX 32768u
-#define TB_HASH_PAIR_MAX 0u
 #define TB_GROUP_LANES 65536u  // one wave per SIMD
 struct hash_plan_t {
-  uint32_t row_max, quad_max, duo_max, pair_max;
+  uint32_t row_max, quad_max, duo_max;
 };
 static const hash_plan_t& hash_plan() {
   static const hash_plan_t v = [] {
-    hash_plan_t h{TB_HASH_ROW_MAX, TB_HASH_QUAD_MAX, TB_HASH_DUO_MAX, TB_HASH_PAIR_MAX};
+    hash_plan_t h{TB_HASH_ROW_MAX, TB_HASH_QUAD_MAX, TB_HASH_DUO_MAX};
     const char* e = getenv("TBLS_HASH_PLAN");
-    unsigned r, q, d, p;
-    if (e && sscanf(e, "%u,%u,%u,%u", &r, &q, &d, &p) == 4) h = {r, q, d, p};
+    unsigned r, q, d;
+    if (e && sscanf(e, "%u,%u,%u", &r, &q, &d) == 3) h = {r, q, d};
     return h;
   }();
   return v;
@@ -349,9 +348,6 @@ static const hash_plan_t& hash_plan() {
 static bool hash_row(uint32_t n) { return n > TB_HASH_WAVE_MAX && n <= hash_plan().row_max; }
 static bool hash_quad(uint32_t n) { return n > TB_HASH_WAVE_MAX && !hash_row(n) && n <= hash_plan().quad_max; }
 static bool hash_duo(uint32_t n) { return n > TB_HASH_WAVE_MAX && !hash_row(n) && !hash_quad(n) && n <= hash_plan().duo_max; }
-static bool hash_pair(uint32_t n) {
-  return n > TB_HASH_WAVE_MAX && !hash_row(n) && !hash_quad(n) && !hash_duo(n) && n <= hash_plan().pair_max;
-}
 // lanes per pair of the Miller line kernel: 4, 2 or 1
 static int line_group(uint32_t n_main) {
   if (hash_plan().quad_max && 4ull * n_main <= TB_GROUP_LANES) return 4;
@@ -612,9 +608,7 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
   } else if (hash_duo(n)) {  // one lane pair per set, then the exact formulas for the sets it flags
     hipLaunchKernelGGL(k_set_hash_duo, dim3((2 * n + TB_BLOCK - 1) / TB_BLOCK), blk, 0, sh, b.msgs, b.msg_off, dst, dlen, n, Q, skip);
     hipLaunchKernelGGL(k_set_hash_fix, g, blk, 0, sh, b.msgs, b.msg_off, dst, dlen, n, Q, skip);
-  } else if (hash_pair(n))
-    hipLaunchKernelGGL(k_set_hash_pair, dim3((2 * n + TB_BLOCK - 1) / TB_BLOCK), blk, 0, sh, b.msgs, b.msg_off, dst, dlen, n, Q, skip);
-  else if (n && w2(n)) {  // two waves per SIMD, then the exact formulas for the sets it flags (skip == 2)
+  } else if (n && w2(n)) {  // two waves per SIMD, then the exact formulas for the sets it flags (skip == 2)
     hipLaunchKernelGGL(k_set_hash_w2, g, blk, 0, sh, b.msgs, b.msg_off, dst, dlen, n, Q, skip);
     hipLaunchKernelGGL(k_set_hash_fix, g, blk, 0, sh, b.msgs, b.msg_off, dst, dlen, n, Q, skip);
   } else if (n)

@@ -5,7 +5,6 @@
 // messages and returns their affine H(m_i) (Montgomery limbs) and skip flags,
 // for tests/test_gpu_hash_variants.py to compare with the oracle.
 //   variant 0  k_set_hash          (one lane per set; batches above 32,768 sets)
-//   variant 1  k_set_hash_pair     (two lanes per set, clearing on one; A/B only)
 //   variant 2  k_hrow_* (5 launches: field, sswu, iso, cof, fix; 513 - 4,096);
 //              force_fix != 0 sends every set through the one-lane k_hrow_fix
 //   variant 3  k_set_hash_coop     (256-thread workgroup per set; <= 512)
@@ -71,7 +70,6 @@ extern "C" int tbls_test_hash_variant(const char* product_so, int variant, const
   int rc = 0;
   switch (variant) {
     case 0: rc = launch(sym("k_set_hash"), g, BLK, a_set); break;
-    case 1: rc = launch(sym("k_set_hash_pair"), (2 * n32 + BLK - 1) / BLK, BLK, a_set); break;
     case 2:  // tb_lib.hip launch_partial's row-hash sequence
       rc = launch(sym("k_hrow_field"), g, BLK, a_field);
       if (!rc) rc = launch(sym("k_hrow_sswu"), (2 * n32 + 3) / 4, 64, a_h);

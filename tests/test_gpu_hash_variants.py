@@ -3,7 +3,7 @@
 batchVerify hashes with one of five kernels by batch size (tb_lib.hip
 launch_partial, hash_plan): k_set_hash_w2 + k_set_hash_fix (> 32,768 sets;
 k_set_hash is its one-wave A/B twin), k_set_hash_duo + k_set_hash_fix
-(8,193 - 32,768; k_set_hash_pair, the clearing on one lane, its A/B twin),
+(8,193 - 32,768),
 k_set_hash_quad + k_set_hash_fix (4,097 - 8,192), the row pipeline k_hrow_*
 (513 - 4,096) and k_set_hash_coop (<= 512; k_set_hash_wave is its
 fall-back).  Each one runs here on the same 640
@@ -32,7 +32,7 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 NUL_DST = b"BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_NUL_"
 RINV = pow(1 << 406, -1, O.P)  # Montgomery R = 2^406 (tb_fp.h)
-VARIANTS = {0: "k_set_hash", 1: "k_set_hash_pair", 2: "k_hrow_*", 3: "k_set_hash_coop", 4: "k_set_hash_wave", 5: "k_set_hash_w2 + k_set_hash_fix", 6: "k_set_hash_quad + k_set_hash_fix", 7: "k_set_hash_duo + k_set_hash_fix"}
+VARIANTS = {0: "k_set_hash", 2: "k_hrow_*", 3: "k_set_hash_coop", 4: "k_set_hash_wave", 5: "k_set_hash_w2 + k_set_hash_fix", 6: "k_set_hash_quad + k_set_hash_fix", 7: "k_set_hash_duo + k_set_hash_fix"}
 
 
 def messages():

@@ -2,13 +2,12 @@
 one-lane kernels: the row hash (k_hrow.hip: one 16-lane coop row per set, 513
 to 4,096 sets), the lane-group hash and Miller lines (k_hquad.hip: a DPP quad per
 set up to 8,192 sets, a lane pair up to 32,768; quad lines up to 16,384
-pairs, pair lines up to 32,768) and the pair hash (k_set_hash_pair, A/B).
+pairs, pair lines up to 32,768).
 The partial record of a seeded batch -- the Miller product over (P_i, H(m_i))
 and the signature pairs, canonicalized mod p -- is identical with the default
-plan (row at 600 sets, quad at 6,000, duo hash and lines at 16,384), the row,
-quad or pair hash forced at 16,384, and all of them off
-(TBLS_HASH_PLAN=0,0,0,0: k_set_hash_w2 and the one-lane line kernel), valid
-and tampered.  The exact fall-backs are pinned byte for byte by
+plan (row at 600 sets, quad at 6,000, duo hash and lines at 16,384), the row
+or quad hash forced at 16,384, and all of them off (TBLS_HASH_PLAN=0,0,0:
+k_set_hash_w2 and the one-lane line kernel), valid and tampered.  The exact fall-backs are pinned byte for byte by
 test_gpu_hash_variants.py.  The verdicts also go through the final
 exponentiation (tools/partial_record.py)."""
 
@@ -33,10 +32,10 @@ def _record(n, env_extra, tamper=-1):
     return json.loads(out.stdout.strip().splitlines()[-1])
 
 
-LANE = {"TBLS_HASH_PLAN": "0,0,0,0"}
+LANE = {"TBLS_HASH_PLAN": "0,0,0"}
 
 
-@pytest.mark.parametrize("n,env", [(600, {}), (6000, {}), (16384, {}), (16384, {"TBLS_HASH_PLAN": "32768,0,0,0"}), (16384, {"TBLS_HASH_PLAN": "0,16384,0,0"}), (16384, {"TBLS_HASH_PLAN": "0,0,0,32768"})])
+@pytest.mark.parametrize("n,env", [(600, {}), (6000, {}), (16384, {}), (16384, {"TBLS_HASH_PLAN": "32768,0,0"}), (16384, {"TBLS_HASH_PLAN": "0,16384,0"})])
 def test_row_and_pair_hash_same_product(n, env):
     fast = _record(n, env)
     lane = _record(n, LANE)
