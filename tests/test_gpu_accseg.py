@@ -22,7 +22,7 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 PLANS = [{"TBLS_ACC_PLAN": "0"}, {}, {"TBLS_ACC_PLAN": "8,4"}, {"TBLS_ACC_PLAN": "1,2"}, {"TBLS_ACC_PLAN": "4,1"},
-         {"TBLS_ACC_PLAN": "2,3"}, {"TBLS_ACC_PLAN": "8,2"}, {"TBLS_ACC_PLAN": "32,16"}, {"TBLS_ACC_PLAN": "16,5"},
+         {"TBLS_ACC_PLAN": "2,3"}, {"TBLS_ACC_PLAN": "8,2"}, {"TBLS_ACC_PLAN": "16,16"}, {"TBLS_ACC_PLAN": "16,5"},
          {"TBLS_ACC_PLAN": "2,16"}]
 
 
@@ -56,7 +56,7 @@ def test_segmented_accumulator_across_line_chunks():
     count that does not divide the chunk would misplace them; the plan only
     takes powers of two)."""
     recs = [_record(300000, p) for p in ({"TBLS_ACC_PLAN": "0"}, {}, {"TBLS_ACC_PLAN": "8,4"}, {"TBLS_ACC_PLAN": "4,3"},
-                                         {"TBLS_ACC_PLAN": "32,16"})]
+                                         {"TBLS_ACC_PLAN": "16,16"})]
     for r in recs:
         assert r["ok"] == 1 and r["n_bad"] == 0
         assert r["coords"] == recs[0]["coords"]
