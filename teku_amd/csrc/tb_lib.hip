@@ -328,7 +328,7 @@ struct pair_plan {
 // overrides the defaults (A/B; 0 disables a kernel).  (Round 3's pair kernel,
 // the SSWU maps on two lanes and the clearing on one, was removed once the
 // duo kernel replaced it: 16,384-set hash stage 5.10 -> 3.65 ms.)
-#define TB_HASH_ROW_MAX 4096u
+#define TB_HASH_ROW_MAX 1024u  // above, the quads win (4,096 sets: partial 6.98 -> 5.81 ms, profiles/r04_stage_row_vs_quad.json)
 #define TB_HASH_QUAD_MAX 8192u
 #define TB_HASH_DUO_MAX 32768u
 #define TB_GROUP_LANES 65536u  // one wave per SIMD
@@ -407,10 +407,9 @@ struct ws_layout {
 #define TB_NSTAGE_EV (2 * TB_NSTAGE)
 // Streams: keys on aux[0], signatures (+ bucket sums) on aux[1], hash_to_G2
 // on aux[2] (high priority); all three join the caller's stream before the
-// Miller loops.  At large n
-// every stage fills the GPU; at small n (config 1) the three per-set chains
-// run side by side.  `serial` (the stage-profile API) runs everything on the
-// caller's stream, for exclusive per-stage timings.
+// Miller loops (the bucket-sum pairs only before the product tree).  `serial`
+// (the stage-profile API) runs everything on the caller's stream, for
+// exclusive per-stage timings.
 
 // The large-batch one-lane kernels (hash, signature check, [r] apk) as their
 // two-waves-per-SIMD twins (k_w2_*.hip) from TB_MSM_MIN sets, where each
@@ -489,15 +488,15 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
   }
   uint8_t* w = c.ws.as<uint8_t>();
   // `serial` (tbls_dev_batch_stage_profile): every stage on the caller's
-  // stream, for exclusive per-stage timings.  Large batches: the per-set
-  // stages in sequence on the caller's stream (signatures, keys, hash -- each
-  // kernel alone fills the GPU in whole wave rounds, no tail of lone hash
-  // waves), only the bucket-sum chain on a side stream (measured 52.5 vs 53.3
-  // ms per 131k step against three concurrent streams); small batches run the
-  // three per-set chains side by side.
-  const bool chain = !serial && pp.msm;
-  hipStream_t sa = (serial || chain) ? s : c.aux[0], sb = serial ? s : c.aux[1], sh = (serial || chain) ? s : c.aux[2];
-  hipStream_t ssig = chain ? s : sb;
+  // stream, for exclusive per-stage timings.  Otherwise the three per-set
+  // chains (keys, signatures + bucket sums, hash) run side by side on their
+  // streams at every batch size.  (Rounds 2-3 ran large batches' per-set
+  // stages in sequence on the caller's stream, 52.5 vs 53.3 ms per 131k step
+  // then; with round 4's kernels side by side wins everywhere: 16,384-set
+  // partial unchanged, 32,768 sets 14.16 -> 12.44 ms, 65,536 26.11 -> 22.23,
+  // 131,072 37.73 -> 36.15, profiles/r04_stage_chain_ab.json.)
+  hipStream_t sa = serial ? s : c.aux[0], sb = serial ? s : c.aux[1], sh = serial ? s : c.aux[2];
+  hipStream_t ssig = sb;
 #define TB_EV(i, st) \
   if (ev) HIPCHK(hipEventRecord(ev[i], st))
   const dim3 blk(TB_BLOCK);
@@ -537,16 +536,12 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
                          (uint32_t*)(w + L.n_bad), 1u);
   }
   TB_EV(5, ssig);
-  if (chain) {  // the bucket sums need the decoded signatures
-    HIPCHK(hipEventRecord(c.e_sig, s));
-    HIPCHK(hipStreamWaitEvent(sb, c.e_sig, 0));
-  }
   // Large split batches: the main pairs' line kernel needs only the signature
   // codes from this stream, not the bucket sums and the extra pairs' Miller
   // loops (one 64-lane launch of ~2.5 ms): it waits on e_sig, and only the
   // product tree waits on e_join[1].
   const bool late_join = !serial && pp.msm && pp.split;
-  if (late_join && !chain) HIPCHK(hipEventRecord(c.e_sig, sb));
+  if (late_join) HIPCHK(hipEventRecord(c.e_sig, sb));
   TB_EV(8, sb);
   if (pp.msm) {
     hipLaunchKernelGGL(k_msm_bucket, dim3(TB_MSM_PARTS / TB_BLOCK), blk, 0, sb, (const g2a*)(w + L.sig_aff), (const uint8_t*)(w + L.sig_use),
@@ -621,7 +616,7 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
   HIPCHK(hipStreamWaitEvent(s, c.e_join[0], 0));
   if (!late_join)
     HIPCHK(hipStreamWaitEvent(s, c.e_join[1], 0));
-  else if (!chain)
+  else
     HIPCHK(hipStreamWaitEvent(s, c.e_sig, 0));  // the set pairs' lines read the signature codes
   // --- Miller loops of all pairs (pairs of invalid sets contribute 1) ---------
   const uint32_t np = pp.n_pairs, nf = pp.n_f();
