@@ -209,7 +209,10 @@ void place_one(placed& pl) {
 // From this many sets on, the signature side of the batch equation is a
 // bucket sum by randomizer byte with 2040 bucket pairs (k_msm_*, k_sigs.hip);
 // below it, one signature pair (-[r_i] g1, sig_i) per set.
-#define TB_MSM_MIN 32768u
+// (Round 4: 32,768 -> 12,288 sets; 16,384-set partial 8.57 -> 7.93 ms, 24,576
+// 13.65 -> 11.63, while 8,192 stays faster with per-set pairs, 6.47 vs 6.77;
+// profiles/r04_stage_msm_min.json.)
+#define TB_MSM_MIN 12288u
 #define TB_HASH_WAVE_MAX 512u  // k_set_hash_wave (one workgroup per set) up to this many sets: at 1024 its waves fill every SIMD and the key / signature stages can no longer run beside it (measured 9.8 vs 8.8 ms partial)
 #define TB_MSM_BUCKETS 2048u  // 8 windows x 256 digits (digit 0 unused)
 #define TB_MSM_NSUM 2040u     // 8 x 255 bucket sums (k_msm_bucket_sum)
@@ -412,7 +415,7 @@ struct ws_layout {
 // exclusive per-stage timings.
 
 // The large-batch one-lane kernels (hash, signature check, [r] apk) as their
-// two-waves-per-SIMD twins (k_w2_*.hip) from TB_MSM_MIN sets, where each
+// two-waves-per-SIMD twins (k_w2_*.hip) from TB_W2_MIN sets, where each
 // stage fills the GPU alone (throughput); TBLS_W2=0 selects the one-wave
 // kernels (A/B).  Below it the stages run side by side and each is a
 // latency chain: the one-wave kernels spill less, and a wave that holds the
@@ -421,9 +424,10 @@ struct ws_layout {
 // line and accumulator kernels measured slower at two waves -- 17.5 and 24.3
 // vs 14.5 ms Miller stage at 131,072 sets, profiles/r04_bench_w2_masks.json
 // -- and stay at one.)
+#define TB_W2_MIN 32768u
 static bool w2(uint32_t n) {
   static const bool v = !(getenv("TBLS_W2") && getenv("TBLS_W2")[0] == '0');
-  return v && n >= TB_MSM_MIN;
+  return v && n >= TB_W2_MIN;
 }
 // Small batches (<= TB_HASH_WAVE_MAX sets) run the key, signature and hash
 // stages, and multi-key aggregation, on the lane-cooperative kernels
