@@ -209,10 +209,18 @@ void place_one(placed& pl) {
 // From this many sets on, the signature side of the batch equation is a
 // bucket sum by randomizer byte with 2040 bucket pairs (k_msm_*, k_sigs.hip);
 // below it, one signature pair (-[r_i] g1, sig_i) per set.
-// (Round 4: 32,768 -> 12,288 sets; 16,384-set partial 8.57 -> 7.93 ms, 24,576
-// 13.65 -> 11.63, while 8,192 stays faster with per-set pairs, 6.47 vs 6.77;
-// profiles/r04_stage_msm_min.json.)
-#define TB_MSM_MIN 12288u
+// (Round 4: 32,768 -> 20,480 sets.  24,576-set batches gain -- device partial
+// 13.65 -> 11.63 ms, host-API p50 15.7 -> 12.8 -- but at 12,288 and 16,384
+// sets the host-API p50 turns bimodal, 9.6 -> 12.4 ms (best runs 9.1; most
+// likely the bucket-sum kernels still resident when the one-round quad line
+// kernel launches push some of its waves into a second round); profiles/r04_stage_msm_min.json,
+// r04_cfg4_msm_ab.json.)
+#define TB_MSM_MIN 20480u
+// TBLS_MSM_MIN overrides (tuning)
+static uint32_t msm_min() {
+  static const uint32_t v = getenv("TBLS_MSM_MIN") ? (uint32_t)atoi(getenv("TBLS_MSM_MIN")) : TB_MSM_MIN;
+  return v;
+}
 #define TB_HASH_WAVE_MAX 512u  // k_set_hash_wave (one workgroup per set) up to this many sets: at 1024 its waves fill every SIMD and the key / signature stages can no longer run beside it (measured 9.8 vs 8.8 ms partial)
 #define TB_MSM_BUCKETS 2048u  // 8 windows x 256 digits (digit 0 unused)
 #define TB_MSM_NSUM 2040u     // 8 x 255 bucket sums (k_msm_bucket_sum)
@@ -299,7 +307,7 @@ struct pair_plan {
   uint32_t n, n_extra, n_pairs, n_main, n_xwave, per, nseg;
   bool msm, wave, split;
   explicit pair_plan(uint32_t n_) : n(n_) {
-    msm = n >= TB_MSM_MIN;
+    msm = n >= msm_min();
     n_extra = msm ? TB_MSM_XPAIRS : n;
     n_pairs = n + n_extra;
     wave = n_pairs <= miller_wave_max();

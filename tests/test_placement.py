@@ -90,12 +90,12 @@ def test_bad_arguments():
     assert L.tbls_place_plan(10, None, 0, 0, None, 0, 2048, dev, cut) < 0
 
 
-@pytest.mark.parametrize("n,plan", [(131072, (16, 8)), (16384, (4, 16)), (1048576, (16, 4)), (3000, (2, 16))])
+@pytest.mark.parametrize("n,plan", [(131072, (16, 8)), (16384, (8, 16)), (1048576, (16, 4)), (3000, (2, 16))])
 def test_accumulator_plan(n, plan):
     """tb_lib.hip acc_plan (tbls_acc_plan, no device): the segmented Miller
     accumulator's pairs per thread x loop segments for the bench batch
     (131,072 sets: one 65,536-thread wave round of 16 x 8), config 4
-    (16,384 sets, bucket-sum signature side: 16,384 pairs, 4 x 16), 1,048,576 sets (262,144-pair
+    (16,384 sets, per-set signature pairs: 32,768 pairs, 8 x 16), 1,048,576 sets (262,144-pair
     chunks: 16 x 4) and 3,000 sets (6,000 pairs: 2 x 16)."""
     per, nseg, split = native.acc_plan(n)
     assert split == 1 and (per, nseg) == plan
