@@ -21,24 +21,36 @@
 using namespace tb;
 
 namespace {
-// g2_clear_cofactor_nx in an order that keeps one point besides the loop
-// state live across each [|x|] chain: t1 = [|x|]P first (its base P is live
-// anyway), then u = psi(P) - t1 and w = t1 + A, w parked in *stash (the
-// caller's LDS slot) while t3 = [|x|]u runs; out = w - t3.  The same point
-// (the group law is associative); an exceptional case anywhere ends at Z = 0
-// as in g2_clear_cofactor_nx.  (The throughput hash: the chains' live
-// points beside the doubling temporaries were spilled every iteration,
-// profiles/pmc_traffic.json.)
+// g2_clear_cofactor_nx in an order that keeps at most two points besides the
+// loop state live in registers, the caller's LDS slot *stash holding a third:
+//   stash = psi(P); t1 = [|x|]P; u = stash - t1 (= psi(P) - t1); stash = u;
+//   w = psi^2(2P) - P - stash (= t1 + A, A = psi^2(2P) - P - psi(P));
+//   u = stash; stash = w; t3 = [|x|]u; out = stash - t3.
+// The same point (the group law is associative and commutative); an
+// exceptional case anywhere ends at Z = 0 as in g2_clear_cofactor_nx.  The
+// empty asm statements with a memory clobber keep the compiler from
+// forwarding a parked point back into registers.  (Round 4: with t1, psi(P),
+// u and A live together the straight-line part spilled ~6,500 scratch
+// accesses per set, profiles/pmc_traffic.json.)
+#define TB_PARK() asm volatile("" ::: "memory")
 __device__ TB_INLINE bool g2_clear_cofactor_nx_stash(g2j& out, const g2j& p, g2j* stash) {
-  const g2j t1 = jac_mul_xabs_nx(p);
-  const g2j t2 = g2_psi(p);
-  const g2j u = jac_add_nx(t2, jac_neg(t1));
-  const g2j A = jac_add_nx(jac_add_nx(g2_psi2(jac_dbl_i(p)), jac_neg(p)), jac_neg(t2));
-  *stash = jac_add_nx(t1, A);
+  *stash = g2_psi(p);
+  TB_PARK();
+  g2j u = jac_mul_xabs_nx(p);
+  u = jac_add_nx(*stash, jac_neg(u));
+  *stash = u;
+  TB_PARK();
+  g2j w = jac_add_nx(g2_psi2(jac_dbl_i(p)), jac_neg(p));
+  w = jac_add_nx(w, jac_neg(*stash));
+  u = *stash;
+  TB_PARK();
+  *stash = w;
+  TB_PARK();
   const g2j t3 = jac_mul_xabs_nx(u);
   out = jac_add_nx(jac_neg(t3), *stash);
   return !fp2_is_zero(out.z);
 }
+#undef TB_PARK
 
 }  // namespace
 

@@ -373,10 +373,13 @@ def test_spi_prepare_complete_combinatorics(hip):
 
 
 def test_large_batch_msm_path(hip):
-    """Batches of >= 32768 sets take the bucket-MSM path for sum r_i sig_i
-    (k_sig_check + k_msm_*) instead of per-set [r_i] sig_i: valid -> True;
-    a signature on the wrong message, an infinity signature, a duplicated
-    signature pair (bucket doubling case) and a non-G2 point -> False.
+    """Batches of >= 20,480 sets take the bucket-MSM path for sum r_i sig_i
+    (k_sig_check + k_msm_*) instead of per-set [r_i] sig_i, and from 32,768
+    sets the two-wave per-set kernels (k_set_pk_w2: [r] pk with the window
+    table in LDS): valid -> True; a signature on the wrong message, an
+    infinity signature, a non-G2 point, another signer's key and the
+    infinity key -> False; a duplicated signature pair (bucket doubling
+    case) -> True.
     Keys / signatures come from the GPU generators (interop keys), which
     test_hash_sign_keys_bit_exact pins to the oracle."""
     bls, native, L, impl = hip
@@ -404,6 +407,12 @@ def test_large_batch_msm_path(hip):
     bad = list(sigs)
     bad[5] = NOT_IN_G2
     assert not _raw(bls, pks, msgs, bad, rands)
+    bad = list(pks)
+    bad[3] = pks[4]
+    assert not _raw(bls, bad, msgs, sigs, rands)
+    bad = list(pks)
+    bad[30000] = bytes([0xC0]) + bytes(47)
+    assert not _raw(bls, bad, msgs, sigs, rands)
     # the same (pk, msg, sig) twice with the same randomizer: equal points in one bucket
     dup_p, dup_m, dup_s, dup_r = list(pks), list(msgs), list(sigs), list(rands)
     dup_p[1], dup_m[1], dup_s[1], dup_r[1] = pks[0], msgs[0], sigs[0], rands[0]
