@@ -59,6 +59,33 @@ int tbls_pk_validate(const uint8_t pk[48]);
 /* BlstSignature.fromBytes + isInGroup (BlstSignature.java:35-47, 147-149). */
 int tbls_sig_validate(const uint8_t sig[96], int* is_inf);
 
+/* ---- host decoding: BlstPublicKey.fromBytes / BlstSignature.fromBytes ----
+ * (BlstPublicKey.java:38-45, BlstSignature.java:35-47: P1_Affine / P2_Affine
+ * deserialization = blst_p1/p2_uncompress, no subgroup check).  Decided on
+ * the CALLER'S THREAD with no device call and no tbls_init needed: flags,
+ * x < p, the curve equation has a root, x != 0.  Returns TBLS_SUCCESS,
+ * TBLS_BAD_ENCODING, TBLS_POINT_NOT_ON_CURVE or TBLS_POINT_NOT_IN_GROUP (x = 0,
+ * blst's "(0, +-2) is not in group"); *is_inf (nullable) = 1 for the
+ * canonical infinity encoding.  The SPI's fromBytes throws BlsException on any
+ * non-success code; the subgroup check stays with isInGroup / isValid
+ * (tbls_sig_validate, tbls_pk_validate, the *_many forms) and the batch. */
+int tbls_pk_decode(const uint8_t pk[48], int* is_inf);
+int tbls_sig_decode(const uint8_t sig[96], int* is_inf);
+/* The same for n items (codes[i], is_inf[i] nullable), spread over up to 16
+ * host threads: one call for a whole gossip batch of fresh objects. */
+int tbls_pk_decode_many(const uint8_t* pks, size_t n, uint8_t* codes, uint8_t* is_inf);
+int tbls_sig_decode_many(const uint8_t* sigs, size_t n, uint8_t* codes, uint8_t* is_inf);
+
+/* Call counters since load (or the last reset): out[0] batch pipelines queued,
+ * out[1] single-object device validations (tbls_pk_validate /
+ * tbls_sig_validate), out[2] helper device calls (hash, sign, aggregate,
+ * *_many, single verifications), out[3] per-set verdict passes
+ * (tbls_verify_each chunks), out[4] final exponentiations, out[5] points
+ * decoded on the host, out[6] failed batches settled from their own Miller
+ * values.  Entries past 7 are 0.  reset != 0 zeroes them after reading.
+ * Observability for services (what a workload cost the device). */
+int tbls_stats(uint64_t* out, size_t n, int reset);
+
 /* BLS12381.aggregatePublicKeys -> BlstPublicKey.aggregate
  * (BLS12381.java:95, BlstPublicKey.java:55-71): k >= 1; any invalid key makes
  * the result the infinity key.  Decode failures -> TBLS_BAD_ENCODING etc. */
@@ -105,8 +132,8 @@ typedef struct {
  * BlstBLS12381.java:112-189).  rand[i] in [1, 2^64] as BlstBLS12381
  * .nextBatchRandomMultiplier (l.191-195) -- the caller owns the RNG.  n_gpus:
  * at most that many devices (0 = all initialised devices); the batch goes to
- * the least-loaded device, or is sharded over several when it has at least
- * 2 x tbls_shard_min() sets (tbls_place_plan); each device produces one Fp12
+ * the least-loaded device, or is sharded over several idle ones when it has at
+ * least 2 x tbls_shard_min() sets (tbls_place_plan); each device produces one Fp12
  * partial product, gathered for one final exponentiation.  *ok = 1 iff every set is valid and the pairing product is
  * 1.  n == 0 -> *ok = 0 (BLS.java:240-241).  A set with n_pks == 0 ->
  * TBLS_BAD_ARGUMENT (BlstPublicKey.aggregate checkArgument, l.56). */
@@ -220,19 +247,20 @@ int tbls_acc_plan(uint32_t n, uint32_t* per, uint32_t* nseg, int* split);
  * work), the function tbls_batch_verify / tbls_verify_each / the single-call
  * entries use (tb_lib.hip place_plan): n sets (n_pks[i] keys
  * each; NULL = one key each) over n_devices devices with load[d] batches in
- * flight (NULL = idle) are sharded over
- *   G = min(n_devices capped by n_gpus > 0, max(1, n / shard_min_sets))
- * devices (shard_min_sets = 0: all of them) -- the G least-loaded ones,
+ * flight (NULL = all idle) are sharded over
+ *   G = min(idle devices, n_devices capped by n_gpus > 0, max(1, n / shard_min_sets))
+ * devices (shard_min_sets = 0: every allowed idle device) -- idle ones only,
  * ties broken round-robin from rr, in ascending order in dev_out[0..G) (the
- * first is the gather root) -- with contiguous shards balanced by key count:
- * device dev_out[k] gets sets [cut_out[k], cut_out[k+1]) (cut_out: G + 1
- * entries).  Returns G >= 1, or -TBLS_BAD_ARGUMENT.  A concurrent caller of
- * the live library sees the devices its batch holds as loaded, so N service
- * workers with small batches land on N different devices
+ * first is the gather root); with no idle device, the least-loaded one --
+ * with contiguous shards balanced by key count: device dev_out[k] gets sets
+ * [cut_out[k], cut_out[k+1]) (cut_out: G + 1 entries).  Returns G >= 1, or
+ * -TBLS_BAD_ARGUMENT.  A concurrent caller of the live library sees the
+ * devices other batches hold as loaded, so N service workers with
+ * config-4-sized batches land on N different devices, one each
  * (AggregatingSignatureVerificationService.java:121-132, 202-205). */
 int tbls_place_plan(size_t n, const uint32_t* n_pks, int n_devices, int n_gpus, const int* load, uint32_t rr, uint32_t shard_min_sets,
                     int* dev_out, size_t* cut_out);
-/* The live shard_min_sets (2048, or TBLS_SHARD_MIN). */
+/* The live shard_min_sets (32768, or TBLS_SHARD_MIN). */
 uint32_t tbls_shard_min(void);
 
 /* Multiply g partial records (device memory, contiguous) and run the final

@@ -1,7 +1,9 @@
 /*
- * PublicKey (impl/PublicKey.java) over the compressed bytes; validity
- * (!infinity && in G1) computed on the device and memoised, as
- * BlstPublicKey.java:74-75.  Mirror: teku_amd/bls.py HipPublicKey.
+ * PublicKey (impl/PublicKey.java) over the compressed bytes.  fromBytes
+ * decodes on the calling thread (tbls_pk_decode: blst_p1_uncompress's checks,
+ * no device call); validity (!infinity && in G1) is computed on the device
+ * when first asked and memoised, as BlstPublicKey.java:74-75.  Mirror:
+ * teku_amd/bls.py HipPublicKey.
  */
 package tech.pegasys.teku.bls.impl.hip;
 
@@ -32,14 +34,12 @@ final class HipPublicKey implements PublicKey {
   /* BlstPublicKey.fromBytes: decode failures throw (BlstPublicKey.java:38-45) */
   static HipPublicKey fromBytes(final Bytes48 compressed) {
     final byte[] b = compressed.toArrayUnsafe();
-    final int code = TekuBlsHip.pkValidate(b);
-    if (code == TekuBlsHip.BAD_ENCODING || code == TekuBlsHip.POINT_NOT_ON_CURVE) {
+    // BAD_ENCODING, POINT_NOT_ON_CURVE, or POINT_NOT_IN_GROUP for x = 0 (blst:
+    // "(0, +-2) is not in group"): P1_Affine throws
+    if (TekuBlsHip.pkDecode(b) != TekuBlsHip.SUCCESS) {
       throw new BlsException("Deserialization of public key bytes failed: " + compressed);
     }
-    if (code == TekuBlsHip.DEVICE_ERROR) {
-      throw new BlsException("GPU BLS backend: device error");
-    }
-    return new HipPublicKey(b, code);
+    return new HipPublicKey(b, null);
   }
 
   static HipPublicKey fromPublicKey(final PublicKey pk) {
@@ -97,7 +97,11 @@ final class HipPublicKey implements PublicKey {
   public boolean isValid() {
     Boolean v = valid;
     if (v == null) {
-      v = TekuBlsHip.pkValidate(bytes) == TekuBlsHip.SUCCESS;
+      final int rc = TekuBlsHip.pkValidate(bytes);
+      if (rc == TekuBlsHip.DEVICE_ERROR) {
+        throw new BlsException("GPU BLS backend: device error");
+      }
+      v = rc == TekuBlsHip.SUCCESS;
       valid = v;
     }
     return v;

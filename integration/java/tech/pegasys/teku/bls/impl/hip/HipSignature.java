@@ -1,7 +1,10 @@
 /*
  * Signature (impl/Signature.java) over the compressed bytes.  Mirror:
- * teku_amd/bls.py HipSignature.  Failures of the device are BlsExceptions,
- * the failure mode of a broken blst load.
+ * teku_amd/bls.py HipSignature.  fromBytes decodes on the calling thread
+ * (tbls_sig_decode: blst_p2_uncompress's checks, no device call); the G2
+ * subgroup check runs on the device when isInGroup is first asked, memoised,
+ * or inside the batch.  Failures of the device are BlsExceptions, the failure
+ * mode of a broken blst load.
  */
 package tech.pegasys.teku.bls.impl.hip;
 
@@ -20,6 +23,7 @@ final class HipSignature implements Signature {
   static final byte[] ETH2_DST = "BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_POP_".getBytes(StandardCharsets.US_ASCII);
 
   private final byte[] bytes;
+  private volatile Boolean inGroup;
 
   HipSignature(final byte[] compressed) {
     this.bytes = compressed.clone();
@@ -31,12 +35,9 @@ final class HipSignature implements Signature {
       throw new BlsException("Expected 96 bytes of input but got " + compressed.size());
     }
     final byte[] b = compressed.toArrayUnsafe();
-    final int code = TekuBlsHip.sigValidate(b, new int[1]);
-    if (code == TekuBlsHip.BAD_ENCODING || code == TekuBlsHip.POINT_NOT_ON_CURVE) {
+    // BAD_ENCODING, POINT_NOT_ON_CURVE, or POINT_NOT_IN_GROUP for x = 0: P2_Affine throws
+    if (TekuBlsHip.sigDecode(b) != TekuBlsHip.SUCCESS) {
       throw new BlsException("Deserialization of signature bytes failed: " + compressed);
-    }
-    if (code == TekuBlsHip.DEVICE_ERROR) {
-      throw new BlsException("GPU BLS backend: device error");
     }
     return new HipSignature(b);
   }
@@ -111,9 +112,24 @@ final class HipSignature implements Signature {
     return Arrays.equals(bytes, INFINITY);
   }
 
+  // BlstSignature.isInGroup (BlstSignature.java:147-149), memoised: one
+  // device check per object at most; the infinity point is in the group
   @Override
   public boolean isInGroup() {
-    return TekuBlsHip.sigValidate(bytes, new int[1]) == TekuBlsHip.SUCCESS;
+    Boolean g = inGroup;
+    if (g == null) {
+      if (isInfinity()) {
+        g = Boolean.TRUE;
+      } else {
+        final int rc = TekuBlsHip.sigValidate(bytes, new int[1]);
+        if (rc == TekuBlsHip.DEVICE_ERROR) {
+          throw new BlsException("GPU BLS backend: device error");
+        }
+        g = rc == TekuBlsHip.SUCCESS;
+      }
+      inGroup = g;
+    }
+    return g;
   }
 
   // BlstSignature.java:152-165: the compressed bytes' hash, and equal to any

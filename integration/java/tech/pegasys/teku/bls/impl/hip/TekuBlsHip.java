@@ -24,6 +24,12 @@ final class TekuBlsHip {
   static native void shutdown(); // tbls_shutdown
   static native int deviceCount(); // tbls_device_count
 
+  /* host decoding, no device call: BlstPublicKey / BlstSignature.fromBytes */
+  static native int pkDecode(byte[] pk48); // tbls_pk_decode
+  static native int sigDecode(byte[] sig96); // tbls_sig_decode
+  static native int pkDecodeMany(byte[] pks, int n, byte[] codes); // tbls_pk_decode_many
+  static native int sigDecodeMany(byte[] sigs, int n, byte[] codes); // tbls_sig_decode_many
+
   static native int pkValidate(byte[] pk48); // tbls_pk_validate
   static native int sigValidate(byte[] sig96, int[] isInf); // tbls_sig_validate
   static native int aggregatePks(byte[] pks, int k, byte[] out48); // tbls_aggregate_pks

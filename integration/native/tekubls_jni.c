@@ -128,6 +128,53 @@ JNIEXPORT jint JNICALL JNAME(sigValidate)(JNIEnv* env, jclass c, jbyteArray sig,
   return rc;
 }
 
+/* host decoding: BlstPublicKey / BlstSignature.fromBytes without a device call */
+JNIEXPORT jint JNICALL JNAME(pkDecode)(JNIEnv* env, jclass c, jbyteArray pk) {
+  (void)c;
+  jbyte b[48];
+  if (fixed_in(env, pk, b, 48)) return TBLS_BAD_ENCODING;
+  return tbls_pk_decode((const uint8_t*)b, NULL);
+}
+
+JNIEXPORT jint JNICALL JNAME(sigDecode)(JNIEnv* env, jclass c, jbyteArray sig) {
+  (void)c;
+  jbyte b[96];
+  if (fixed_in(env, sig, b, 96)) return TBLS_BAD_ENCODING;
+  return tbls_sig_decode((const uint8_t*)b, NULL);
+}
+
+/* n items of `width` bytes -> n codes (decode_many: tbls_pk_decode_many / tbls_sig_decode_many) */
+static jint decode_many(JNIEnv* env, jbyteArray items, jint n, jbyteArray codes, size_t width,
+                        int (*decode_many)(const uint8_t*, size_t, uint8_t*, uint8_t*)) {
+  jsize il;
+  int rc = TBLS_SUCCESS;
+  if (n < 0 || alen(env, codes) < n) return TBLS_BAD_ARGUMENT;
+  uint8_t* p = bytes_in(env, items, &il, &rc);
+  if (!p) return rc;
+  uint8_t* cd = (uint8_t*)malloc(n ? (size_t)n : 1);
+  if (!cd) {
+    rc = TBLS_DEVICE_ERROR;
+  } else if ((size_t)il < width * (size_t)n) {
+    rc = TBLS_BAD_ARGUMENT;
+  } else {
+    rc = decode_many(p, (size_t)n, cd, NULL);
+    if (n) (*env)->SetByteArrayRegion(env, codes, 0, n, (const jbyte*)cd);
+  }
+  free(cd);
+  free(p);
+  return rc;
+}
+
+JNIEXPORT jint JNICALL JNAME(pkDecodeMany)(JNIEnv* env, jclass c, jbyteArray pks, jint n, jbyteArray codes) {
+  (void)c;
+  return decode_many(env, pks, n, codes, 48, tbls_pk_decode_many);
+}
+
+JNIEXPORT jint JNICALL JNAME(sigDecodeMany)(JNIEnv* env, jclass c, jbyteArray sigs, jint n, jbyteArray codes) {
+  (void)c;
+  return decode_many(env, sigs, n, codes, 96, tbls_sig_decode_many);
+}
+
 JNIEXPORT jint JNICALL JNAME(aggregatePks)(JNIEnv* env, jclass c, jbyteArray pks, jint k, jbyteArray out) {
   (void)c;
   jsize n;
@@ -273,7 +320,8 @@ static tbls_set* sets_of(const uint8_t* pk, const int32_t* np, const uint8_t* m,
 
 /* the common inputs of batchVerify / verifyEach, copied and checked */
 typedef struct {
-  jsize n, n_off, ml, pl, sl;
+  jsize n, n_off, ml, sl;
+  size_t pl_bytes; /* key bytes (48 per key, or 4 per table index) */
   int32_t *np, *mo;
   uint8_t *pk, *m, *sg;
 } flat_sets;
@@ -297,16 +345,18 @@ static int flat_in(JNIEnv* env, flat_sets* f, jbyteArray pks, jintArray keyIdx, 
     if (keyIdx) {
       jsize ni;
       f->pk = (uint8_t*)ints_in(env, keyIdx, &ni, &rc);
-      f->pl = ni * 4;
+      f->pl_bytes = 4u * (size_t)ni; /* in size_t: 2^29 or more indices would overflow a jsize */
     } else {
-      f->pk = bytes_in(env, pks, &f->pl, &rc);
+      jsize pl;
+      f->pk = bytes_in(env, pks, &pl, &rc);
+      f->pl_bytes = (size_t)pl;
     }
   }
   if (f->pk) f->m = bytes_in(env, msgs, &f->ml, &rc);
   if (f->m) f->sg = bytes_in(env, sigs, &f->sl, &rc);
   if (!f->sg) return rc;
   const size_t unit = keyIdx ? 4 : 48;
-  if (!sets_shape_ok(f->np, f->n, f->mo, f->n_off, f->ml, (size_t)f->pl / unit) || (size_t)f->sl < 96u * (size_t)f->n)
+  if (!sets_shape_ok(f->np, f->n, f->mo, f->n_off, f->ml, f->pl_bytes / unit) || (size_t)f->sl < 96u * (size_t)f->n)
     return TBLS_BAD_ARGUMENT;
   return TBLS_SUCCESS;
 }
@@ -476,7 +526,9 @@ JNIEXPORT jint JNICALL JNAME(aggregateSigsMany)(JNIEnv* env, jclass c, jbyteArra
   (void)c;
   jsize sl, no;
   int rc = TBLS_SUCCESS;
-  if (groups < 0 || alen(env, out) < 96 * (jsize)groups || alen(env, status) < groups) return TBLS_BAD_ARGUMENT;
+  /* the output length in size_t: 96 * groups overflows a jsize from 22.4 M groups */
+  if (groups < 0 || alen(env, out) < 0 || (size_t)alen(env, out) < 96u * (size_t)groups || alen(env, status) < groups)
+    return TBLS_BAD_ARGUMENT;
   uint8_t* s = bytes_in(env, sigs, &sl, &rc);
   int32_t* o = s ? ints_in(env, off, &no, &rc) : NULL;
   if (o) {

@@ -114,10 +114,16 @@ class Signature:
         return java_bytes_hash(self.to_bytes_compressed())
 
 
+def _decode_failed(what: str, b: bytes) -> BlsException:
+    return BlsException(f"Deserialization of {what} bytes failed: 0x" + bytes(b).hex())
+
+
 class HipPublicKey(PublicKey):
     """impl/PublicKey.java:20-82 (BlstPublicKey.java analogue).  Holds the
-    compressed bytes; validity (!infinity && in G1) is computed on the GPU and
-    memoised (BlstPublicKey.java:74-75)."""
+    compressed bytes.  from_bytes decodes on the host (tbls_pk_decode: flags,
+    x < p, on the curve, x != 0 -- blst_p1_uncompress's contract, no device
+    call); validity (!infinity && in G1) is computed on the GPU when first
+    asked and memoised (BlstPublicKey.java:74-75)."""
 
     __slots__ = ("_b", "_valid", "_inf")
 
@@ -131,14 +137,10 @@ class HipPublicKey(PublicKey):
         # BlstPublicKey.fromBytes: decode failures throw (l.38-45)
         if len(compressed) != 48:
             raise BlsException("Deserialization of public key bytes failed")
-        code = native.lib().tbls_pk_validate(bytes(compressed))
-        if code in (native.BAD_ENCODING, native.POINT_NOT_ON_CURVE):
-            raise BlsException("Deserialization of public key bytes failed: 0x" + bytes(compressed).hex())
-        if code == native.POINT_NOT_IN_GROUP and compressed[0] & 0x1F == 0 and not any(compressed[1:]):
-            raise BlsException("Deserialization of public key bytes failed: 0x" + bytes(compressed).hex())
-        if code == native.DEVICE_ERROR:
-            raise native.NativeError(code, "tbls_pk_validate")
-        return HipPublicKey(compressed, code)
+        b = bytes(compressed)
+        if native.host().tbls_pk_decode(b, None) != native.SUCCESS:
+            raise _decode_failed("public key", b)
+        return HipPublicKey(b)
 
     def to_bytes_compressed(self) -> bytes:
         return self._b
@@ -148,7 +150,10 @@ class HipPublicKey(PublicKey):
 
     def is_valid(self) -> bool:
         if self._valid is None:
-            self._valid = native.lib().tbls_pk_validate(self._b) == native.SUCCESS
+            rc = native.lib().tbls_pk_validate(self._b)
+            if rc == native.DEVICE_ERROR:
+                raise native.NativeError(rc, "tbls_pk_validate")
+            self._valid = rc == native.SUCCESS
         return self._valid
 
     def is_in_group(self) -> bool:
@@ -164,27 +169,26 @@ class HipPublicKey(PublicKey):
 
 
 class HipSignature(Signature):
-    """impl/Signature.java:20-91 (BlstSignature.java analogue)."""
+    """impl/Signature.java:20-91 (BlstSignature.java analogue).  from_bytes
+    decodes on the host (tbls_sig_decode: blst_p2_uncompress's contract, no
+    device call); the G2 subgroup check runs on the GPU when first asked
+    (is_in_group, memoised) or inside the batch."""
 
-    __slots__ = ("_b",)
+    __slots__ = ("_b", "_in_group")
 
     def __init__(self, compressed: bytes):
         self._b = bytes(compressed)
+        self._in_group = None
 
     @staticmethod
     def from_bytes(compressed: bytes) -> "HipSignature":
         # BlstSignature.fromBytes: size check + decode, failures -> BlsException (l.35-47)
         if len(compressed) != 96:
             raise BlsException(f"Expected 96 bytes of input but got {len(compressed)}")
-        inf = ctypes.c_int(0)
-        code = native.lib().tbls_sig_validate(bytes(compressed), ctypes.byref(inf))
-        if code in (native.BAD_ENCODING, native.POINT_NOT_ON_CURVE):
-            raise BlsException("Deserialization of signature bytes failed: 0x" + bytes(compressed).hex())
-        if code == native.POINT_NOT_IN_GROUP and bytes(compressed[1:48]) == bytes(47) and compressed[0] & 0x1F == 0 and bytes(compressed[48:]) == bytes(48):
-            raise BlsException("Deserialization of signature bytes failed")
-        if code == native.DEVICE_ERROR:
-            raise native.NativeError(code, "tbls_sig_validate")
-        return HipSignature(compressed)
+        b = bytes(compressed)
+        if native.host().tbls_sig_decode(b, None) != native.SUCCESS:
+            raise _decode_failed("signature", b)
+        return HipSignature(b)
 
     def to_bytes_compressed(self) -> bytes:
         return self._b
@@ -193,8 +197,17 @@ class HipSignature(Signature):
         return self._b == INFINITY_G2
 
     def is_in_group(self) -> bool:
-        inf = ctypes.c_int(0)
-        return native.lib().tbls_sig_validate(self._b, ctypes.byref(inf)) == native.SUCCESS
+        # BlstSignature.isInGroup (l.147-149): ec2Point.in_group(); the infinity
+        # point is in the group
+        if self._in_group is None:
+            if self.is_infinity():
+                self._in_group = True
+            else:
+                rc = native.lib().tbls_sig_validate(self._b, None)
+                if rc == native.DEVICE_ERROR:
+                    raise native.NativeError(rc, "tbls_sig_validate")
+                self._in_group = rc == native.SUCCESS
+        return self._in_group
 
     # Signature.verify overloads (Signature.java:36-68)
     def verify(self, public_key_or_keys, message: bytes = None, dst=None) -> bool:
@@ -759,6 +772,9 @@ class BLS:
             count = len(public_keys)
             if count == 0:
                 return False
+            impl = BLS.get_bls_impl()
+            if type(impl) is HipBLS12381 and not impl.eager:
+                return _hip_facade_batch(impl, public_keys, messages, signatures, double_pairing)
             prepared = []
             if double_pairing:
                 for i in range(0, count, 2):
@@ -799,3 +815,71 @@ class BLS:
         if BLS.verification_disabled:
             return True
         return BLS.get_bls_impl().complete_batch_verify(prepared)
+
+
+# ---------------------------------------------------------------------------
+# The facade's batch path on HipBLS12381
+# ---------------------------------------------------------------------------
+def predecode(public_keys=(), signatures=()) -> None:
+    """Decode every not-yet-decoded BLSPublicKey / BLSSignature in two host
+    calls (tbls_pk_decode_many / tbls_sig_decode_many, spread over host
+    threads, no device call): the verdicts and memoisation of calling
+    get_public_key() / get_signature() on each (BLSSignature.java:83-87,
+    BLSPublicKey.java:116-120) when the installed implementation is
+    HipBLS12381, whose from_bytes is that host decode.  Objects that do not
+    decode stay undecoded: get_*() raises for them as before."""
+    for objs, many, width, make in (
+        (signatures, "tbls_sig_decode_many", 96, HipSignature),
+        (public_keys, "tbls_pk_decode_many", 48, HipPublicKey),
+    ):
+        todo = [o for o in objs if type(o) in (BLSSignature, BLSPublicKey) and o._impl is None and len(o._b) == width]
+        if not todo:
+            continue
+        codes = ctypes.create_string_buffer(len(todo))
+        native.check(getattr(native.host(), many)(b"".join(o._b for o in todo), len(todo), codes, None), many)
+        for o, c in zip(todo, codes.raw):
+            if c == native.SUCCESS:
+                o._impl = make(o._b)
+
+
+def _hip_facade_batch(impl, public_keys, messages, signatures, double_pairing) -> bool:
+    """BLS.batchVerify's 5-argument body (BLS.java:297-336) on HipBLS12381,
+    without the per-set semi-aggregate objects: HipBLS12381.prepareBatchVerify
+    only captures bytes, so the verdict and the exceptions are those of the
+    prepare / complete loop -- a unit (a pair of sets with double_pairing,
+    BLS.java:306-322, else one set) with an undecodable key or signature is
+    an InvalidBatchSemiAggregate (the batch is false); otherwise an empty key
+    list raises (BlstPublicKey.aggregate's checkArgument) -- and all sets go
+    to the device as one tbls_batch_verify.  Decoding is one multi-threaded
+    host call per batch (predecode)."""
+    from .synth import SetArray, fast_multipliers
+
+    key_lists = [list(ks) for ks in public_keys]
+    predecode([k for ks in key_lists for k in ks], signatures)
+
+    def decoded(o):
+        if isinstance(o, (BLSPublicKey, BLSSignature)):
+            return o._impl is not None
+        try:
+            _as_pk(o) if isinstance(o, (PublicKey, HipPublicKey)) else _as_sig(o)
+            return True
+        except BlsException:
+            return False
+
+    n = len(key_lists)
+    ok_dec = [all(decoded(k) for k in key_lists[i]) and decoded(signatures[i]) for i in range(n)]
+    step = 2 if double_pairing else 1
+    invalid = False
+    for i in range(0, n, step):
+        unit = range(i, min(n, i + step))
+        if not all(ok_dec[j] for j in unit):
+            invalid = True
+        elif any(len(key_lists[j]) == 0 for j in unit):
+            raise ValueError("empty public key list")
+    if invalid:
+        return False
+    pk_blob = b"".join(k.to_bytes_compressed() for ks in key_lists for k in ks)
+    msgs = [bytes(m) for m in messages]
+    arr = SetArray(pk_blob, [len(ks) for ks in key_lists], b"".join(msgs), [len(m) for m in msgs],
+                   b"".join(sg.to_bytes_compressed() for sg in signatures))
+    return arr.batch_verify(fast_multipliers(n), impl.n_gpus)

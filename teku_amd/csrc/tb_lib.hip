@@ -117,22 +117,32 @@ size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
 // Placement of a batch on the devices.  The reference runs
 // numThreads service workers side by side, each with its own batch
 // (AggregatingSignatureVerificationService.java:121-132, 202-205), so a
-// device should hold one caller's batch, not every caller's:
-//  * a batch of n sets is sharded over G = min(D', floor(n / shard_min)) >= 1
-//    devices (D' = the initialised devices, capped by n_gpus > 0), so a shard
-//    never drops below shard_min sets: below ~2,048 sets a device's partial is
-//    latency-bound (5.7 ms at 1,024 sets, 9.3 ms at 4,096, 12.3 ms at 16,384
-//    on one MI355X), and splitting it further gains
-//    little while it takes every device from every other caller;
-//  * the G devices are the least-loaded ones (batches placed and not yet
-//    finished), ties broken round-robin from a counter, then taken in
-//    ascending order (lock order; the lowest is the gather root);
+// device should hold one caller's batch, not a slice of every caller's:
+//  * a batch is sharded only over devices that are IDLE at placement time
+//    (no batch in flight), and only into shards of at least shard_min sets:
+//    G = min(idle devices, n_gpus cap, floor(n / shard_min)) >= 1.
+//    shard_min = 32,768 sets, where one MI355X's partial stops being a
+//    latency chain (profiles/r04_stage_sweep_final.json, device partial:
+//    16,384 sets 8.6 ms = 1.9 M sets/s, 32,768 sets 12.5 ms = 2.6 M/s, 65,536
+//    21.8 ms = 3.0 M/s, 131,072 37.4 ms = 3.5 M/s); below it a second device
+//    buys a lone batch a few ms of latency and costs every concurrent caller a
+//    whole device.  So a lone 131,072-set batch runs as 4 shards of 32,768,
+//    1,048,576 sets over all 8 devices, and 8 workers with 16,384-set batches
+//    (config 4) take 8 different devices, one each;
+//  * with no idle device the batch goes whole to the least-loaded one;
+//  * among equals, ties are broken round-robin from a counter; the chosen
+//    devices are taken in ascending order (lock order; the lowest is the
+//    gather root);
 //  * shards are contiguous and balanced by key count, as teku_amd/dist.py
 //    shard_bounds.
-// TBLS_SHARD_MIN overrides shard_min (0: always every allowed device).
+// (Round 4 sharded any batch of 2 x 2,048 sets over the least-loaded devices
+// whatever their load: a 16,384-set batch took all 8 devices and concurrent
+// workers serialized on them -- about 2.5 M sigs/s for the node where one
+// batch per device gives about 13.9 M)
+// TBLS_SHARD_MIN overrides shard_min (0: every allowed idle device).
 // tbls_place_plan exposes the same function for CPU tests.
 // ---------------------------------------------------------------------------
-#define TB_SHARD_MIN 2048u
+#define TB_SHARD_MIN 32768u
 uint32_t shard_min() {
   static const uint32_t v = getenv("TBLS_SHARD_MIN") ? (uint32_t)atoi(getenv("TBLS_SHARD_MIN")) : TB_SHARD_MIN;
   return v;
@@ -143,17 +153,20 @@ uint32_t shard_min() {
 template <class KEYS>
 int place_plan(size_t n, const KEYS& keys, int D, int n_gpus, const int* load, uint32_t rr, uint32_t smin, int* dev, size_t* cut) {
   if (D < 1) return 0;
-  int Gmax = (n_gpus > 0 && n_gpus < D) ? n_gpus : D;
-  size_t g = smin ? n / smin : (size_t)Gmax;
-  int G = (int)std::min<size_t>(std::max<size_t>(g, 1), (size_t)Gmax);
-  if ((size_t)G > n) G = n ? (int)n : 1;
+  const int Gmax = (n_gpus > 0 && n_gpus < D) ? n_gpus : D;
   std::vector<int> order(D);
   for (int d = 0; d < D; d++) order[d] = d;
+  // least loaded first, ties round-robin from rr
   std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
     const int la = load ? load[a] : 0, lb = load ? load[b] : 0;
     if (la != lb) return la < lb;
     return (uint32_t)(a - (int)(rr % (uint32_t)D) + D) % (uint32_t)D < (uint32_t)(b - (int)(rr % (uint32_t)D) + D) % (uint32_t)D;
   });
+  int idle = 0;
+  while (idle < D && (!load || load[order[idle]] == 0)) idle++;
+  const size_t g = smin ? n / smin : (size_t)Gmax;
+  int G = (int)std::min<size_t>(std::max<size_t>(g, 1), (size_t)std::min(Gmax, std::max(idle, 1)));
+  if ((size_t)G > n) G = n ? (int)n : 1;
   std::sort(order.begin(), order.begin() + G);
   for (int k = 0; k < G; k++) dev[k] = order[k];
   uint64_t totalK = 0;
@@ -277,9 +290,17 @@ static void acc_env(int& e_per, int& e_seg) {
     e_seg = g;
   }
 }
+struct acc_env_t {
+  int per, seg;
+};
 static void acc_plan(uint32_t n_main, uint32_t& per, uint32_t& nseg) {
-  static int e_per = -2, e_seg = -2;
-  if (e_per == -2) acc_env(e_per, e_seg);
+  // read once, thread-safe (C++11 magic static): concurrent batch callers plan at once
+  static const acc_env_t env = [] {
+    acc_env_t e;
+    acc_env(e.per, e.seg);
+    return e;
+  }();
+  const int e_per = env.per, e_seg = env.seg;
   if (e_seg == 0) {  // the unsegmented kernels
     per = n_main >= TB_MILLER_PER2_MIN ? 2u : 1u;
     nseg = 1;
@@ -493,6 +514,7 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
   const uint32_t K = use_tab ? 0 : b.n_keys;
   const pair_plan pp(n);
   L = ws_layout(pp, K);
+  tb::stat_add(tb::TB_STAT_PARTIALS);
   HIPCHK(ws_acquire(c, s));
   if (L.total > c.ws.cap) {  // growing frees the old buffer: drain its users first
     HIPCHK(hipStreamSynchronize(s));
@@ -719,6 +741,7 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
 int launch_final(dev_ctx& c, const void* recs, uint32_t g, hipStream_t s, int* result_host) {
   if (c.fin.ensure(256)) return TBLS_DEVICE_ERROR;
   int* res = c.fin.as<int>();
+  tb::stat_add(tb::TB_STAT_FINALS);
   tb_launch_final_recs((const uint8_t*)recs, g, s, res);
   HIPCHK(hipGetLastError());
   if (c.hout.ensure(16)) return TBLS_DEVICE_ERROR;
@@ -1033,6 +1056,7 @@ int with_device(const std::function<int(dev_ctx&)>& fn) {
   if (ensure_init()) return TBLS_DEVICE_ERROR;
   placed pl;
   place_one(pl);
+  tb::stat_add(tb::TB_STAT_HELPERS);
   dev_ctx* c = ctx_for(pl.dev[0]);
   std::lock_guard<std::mutex> lk(c->mu);
   HIPCHK(hipSetDevice(c->dev));
@@ -1315,6 +1339,7 @@ static int run_each(int d, const tbls_set* sets, size_t lo, size_t hi, uint8_t* 
   dev_ctx* c = ctx_for(d);
   if (!c) return TBLS_DEVICE_ERROR;
   std::lock_guard<std::mutex> lk(c->mu);
+  tb::stat_add(tb::TB_STAT_EACH);
   HIPCHK(hipSetDevice(c->dev));
   packed p = pack_layout(sets, lo, hi, 43);
   if (c->hin.ensure(p.total + 256) || c->in.ensure(p.total + 256)) return TBLS_DEVICE_ERROR;
@@ -1444,6 +1469,7 @@ extern "C" int tbls_aggregate_verify(const uint8_t* pks, const uint8_t* const* m
 }
 
 extern "C" int tbls_pk_validate(const uint8_t pk[48]) {
+  tb::stat_add(tb::TB_STAT_ONE_VALIDATE);
   return with_device([&](dev_ctx& c) -> int {
     upload u;
     size_t o = u.add(pk, 48);
@@ -1459,6 +1485,7 @@ extern "C" int tbls_pk_validate(const uint8_t pk[48]) {
 }
 
 extern "C" int tbls_sig_validate(const uint8_t sig[96], int* is_inf) {
+  tb::stat_add(tb::TB_STAT_ONE_VALIDATE);
   return with_device([&](dev_ctx& c) -> int {
     upload u;
     size_t o = u.add(sig, 96);

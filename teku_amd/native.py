@@ -81,6 +81,11 @@ _SIGS = {
     "tbls_device_count": (ctypes.c_int, []),
     "tbls_pk_validate": (ctypes.c_int, [ctypes.c_char_p]),
     "tbls_sig_validate": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int)]),
+    "tbls_pk_decode": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int)]),
+    "tbls_sig_decode": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int)]),
+    "tbls_pk_decode_many": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_char_p]),
+    "tbls_sig_decode_many": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_char_p]),
+    "tbls_stats": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint64), ctypes.c_size_t, ctypes.c_int]),
     "tbls_aggregate_pks": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p]),
     "tbls_aggregate_sigs": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p]),
     "tbls_hash_to_g2": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p]),
@@ -176,16 +181,78 @@ _SIGS = {
 EXPORTED = tuple(_SIGS)
 
 
+def _loaded_hip_runtimes():
+    """Paths of the libamdhip64 copies mapped into this process."""
+    try:
+        with open("/proc/self/maps") as f:
+            return sorted({line.split()[-1] for line in f if "libamdhip64" in line and "/" in line})
+    except OSError:
+        return []
+
+
+def _preload_process_hip_runtime():
+    """One HIP runtime per process.
+
+    libtekubls_hip.so needs libamdhip64.so.7; PyTorch-ROCm ships its own copy
+    (torch/lib/libamdhip64.so, same soname) and its libraries ask for it as
+    "libamdhip64.so".  If this library is loaded first, the loader takes
+    /opt/rocm's copy for it and torch later maps its own beside it: two HIP
+    and two HSA runtimes in one process, and torch's initialisation failed
+    with "No HIP GPUs are available" once the library had used the device
+    (round 4).  Loading torch's runtime first, by path
+    and RTLD_GLOBAL, makes every later request resolve to that one copy: this
+    library's soname request matches it, and torch's own load finds the same
+    file already mapped.  A process without torch keeps the system runtime.
+    TBLS_HIP_PRELOAD=0 disables this (diagnostics)."""
+    if os.environ.get("TBLS_HIP_PRELOAD", "1") == "0" or _loaded_hip_runtimes():
+        return
+    try:
+        import importlib.util
+
+        spec = importlib.util.find_spec("torch")
+    except (ImportError, ValueError):
+        spec = None
+    if spec is None or not spec.origin:
+        return
+    rt = os.path.join(os.path.dirname(spec.origin), "lib", "libamdhip64.so")
+    if os.path.exists(rt):
+        ctypes.CDLL(rt, mode=ctypes.RTLD_GLOBAL)
+
+
 def load_library(path: str = LIB_PATH):
     """dlopen the library and bind every entry point (no device initialisation)."""
     if not os.path.exists(path):
         raise NativeError(DEVICE_ERROR, f"HIP library not built: {path} (run __graft_entry__.build())")
+    _preload_process_hip_runtime()
     lib = ctypes.CDLL(path)
     for name, (res, args) in _SIGS.items():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
     return lib
+
+
+_host_lib = None
+
+
+def host():
+    """The library for its host-only entry points (tbls_*_decode*, tbls_stats,
+    tbls_place_plan): loaded, never initialised -- no device needed."""
+    global _host_lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if _host_lib is None:
+            _host_lib = load_library()
+        return _host_lib
+
+
+def stats(reset=False):
+    """tbls_stats as a dict (what the device and the host decoders did)."""
+    out = (ctypes.c_uint64 * 8)()
+    check(host().tbls_stats(out, 8, 1 if reset else 0), "tbls_stats")
+    names = ("partials", "one_validate", "helpers", "each_passes", "finals", "host_decodes", "settled")
+    return dict(zip(names, out[: len(names)]))
 
 
 def lib():

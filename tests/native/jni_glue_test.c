@@ -64,6 +64,20 @@ void tbls_shutdown(void) {}
 int tbls_device_count(void) { return 1; }
 int tbls_pk_validate(const uint8_t pk[48]) { (void)pk; FAKE_OK() }
 int tbls_sig_validate(const uint8_t s[96], int* inf) { (void)s; *inf = 0; FAKE_OK() }
+int tbls_pk_decode(const uint8_t pk[48], int* inf) { (void)pk; if (inf) *inf = 0; FAKE_OK() }
+int tbls_sig_decode(const uint8_t s[96], int* inf) { (void)s; if (inf) *inf = 0; FAKE_OK() }
+int tbls_pk_decode_many(const uint8_t* p, size_t n, uint8_t* c, uint8_t* inf) {
+  for (size_t i = 0; i < n; i++) c[i] = p[48 * i + 47] ? 1 : 0;  /* touch every item's last byte */
+  (void)inf;
+  last_n = n;
+  FAKE_OK()
+}
+int tbls_sig_decode_many(const uint8_t* s, size_t n, uint8_t* c, uint8_t* inf) {
+  for (size_t i = 0; i < n; i++) c[i] = s[96 * i + 95] ? 1 : 0;
+  (void)inf;
+  last_n = n;
+  FAKE_OK()
+}
 int tbls_aggregate_pks(const uint8_t* p, size_t k, uint8_t o[48]) { (void)p, (void)k; memset(o, 0, 48); FAKE_OK() }
 int tbls_aggregate_sigs(const uint8_t* p, size_t k, uint8_t o[96]) { (void)p, (void)k; memset(o, 0, 96); FAKE_OK() }
 int tbls_sign(const uint8_t sk[32], const uint8_t* m, size_t l, const uint8_t* d, size_t dl, uint8_t o[96]) {
@@ -137,6 +151,10 @@ jint J(verify)(JNIEnv*, jclass, jbyteArray, jbyteArray, jbyteArray, jbyteArray, 
 jint J(pkValidate)(JNIEnv*, jclass, jbyteArray);
 jint J(aggregateSigsMany)(JNIEnv*, jclass, jbyteArray, jintArray, jint, jbyteArray, jintArray);
 jint J(pkTableLoad)(JNIEnv*, jclass, jbyteArray, jint, jbyteArray);
+jint J(pkDecode)(JNIEnv*, jclass, jbyteArray);
+jint J(sigDecode)(JNIEnv*, jclass, jbyteArray);
+jint J(pkDecodeMany)(JNIEnv*, jclass, jbyteArray, jint, jbyteArray);
+jint J(sigDecodeMany)(JNIEnv*, jclass, jbyteArray, jint, jbyteArray);
 
 static int failures;
 #define CHECK(cond, what)                                  \
@@ -290,6 +308,44 @@ int main(void) {
     calls = 0;
     CHECK(J(pkTableLoad)(&ENV, NULL, pks, 3, codes) == TBLS_BAD_ARGUMENT && calls == 0, "pkTableLoad keys short");
     arr_free(pks), arr_free(codes);
+  }
+  /* aggregateSigsMany with 96 * groups past 2^31: the output-length check is
+   * done in size_t (a jsize product went negative and let the call through) */
+  {
+    jobject sigs = arr(96, 1), off = arr(1, 4), out = arr(96, 1), st = arr(1, 4);
+    st->len = 30000000; /* only the length is read before the check fails */
+    calls = 0;
+    pending = 0;
+    CHECK(J(aggregateSigsMany)(&ENV, NULL, sigs, off, 30000000, out, st) == TBLS_BAD_ARGUMENT && calls == 0 && !pending,
+          "aggregateSigsMany huge group count");
+    st->len = 1;
+    arr_free(sigs), arr_free(off), arr_free(out), arr_free(st);
+  }
+  /* host decoders: fixed sizes, n items inside the array, codes long enough */
+  {
+    jobject pk = arr(48, 1), sig = arr(96, 1), pks = arr(48 * 3, 1), sigs = arr(96 * 3, 1), codes = arr(3, 1);
+    calls = 0;
+    pending = 0;
+    CHECK(J(pkDecode)(&ENV, NULL, pk) == TBLS_SUCCESS && J(sigDecode)(&ENV, NULL, sig) == TBLS_SUCCESS && calls == 2, "decode valid");
+    pk->len = 47;
+    sig->len = 95;
+    calls = 0;
+    CHECK(J(pkDecode)(&ENV, NULL, pk) == TBLS_BAD_ENCODING && J(sigDecode)(&ENV, NULL, sig) == TBLS_BAD_ENCODING && calls == 0,
+          "decode short");
+    pk->len = 48;
+    sig->len = 96;
+    ((jbyte*)sigs->data)[96 * 3 - 1] = 1;
+    calls = 0;
+    CHECK(J(sigDecodeMany)(&ENV, NULL, sigs, 3, codes) == TBLS_SUCCESS && calls == 1 && last_n == 3 && ((jbyte*)codes->data)[2] == 1,
+          "sigDecodeMany valid");
+    CHECK(J(pkDecodeMany)(&ENV, NULL, pks, 3, codes) == TBLS_SUCCESS && calls == 2 && last_n == 3, "pkDecodeMany valid");
+    calls = 0;
+    CHECK(J(sigDecodeMany)(&ENV, NULL, sigs, 4, codes) == TBLS_BAD_ARGUMENT && calls == 0, "sigDecodeMany codes short");
+    codes->len = 4;
+    CHECK(J(pkDecodeMany)(&ENV, NULL, pks, 4, codes) == TBLS_BAD_ARGUMENT && calls == 0, "pkDecodeMany keys short");
+    codes->len = 3;
+    CHECK(J(pkDecodeMany)(&ENV, NULL, pks, -1, codes) == TBLS_BAD_ARGUMENT && calls == 0, "pkDecodeMany negative n");
+    arr_free(pk), arr_free(sig), arr_free(pks), arr_free(sigs), arr_free(codes);
   }
   if (failures) return 1;
   printf("ok\n");

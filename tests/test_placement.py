@@ -1,7 +1,9 @@
 """Device placement of batches (tb_lib.hip place_plan through tbls_place_plan;
-pure host logic, no device): small batches go whole to the least-loaded
-device, large ones shard over every device with key-balanced cuts, and
-concurrent callers land on different devices (SURVEY.md 8(e);
+pure host logic, no device): a batch is sharded only over IDLE devices and
+only into shards of at least shard_min = 32,768 sets (where one device's
+partial stops being a latency chain, profiles/r04_stage_sweep_final.json);
+with no idle device it goes whole to the least-loaded one, so concurrent
+callers land on different devices (SURVEY.md 8(e);
 AggregatingSignatureVerificationService.java:121-132, 202-205)."""
 
 import random
@@ -10,51 +12,86 @@ import pytest
 
 from teku_amd import dist, native
 
+SMIN = 32768
+
 
 def test_shard_min_default():
-    assert native.load_library().tbls_shard_min() == 2048
+    assert native.load_library().tbls_shard_min() == SMIN
 
 
 @pytest.mark.parametrize("D", [1, 2, 4, 8])
 def test_config1_batch_stays_on_one_device(D):
     for rr in range(2 * D):
-        devs, cuts = native.place_plan(128, n_devices=D, rr=rr, shard_min=2048)
+        devs, cuts = native.place_plan(128, n_devices=D, rr=rr, shard_min=SMIN)
         assert devs == [rr % D] and cuts == [0, 128]
 
 
 @pytest.mark.parametrize("D", [1, 2, 4, 8])
-def test_config4_batch_uses_every_device(D):
-    devs, cuts = native.place_plan(16384, n_devices=D, shard_min=2048)
-    assert devs == list(range(D))
-    assert cuts == [16384 * k // D for k in range(D + 1)]
+def test_config4_batch_takes_one_device(D):
+    """16,384 sets is below shard_min: one device, whatever the node's load."""
+    for rr in range(D):
+        devs, cuts = native.place_plan(16384, n_devices=D, rr=rr, shard_min=SMIN)
+        assert devs == [rr % D] and cuts == [0, 16384]
 
 
-@pytest.mark.parametrize("n,D,G", [(2047, 8, 1), (2048, 8, 1), (4095, 8, 1), (4096, 8, 2), (6144, 8, 3), (16383, 8, 7),
-                                   (1048576, 8, 8), (131072, 4, 4), (5, 8, 1)])
+def test_eight_concurrent_config4_batches_get_eight_devices():
+    """8 simulated devices, 8 service workers each
+    placing a 16,384-set batch while the earlier ones are still in flight ->
+    8 distinct single devices (round 4: every batch took all 8)."""
+    load = [0] * 8
+    got = []
+    for w in range(8):
+        devs, cuts = native.place_plan(16384, n_devices=8, load=load, rr=3 * w + 1, shard_min=SMIN)
+        assert len(devs) == 1 and cuts == [0, 16384]
+        load[devs[0]] += 1
+        got.append(devs[0])
+    assert sorted(got) == list(range(8))
+    # a ninth caller shares the least-loaded device (all hold one batch)
+    devs, _ = native.place_plan(16384, n_devices=8, load=load, rr=5, shard_min=SMIN)
+    assert devs == [5]
+
+
+@pytest.mark.parametrize("n,D,G", [(32767, 8, 1), (65535, 8, 1), (65536, 8, 2), (131072, 8, 4), (131072, 4, 4), (131072, 2, 2),
+                                   (262144, 8, 8), (1048576, 8, 8), (5, 8, 1)])
 def test_device_count_follows_shard_min(n, D, G):
-    devs, cuts = native.place_plan(n, n_devices=D, shard_min=2048)
+    """A lone batch on an idle node: 131,072 sets still shards (4 x 32,768),
+    config 5's 1,048,576 sets use all 8 devices."""
+    devs, cuts = native.place_plan(n, n_devices=D, shard_min=SMIN)
     assert len(devs) == G and cuts[0] == 0 and cuts[-1] == n
     assert all(cuts[k] <= cuts[k + 1] for k in range(G))
     if G > 1:
-        assert min(cuts[k + 1] - cuts[k] for k in range(G)) >= 2048 - 1
+        assert min(cuts[k + 1] - cuts[k] for k in range(G)) >= SMIN - 1
+
+
+def test_sharding_uses_idle_devices_only():
+    # 1M sets with 3 devices busy: the 5 idle ones, ascending
+    devs, cuts = native.place_plan(1048576, n_devices=8, load=[1, 0, 2, 0, 0, 1, 0, 0], rr=0, shard_min=SMIN)
+    assert devs == [1, 3, 4, 6, 7] and cuts[-1] == 1048576
+    # every device busy: whole batch on the least loaded one
+    devs, cuts = native.place_plan(1048576, n_devices=4, load=[2, 1, 3, 1], rr=0, shard_min=SMIN)
+    assert devs == [1] and cuts == [0, 1048576]
+    devs, _ = native.place_plan(1048576, n_devices=4, load=[2, 1, 3, 1], rr=2, shard_min=SMIN)
+    assert devs == [3]  # equal loads: round-robin from rr
 
 
 def test_n_gpus_caps_and_shard_min_zero():
-    devs, _ = native.place_plan(1048576, n_devices=8, n_gpus=2, shard_min=2048)
+    devs, _ = native.place_plan(1048576, n_devices=8, n_gpus=2, shard_min=SMIN)
     assert len(devs) == 2
     devs, cuts = native.place_plan(6, n_devices=8, shard_min=0)
     assert len(devs) == 6 and cuts == list(range(7))  # never more devices than sets
     devs, _ = native.place_plan(100, n_devices=4, shard_min=0)
     assert devs == [0, 1, 2, 3]
+    devs, _ = native.place_plan(100, n_devices=4, load=[0, 1, 0, 0], shard_min=0)
+    assert devs == [0, 2, 3]
 
 
 def test_least_loaded_devices_chosen():
-    devs, _ = native.place_plan(128, n_devices=4, load=[1, 0, 2, 0], rr=0, shard_min=2048)
+    devs, _ = native.place_plan(128, n_devices=4, load=[1, 0, 2, 0], rr=0, shard_min=SMIN)
     assert devs == [1]
-    devs, _ = native.place_plan(128, n_devices=4, load=[1, 0, 2, 0], rr=2, shard_min=2048)
+    devs, _ = native.place_plan(128, n_devices=4, load=[1, 0, 2, 0], rr=2, shard_min=SMIN)
     assert devs == [3]  # equal loads: round-robin from rr
-    devs, _ = native.place_plan(4096, n_devices=4, load=[3, 0, 2, 1], rr=0, shard_min=2048)
-    assert devs == [1, 3]  # the two least loaded, ascending (lock order, root first)
+    devs, _ = native.place_plan(4 * SMIN, n_devices=4, load=[3, 0, 2, 0], rr=0, shard_min=SMIN)
+    assert devs == [1, 3]  # the two idle ones, ascending (lock order, root first)
 
 
 def test_concurrent_workers_spread_over_devices():
@@ -64,7 +101,7 @@ def test_concurrent_workers_spread_over_devices():
         load = [0] * D
         got = []
         for w in range(D):
-            devs, _ = native.place_plan(250, n_devices=D, load=load, rr=7 * w, shard_min=2048)
+            devs, _ = native.place_plan(250, n_devices=D, load=load, rr=7 * w, shard_min=SMIN)
             assert len(devs) == 1
             load[devs[0]] += 1
             got.append(devs[0])
