@@ -182,6 +182,18 @@ int tbls_fast_aggregate_verify_many(const tbls_set* sets, size_t n, int* ok_per_
  * over at most n_gpus devices (0 = all), the least-loaded first. */
 int tbls_verify_each(const tbls_set* sets, size_t n, int n_gpus, int* ok_per_set);
 
+/* The service's batch with its failure path in one call: tbls_batch_verify
+ * over the sets (*ok), and when it fails, every set's verdict
+ * ok_per_set[i] = BLS.fastAggregateVerify(sets[i]) (BLS.java:185-207) settled
+ * from the batch's own work on the devices that ran it -- per-set Miller
+ * values from the batch's G2 lines, group tests (product + final
+ * exponentiation) over 256- and 16-set groups, then single sets -- instead of
+ * a second full pass (tbls_verify_each) or the reference's recursive halving
+ * (AggregatingSignatureVerificationService.java:206-233).  When the batch
+ * passes, every set with keys gets 1.  A set with n_pks == 0 gets 0 and makes
+ * *ok 0 (it is left out of the batch).  rand as tbls_batch_verify. */
+int tbls_batch_verify_each(const tbls_set* sets, size_t n, const uint64_t* rand, int n_gpus, int* ok, int* ok_per_set, tbls_timing* t);
+
 /* ---- batched deserialization and aggregation ----
  * Gossip decoding validates every key / signature it sees (lazy
  * BLSSignature.getSignature, BLSSignature.java:83-87; the eth reference

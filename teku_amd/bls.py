@@ -844,42 +844,52 @@ def predecode(public_keys=(), signatures=()) -> None:
 
 def _hip_facade_batch(impl, public_keys, messages, signatures, double_pairing) -> bool:
     """BLS.batchVerify's 5-argument body (BLS.java:297-336) on HipBLS12381,
-    without the per-set semi-aggregate objects: HipBLS12381.prepareBatchVerify
-    only captures bytes, so the verdict and the exceptions are those of the
-    prepare / complete loop -- a unit (a pair of sets with double_pairing,
-    BLS.java:306-322, else one set) with an undecodable key or signature is
-    an InvalidBatchSemiAggregate (the batch is false); otherwise an empty key
-    list raises (BlstPublicKey.aggregate's checkArgument) -- and all sets go
-    to the device as one tbls_batch_verify.  Decoding is one multi-threaded
-    host call per batch (predecode)."""
+    without per-set semi-aggregate objects and without decoding on the host:
+    HipBLS12381.prepareBatchVerify only captures bytes, and the device
+    decodes every key and signature inside the batch with the same rules
+    (tb_codec.h = tbls_*_decode's), so the verdict is the prepare / complete
+    loop's -- a unit (a pair of sets with double_pairing, BLS.java:306-322,
+    else one set) holding an undecodable key or signature is an
+    InvalidBatchSemiAggregate (the batch is false), which the device's batch
+    also returns.  The one case where the host must decode: a unit with an
+    empty key list raises (BlstPublicKey.aggregate's checkArgument) unless an
+    object of that unit fails to decode first (then it is invalid, no raise),
+    so only such units' objects are decoded here.  One device batch, no
+    single-object device call, no per-object decode for fresh objects."""
     from .synth import SetArray, fast_multipliers
 
-    key_lists = [list(ks) for ks in public_keys]
-    predecode([k for ks in key_lists for k in ks], signatures)
-
-    def decoded(o):
-        if isinstance(o, (BLSPublicKey, BLSSignature)):
-            return o._impl is not None
-        try:
-            _as_pk(o) if isinstance(o, (PublicKey, HipPublicKey)) else _as_sig(o)
-            return True
-        except BlsException:
-            return False
-
+    key_lists = public_keys if all(type(ks) is list for ks in public_keys) else [list(ks) for ks in public_keys]
     n = len(key_lists)
-    ok_dec = [all(decoded(k) for k in key_lists[i]) and decoded(signatures[i]) for i in range(n)]
-    step = 2 if double_pairing else 1
-    invalid = False
-    for i in range(0, n, step):
-        unit = range(i, min(n, i + step))
-        if not all(ok_dec[j] for j in unit):
-            invalid = True
-        elif any(len(key_lists[j]) == 0 for j in unit):
-            raise ValueError("empty public key list")
-    if invalid:
+    empty = [i for i in range(n) if not key_lists[i]]
+    if empty:
+        step = 2 if double_pairing else 1
+
+        def decodes(o):
+            try:
+                (o.get_public_key() if isinstance(o, BLSPublicKey) else o.get_signature() if isinstance(o, BLSSignature)
+                 else _as_pk(o) if isinstance(o, PublicKey) else _as_sig(o))
+                return True
+            except BlsException:
+                return False
+
+        for u in sorted({i - i % step for i in empty}):
+            unit = range(u, min(n, u + step))
+            if all(decodes(k) for j in unit for k in key_lists[j]) and all(decodes(signatures[j]) for j in unit):
+                raise ValueError("empty public key list")
+        return False  # every empty-key unit holds an undecodable object: InvalidBatchSemiAggregate
+
+    def raw(o):
+        return o._b if type(o) in (BLSPublicKey, BLSSignature) else bytes(o.to_bytes_compressed())
+
+    if all(len(ks) == 1 for ks in key_lists):
+        pk_blob = b"".join([raw(ks[0]) for ks in key_lists])
+        n_pks = [1] * n
+    else:
+        pk_blob = b"".join([raw(k) for ks in key_lists for k in ks])
+        n_pks = [len(ks) for ks in key_lists]
+    msgs = [m if type(m) is bytes else bytes(m) for m in messages]
+    sig_blob = b"".join([raw(sg) for sg in signatures])
+    if len(sig_blob) != 96 * n or len(pk_blob) != 48 * sum(n_pks):  # a wrong-size encoding never decodes
         return False
-    pk_blob = b"".join(k.to_bytes_compressed() for ks in key_lists for k in ks)
-    msgs = [bytes(m) for m in messages]
-    arr = SetArray(pk_blob, [len(ks) for ks in key_lists], b"".join(msgs), [len(m) for m in msgs],
-                   b"".join(sg.to_bytes_compressed() for sg in signatures))
+    arr = SetArray(pk_blob, n_pks, b"".join(msgs), [len(m) for m in msgs], sig_blob)
     return arr.batch_verify(fast_multipliers(n), impl.n_gpus)

@@ -191,3 +191,32 @@ extern "C" __global__ void k_final_verify(const fp12* __restrict__ f, const uint
 extern "C" __global__ void __launch_bounds__(64) k_fp12_one(fp12* __restrict__ f) {
   if (threadIdx.x == 0) f[0] = fp12_one();
 }
+
+// Group tests for settling a failed batch from its own Miller values
+// (tb_lib.hip settle_sets): block b tests group list[b] of a segmented value
+// array -- segment j of group g at vals[j * stride + g], the Miller value of
+// the group being prod_j v_j^(2^D_j) as in k_fp12_seg_combine_coop -- by the
+// Horner combine then the final exponentiation: out[b] = 1 iff the result is
+// 1, i.e. (the values carry the batch's randomizers r_i, 0 < r_i < 2^64 < r)
+// iff every set of the group verifies, except with probability 2^-64 per
+// forged set as for the batch itself; a group of one set is that set's exact
+// verdict.  One 256-thread coop workgroup per group (tb_cfe.h).
+extern "C" __global__ void __launch_bounds__(CFE_THREADS)
+    k_group_test_coop(const fp12* __restrict__ vals, uint32_t stride, uint32_t nseg, const uint32_t* __restrict__ list,
+                      uint8_t* __restrict__ out) {
+  __shared__ cfe_lds L;
+  tb_latency_prio();
+  cfe::init(L);
+  cfe_regs R;
+  cfe::regs_load(R, L);
+  const uint32_t g = list[blockIdx.x];
+  cfe::load_coords(L.F, reinterpret_cast<const fp*>(vals + g));
+  for (uint32_t j = 1; j < nseg; j++) {
+    const uint32_t d = seg_doublings(j, nseg);
+    for (uint32_t k = 0; k < d; k++) cfe::mul(L.F, L.F, L.F, L, R);
+    cfe::load_coords(L.X, reinterpret_cast<const fp*>(vals + (size_t)j * stride + g));
+    cfe::mul(L.F, L.F, L.X, L, R);
+  }
+  const bool one = cfe::final_exp_is_one(L, R);
+  if (threadIdx.x == 0) out[blockIdx.x] = one ? 1 : 0;
+}

@@ -97,6 +97,7 @@ struct dev_ctx {
   // first waits for this event, then records it after its own work.
   hipEvent_t e_ws = nullptr;
   dbuf recs;  // partial records gathered for the final exponentiation (gather_partials, device 0)
+  dbuf sws;   // settling a failed batch (settle_sets): per-set Miller values, group levels, test lists
   dbuf comb;  // (d 2^(8w)) g1 for w < 8, d < 256 (k_g1_comb_init): the signature pairs' G1 side
   hbuf hin, hout;
   int load = 0;  // batches placed on this device and not yet finished (g_place_mu)
@@ -327,11 +328,14 @@ static void acc_plan(uint32_t n_main, uint32_t& per, uint32_t& nseg) {
 struct pair_plan {
   uint32_t n, n_extra, n_pairs, n_main, n_xwave, per, nseg;
   bool msm, wave, split;
-  explicit pair_plan(uint32_t n_) : n(n_) {
-    msm = n >= msm_min();
+  // settle: the per-set layout a failed batch is settled on (settle_sets):
+  // one signature pair per set (no bucket sums), split line / accumulator
+  // kernels at every size
+  explicit pair_plan(uint32_t n_, bool settle = false) : n(n_) {
+    msm = !settle && n >= msm_min();
     n_extra = msm ? TB_MSM_XPAIRS : n;
     n_pairs = n + n_extra;
-    wave = n_pairs <= miller_wave_max();
+    wave = !settle && n_pairs <= miller_wave_max();
     split = !wave;
     n_xwave = split && msm ? n_extra : 0u;  // bit-sum pairs on their own waves
     n_main = n_pairs - n_xwave;             // pairs owned by accumulator threads
@@ -494,6 +498,39 @@ void launch_set_pk(hipStream_t s, uint32_t n, uint32_t n_entries, const uint32_t
                        (const uint32_t*)mlist, (const uint32_t*)mcnt, P, set_code, n_bad, key_idx, tab_n);
 }
 
+// k_lines.hip: the segmented accumulator with f in LDS and two lines per
+// product (tb_lines.h miller_accs_lds_body).  Measured at 131,072 sets
+// (profiles/r05_bench_acc_lds_ab.json): Miller stage alone 13.3 -> 12.6 ms
+// and scratch writes 3.3 -> 1.5 GB per launch, but beside the bucket-sum
+// stream's workgroups (k_msm_bucket_sum, 18 KB of LDS each) part of its
+// one-round grid (4 x 36,864 B per CU) found no CU with the LDS free and ran
+// a second round: 131k step 38.2 -> 43.9 ms; waiting for that stream first
+// (TBLS_ACC_JOIN=1) gives 38.5.  So by default it runs where nothing runs
+// beside it -- batches without bucket sums (< 20,480 sets: config 4) and the
+// per-set settling of a failed batch -- and the register-resident
+// k_miller_accs where the bucket sums may still run.  TBLS_ACC_LDS=0 / 1
+// forces one kernel everywhere (A/B).
+extern "C" __global__ void k_miller_accs_lds(const uint4* __restrict__ lines, const uint8_t* __restrict__ skip, const uint8_t* __restrict__ code_a,
+                                             const uint8_t* __restrict__ code_b, uint32_t n, uint32_t per, uint32_t nseg, uint32_t g_pad,
+                                             fp12* __restrict__ f_out, uint32_t seg_stride);
+extern "C" __global__ void k_miller_wave_g(const g1a* __restrict__ P, const g2a* __restrict__ Q, const uint8_t* __restrict__ skip,
+                                           const uint8_t* __restrict__ code_a, const uint8_t* __restrict__ code_b, uint32_t n,
+                                           fp12* __restrict__ f);  // k_mwave.hip: level tables from global memory
+static int acc_lds_env() {  // -1 auto, 0 never, 1 always
+  static const int v = getenv("TBLS_ACC_LDS") ? (getenv("TBLS_ACC_LDS")[0] == '0' ? 0 : 1) : -1;
+  return v;
+}
+// the LDS accumulator for a launch with (msm_beside) or without the bucket-sum stream running beside it
+static bool acc_lds(bool msm_beside = false) {
+  const int e = acc_lds_env();
+  return e < 0 ? !msm_beside : e == 1;
+}
+// TBLS_ACC_JOIN=1: the accumulator waits for the bucket-sum stream (its
+// k_miller_wave workgroups hold LDS the accumulator's one-round grid needs)
+static bool acc_join() {
+  static const bool v = getenv("TBLS_ACC_JOIN") && getenv("TBLS_ACC_JOIN")[0] == '1';
+  return v;
+}
 extern "C" __global__ void k_set_hash_wave(const uint8_t* __restrict__ msgs, const uint32_t* __restrict__ msg_off,
                                            const uint8_t* __restrict__ dst, uint32_t dlen, uint32_t n, g2a* __restrict__ Q,
                                            uint8_t* __restrict__ skip);  // k_hwave.hip
@@ -508,11 +545,11 @@ extern "C" __global__ void k_sig_check_coop(const uint8_t* __restrict__ sigs, ui
                                             uint8_t* __restrict__ sig_code, uint32_t* __restrict__ n_bad);  // k_kcoop.hip
 int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* partial_out, ws_layout& L,
                    const uint8_t* dst, uint32_t dlen, hipEvent_t* ev = nullptr, bool serial = false,
-                   const uint32_t* key_idx = nullptr) {
+                   const uint32_t* key_idx = nullptr, bool settle = false) {
   const uint32_t n = b.n;
   const bool use_tab = key_idx != nullptr;  // keys = indices into the resident table: no decompression
   const uint32_t K = use_tab ? 0 : b.n_keys;
-  const pair_plan pp(n);
+  const pair_plan pp(n, settle);
   L = ws_layout(pp, K);
   tb::stat_add(tb::TB_STAT_PARTIALS);
   HIPCHK(ws_acquire(c, s));
@@ -584,7 +621,9 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
     hipLaunchKernelGGL(k_msm_bitsum_pairs, dim3(TB_MSM_XPAIRS), dim3(64), 0, sb, (const g2j*)(w + L.msm_sum), c.comb.as<const g1a>(),
                        P + n, Q + n, skip + n);
     if (pp.n_xwave)  // their Miller loops, one wave each, on this stream: f[n_f_main ..)
-      hipLaunchKernelGGL(k_miller_wave, dim3(pp.n_xwave), dim3(64), 0, sb, (const g1a*)P + n, (const g2a*)Q + n, (const uint8_t*)skip + n,
+      hipLaunchKernelGGL(acc_lds(!acc_join()) ? k_miller_wave_g : k_miller_wave, dim3(pp.n_xwave), dim3(64), 0, sb, (const g1a*)P + n,
+                         (const g2a*)Q + n,
+                         (const uint8_t*)skip + n,
                          (const uint8_t*)(w + L.set_code + n), (const uint8_t*)(w + L.sig_code + n), pp.n_xwave, (fp12*)(w + L.f) + pp.n_f_main());
   }
   TB_EV(9, sb);
@@ -674,9 +713,13 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
         else
           hipLaunchKernelGGL(k_miller_lines_w2, dim3((m + TB_BLOCK - 1) / TB_BLOCK), blk, 0, s,
                              (const g1a*)P + lo, (const g2a*)Q + lo, (const uint8_t*)skip + lo, ca + lo, cb + lo, m, lines);
+        if (settle) continue;  // settle_sets accumulates per set from these lines
+        if (late_join && acc_join() && lo == 0) HIPCHK(hipStreamWaitEvent(s, c.e_join[1], 0));
         if (pp.seg()) {
           const uint32_t g_pad = (mt + TB_BLOCK - 1) / TB_BLOCK * TB_BLOCK;
-          hipLaunchKernelGGL(k_miller_accs, dim3(pp.nseg * g_pad / TB_BLOCK), blk, 0, s, (const uint4*)lines, (const uint8_t*)skip + lo,
+          hipLaunchKernelGGL(acc_lds(pp.msm && !acc_join()) ? k_miller_accs_lds : k_miller_accs, dim3(pp.nseg * g_pad / TB_BLOCK), blk, 0, s,
+                             (const uint4*)lines,
+                             (const uint8_t*)skip + lo,
                              ca + lo, cb + lo, m, pp.per, pp.nseg, g_pad, f + lo / pp.per, pp.n_groups());
         } else {
           hipLaunchKernelGGL(pp.per == 2 ? k_miller_acc2 : k_miller_acc1, dim3((mt + TB_BLOCK - 1) / TB_BLOCK), blk, 0, s,
@@ -686,6 +729,11 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
     }
   }
   if (late_join) HIPCHK(hipStreamWaitEvent(s, c.e_join[1], 0));  // every stream joins before ws_release
+  if (settle) {
+    HIPCHK(hipGetLastError());
+    HIPCHK(ws_release(c, s));
+    return TBLS_SUCCESS;
+  }
   TB_EV(11, s);
   TB_EV(12, s);
   if (nf == 0) {  // no pairs at all: the partial product is 1
@@ -830,7 +878,7 @@ const uint8_t ETH2_DST[] = "BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_POP_";
 // memory, c->in) -- nothing is synchronized.  e_t0/e_t1 bracket the kernels.
 template <class SET>
 int shard_launch(dev_ctx* c, const SET* sets, size_t lo, size_t hi, const uint64_t* rand, const uint8_t* dst, uint32_t dlen,
-                 uint8_t** dpart, ws_layout& L, uint32_t* n_out) {
+                 uint8_t** dpart, ws_layout& L, uint32_t* n_out, bool settle = false) {
   constexpr bool idx_mode = !std::is_same<SET, tbls_set>::value;
   HIPCHK(hipSetDevice(c->dev));
   if (idx_mode) {  // key indices against this device's table, under its lock (a reload cannot interleave)
@@ -859,7 +907,8 @@ int shard_launch(dev_ctx* c, const SET* sets, size_t lo, size_t hi, const uint64
   *dpart = di + align_up(p.total);
   *n_out = p.n;
   HIPCHK(hipEventRecord(c->e_t0, s));
-  int rc = launch_partial(*c, b, s, *dpart, L, di + p.off_dst, dlen, nullptr, false, idx_mode ? (const uint32_t*)(di + p.off_pks) : nullptr);
+  int rc = launch_partial(*c, b, s, *dpart, L, di + p.off_dst, dlen, nullptr, false, idx_mode ? (const uint32_t*)(di + p.off_pks) : nullptr,
+                          settle);
   if (rc) return rc;
   HIPCHK(hipEventRecord(c->e_t1, s));
   return TBLS_SUCCESS;
@@ -901,6 +950,146 @@ int verify_on_device(int d, const SET* sets, size_t n, const uint64_t* rand, con
     *dev_ms = ms;
   }
   return codes_host ? shard_codes(c, L, nn, codes_host) : TBLS_SUCCESS;
+}
+
+// ---------------------------------------------------------------------------
+// Per-set verdicts of a failed batch from the batch's own work (SURVEY.md
+// 8(f) rank 2).  The reference settles a failed batch by recursive halving,
+// one full batchVerify per half (AggregatingSignatureVerificationService.java:
+// 206-233); round 4 ran every set again from its bytes with its own final
+// exponentiation (tbls_verify_each: 75 ms for a failed 16,384-set batch whose
+// batch pass takes 9.8).  Here, on the device that ran the batch and with its
+// workspace intact:
+//  * per-set Miller values from the batch's own G2 lines: the segmented
+//    accumulator with two pairs per thread, where thread g owns pairs g and
+//    g + n -- set g's (r apk, H(m)) and (-r g1, sig) -- so each thread's
+//    value is that set's randomized Miller value, in nseg segments;
+//  * two levels of wave products (16 sets per group, then 256), the same
+//    kernels as the batch's product tree;
+//  * group tests, top level first: one coop workgroup per group runs the
+//    segments' Horner combine and the final exponentiation
+//    (k_group_test_coop); a group whose product is 1 holds only valid sets
+//    (its sets' randomizers make a false pass as unlikely as the batch's own,
+//    2^-64 per forged set); failing groups are opened one level down, to
+//    single sets, whose test is exact.  A set with a failed decode / group /
+//    key check is invalid from its per-set code alone.
+// Batches that ran the bucket-sum signature side (>= 20,480 sets) or the
+// wave Miller loops (<= 1,024 sets) have no per-set signature pairs or no
+// lines: their sets are re-staged in chunks of TB_SETTLE_MAX in the settle
+// layout (pair_plan settle: one signature pair per set, split kernels),
+// which runs the per-set stages and the line kernel only.
+// ---------------------------------------------------------------------------
+extern "C" __global__ void k_group_test_coop(const fp12* __restrict__ vals, uint32_t stride, uint32_t nseg, const uint32_t* __restrict__ list,
+                                             uint8_t* __restrict__ out);  // k_pair.hip
+#define TB_SETTLE_FAN 16u                  // sets per group and groups per group of the next level (k_fp12_prod_wave_seg chunk)
+#define TB_SETTLE_MAX (TB_LINE_CHUNK / 2u)  // sets per settle chunk: both pairs of every set in one line chunk
+
+// segments of the per-set accumulation: fill the GPU once (n threads per segment)
+static uint32_t settle_nseg(uint32_t n) {
+  uint32_t sg = 1;
+  while (sg < 16 && 2ull * sg * n <= TB_ACC_FULL) sg *= 2;
+  return sg;
+}
+
+// true when the pipeline that just ran over n sets left what settle_sets needs:
+// one signature pair per set and both pairs' lines in one chunk
+static bool settle_ready(uint32_t n) {
+  const pair_plan pp(n);
+  return pp.split && !pp.msm && 2ull * n <= TB_LINE_CHUNK;
+}
+
+// Group tests of the listed groups of a segmented value array on c's stream:
+// pass[k] = 1 iff group list[k] tests 1.
+static int group_tests(dev_ctx* c, const fp12* vals, uint32_t stride, uint32_t nseg, const std::vector<uint32_t>& list, uint32_t* dlist,
+                       uint8_t* dout, std::vector<uint8_t>& pass) {
+  pass.assign(list.size(), 0);
+  if (list.empty()) return TBLS_SUCCESS;
+  hipStream_t s = c->stream;
+  HIPCHK(hipMemcpyAsync(dlist, list.data(), 4 * list.size(), hipMemcpyHostToDevice, s));
+  hipLaunchKernelGGL(k_group_test_coop, dim3((uint32_t)list.size()), dim3(TB_CFE_THREADS), 0, s, vals, stride, nseg, (const uint32_t*)dlist, dout);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(pass.data(), dout, list.size(), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  return TBLS_SUCCESS;
+}
+
+// ok[0..n) for the n sets whose pipeline (normal and settle_ready, or the
+// settle layout) just ran on c; lock held, workspace L intact.
+static int settle_sets(dev_ctx* c, const ws_layout& L, uint32_t n, uint8_t* ok) {
+  if (!n) return TBLS_SUCCESS;
+  tb::stat_add(tb::TB_STAT_SETTLE);
+  std::vector<uint8_t> codes(n);
+  int rc = shard_codes(c, L, n, codes.data());  // synchronizes the stream
+  if (rc) return rc;
+  const uint32_t F = TB_SETTLE_FAN, nseg = settle_nseg(n);
+  const uint32_t nA = (n + F - 1) / F, nB = (nA + F - 1) / F;
+  size_t o = 0;
+  const size_t oV = o;
+  o = align_up(o + (size_t)nseg * n * sizeof(fp12));
+  const size_t oA = o;
+  o = align_up(o + (size_t)nseg * nA * sizeof(fp12));
+  const size_t oB = o;
+  o = align_up(o + (size_t)nseg * nB * sizeof(fp12));
+  const size_t oL = o;
+  o = align_up(o + (size_t)n * 4);
+  const size_t oO = o;
+  o = align_up(o + n);
+  if (c->sws.ensure(o)) return TBLS_DEVICE_ERROR;
+  uint8_t* sw = c->sws.as<uint8_t>();
+  uint8_t* w = c->ws.as<uint8_t>();
+  fp12 *V = (fp12*)(sw + oV), *A = (fp12*)(sw + oA), *B = (fp12*)(sw + oB);
+  hipStream_t s = c->stream;
+  const uint32_t g_pad = (n + TB_BLOCK - 1) / TB_BLOCK * TB_BLOCK;
+  hipLaunchKernelGGL(acc_lds() ? k_miller_accs_lds : k_miller_accs, dim3(nseg * g_pad / TB_BLOCK), dim3(TB_BLOCK), 0, s,
+                     (const uint4*)(w + L.lines), (const uint8_t*)(w + L.skip), (const uint8_t*)(w + L.set_code), (const uint8_t*)(w + L.sig_code),
+                     2u * n, 2u, nseg, g_pad, V, n);
+  hipLaunchKernelGGL(k_fp12_prod_wave_seg, dim3(nA, nseg), dim3(64), 0, s, (const fp12*)V, n, n, nseg, n, F, A, nA);
+  hipLaunchKernelGGL(k_fp12_prod_wave_seg, dim3(nB, nseg), dim3(64), 0, s, (const fp12*)A, nA, nA, nseg, nA, F, B, nB);
+  HIPCHK(hipGetLastError());
+  uint32_t* dlist = (uint32_t*)(sw + oL);
+  uint8_t* dout = sw + oO;
+  std::vector<uint32_t> lb(nB), la, l0;
+  for (uint32_t b = 0; b < nB; b++) lb[b] = b;
+  std::vector<uint8_t> pb, pa, p0;
+  if ((rc = group_tests(c, B, nB, nseg, lb, dlist, dout, pb))) return rc;
+  for (uint32_t b = 0; b < nB; b++)
+    if (!pb[b])
+      for (uint32_t a = b * F; a < std::min(nA, (b + 1) * F); a++) la.push_back(a);
+  if ((rc = group_tests(c, A, nA, nseg, la, dlist, dout, pa))) return rc;
+  std::vector<uint8_t> passA(nA, 0);
+  for (size_t k = 0; k < la.size(); k++) passA[la[k]] = pa[k];
+  for (uint32_t a : la)
+    if (!passA[a])
+      for (uint32_t i = a * F; i < std::min(n, (a + 1) * F); i++)
+        if (codes[i] == 0) l0.push_back(i);
+  if ((rc = group_tests(c, V, n, nseg, l0, dlist, dout, p0))) return rc;
+  std::vector<uint8_t> leaf(n, 0);
+  for (size_t k = 0; k < l0.size(); k++) leaf[l0[k]] = p0[k];
+  for (uint32_t i = 0; i < n; i++) {
+    const uint32_t a = i / F, b = a / F;
+    ok[i] = codes[i] == 0 && (pb[b] || passA[a] || leaf[i]) ? 1 : 0;
+  }
+  return TBLS_SUCCESS;
+}
+
+// settle sets [lo, hi) of `sets` on c (lock held) after their batch failed:
+// from the batch's workspace when it is settle_ready (reuse = the batch ran
+// exactly these sets), else re-staged in the settle layout chunk by chunk
+template <class SET>
+static int settle_range(dev_ctx* c, const SET* sets, size_t lo, size_t hi, const uint64_t* rand, bool reuse, const ws_layout& Lb,
+                        uint8_t* ok) {
+  const uint32_t n = (uint32_t)(hi - lo);
+  if (reuse && settle_ready(n)) return settle_sets(c, Lb, n, ok);
+  for (size_t a = lo; a < hi; a += TB_SETTLE_MAX) {
+    const size_t b = std::min(hi, a + (size_t)TB_SETTLE_MAX);
+    uint8_t* dpart = nullptr;
+    ws_layout L;
+    uint32_t nn = 0;
+    int rc = shard_launch(c, sets, a, b, rand, ETH2_DST, 43, &dpart, L, &nn, true);
+    if (!rc) rc = settle_sets(c, L, nn, ok + (a - lo));
+    if (rc) return rc;
+  }
+  return TBLS_SUCCESS;
 }
 
 // ---------------------------------------------------------------------------
@@ -1176,6 +1365,7 @@ extern "C" void tbls_shutdown(void) {
     if (c->fin.p) (void)hipFree(c->fin.p);
     if (c->dstb.p) (void)hipFree(c->dstb.p);
     if (c->recs.p) (void)hipFree(c->recs.p);
+    if (c->sws.p) (void)hipFree(c->sws.p);
     if (c->comb.p) (void)hipFree(c->comb.p);
     if (c->tab_aff.p) (void)hipFree(c->tab_aff.p);
     if (c->tab_code.p) (void)hipFree(c->tab_code.p);
@@ -1260,6 +1450,94 @@ int batch_verify_impl(const SET* sets, size_t n, const uint64_t* rand, int n_gpu
 
 extern "C" int tbls_batch_verify(const tbls_set* sets, size_t n, const uint64_t* rand, int n_gpus, int* ok, tbls_timing* t) {
   return batch_verify_impl(sets, n, rand, n_gpus, ok, t);
+}
+
+// tbls_batch_verify_each: the randomized batch, and on failure each set's
+// verdict settled from the batch's own work on the devices that ran it
+// (settle_range).  Sets with no keys are false and left out of the batch.
+extern "C" int tbls_batch_verify_each(const tbls_set* sets_in, size_t n_in, const uint64_t* rand_in, int n_gpus, int* ok, int* ok_per_set,
+                                      tbls_timing* t) {
+  auto t0 = std::chrono::steady_clock::now();
+  const caller_device keep;
+  if (!ok || (n_in && (!sets_in || !rand_in || !ok_per_set))) return TBLS_BAD_ARGUMENT;
+  *ok = 0;
+  if (ensure_init()) return TBLS_DEVICE_ERROR;
+  if (n_in == 0) return TBLS_SUCCESS;  // BLS.java:240-241
+  std::vector<tbls_set> sets;
+  std::vector<uint64_t> rand;
+  std::vector<size_t> pos;
+  for (size_t i = 0; i < n_in; i++) {
+    ok_per_set[i] = 0;  // an empty key list: false (BLS.java:193-195)
+    if (sets_in[i].n_pks) {
+      sets.push_back(sets_in[i]);
+      rand.push_back(rand_in[i]);
+      pos.push_back(i);
+    }
+  }
+  const size_t n = sets.size();
+  if (n == 0) return TBLS_SUCCESS;
+  placed pl;
+  place_batch(pl, n, [&](size_t i) { return sets[i].n_pks; }, n_gpus, shard_min());
+  const int G = pl.G;
+  std::vector<std::unique_lock<std::mutex>> locks;  // ascending device order: no deadlock
+  for (int g = 0; g < G; g++) locks.emplace_back(ctx_for(pl.dev[g])->mu);
+  std::vector<uint8_t*> dpart(G, nullptr);
+  std::vector<ws_layout> Ls(G);
+  std::vector<int> rcs(G, 0);
+  auto stage = [&](int g) {
+    uint32_t nn;
+    rcs[g] = shard_launch(ctx_for(pl.dev[g]), sets.data(), pl.cut[g], pl.cut[g + 1], rand.data(), ETH2_DST, 43, &dpart[g], Ls[g], &nn);
+  };
+  auto run_all = [&](const std::function<void(int)>& fn) {
+    if (G == 1) {
+      fn(0);
+      return;
+    }
+    std::vector<std::thread> th;
+    for (int g = 0; g < G; g++) th.emplace_back(fn, g);
+    for (auto& x : th) x.join();
+  };
+  run_all(stage);
+  for (int g = 0; g < G; g++)
+    if (rcs[g]) return rcs[g];
+  int rc = TBLS_SUCCESS;
+  dev_ctx* root = ctx_for(pl.dev[0]);
+  if (G == 1 && !gather_forced()) {
+    rc = launch_final(*root, dpart[0], 1, root->stream, ok);
+  } else {
+    rc = gather_partials(gather_sel(), pl.dev, G, dpart);
+    if (!rc) rc = launch_final(*root, root->recs.p, (uint32_t)G, root->stream, ok);
+  }
+  if (rc) return rc;
+  std::vector<uint8_t> verdict(n, 1);
+  if (!*ok) {
+    auto settle = [&](int g) {
+      dev_ctx* c = ctx_for(pl.dev[g]);
+      if (hipSetDevice(c->dev) != hipSuccess || hipStreamSynchronize(c->stream) != hipSuccess) {
+        rcs[g] = TBLS_DEVICE_ERROR;
+        return;
+      }
+      rcs[g] = settle_range(c, sets.data(), pl.cut[g], pl.cut[g + 1], rand.data(), true, Ls[g], verdict.data() + pl.cut[g]);
+    };
+    run_all(settle);
+    for (int g = 0; g < G; g++)
+      if (rcs[g]) return rcs[g];
+  }
+  for (size_t k = 0; k < n; k++) ok_per_set[pos[k]] = verdict[k];
+  if (n != n_in) *ok = 0;  // a set without keys fails the whole batch as well
+  if (t) {
+    t->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    t->device_ms = 0;
+    for (int g = 0; g < G; g++) {
+      dev_ctx* c = ctx_for(pl.dev[g]);
+      float ms = 0;
+      (void)hipSetDevice(c->dev);
+      (void)hipEventElapsedTime(&ms, c->e_t0, c->e_t1);
+      t->device_ms += ms;
+    }
+    t->n_devices = (uint32_t)G;
+  }
+  return TBLS_SUCCESS;
 }
 
 // --------------------------------------------------------------------------

@@ -303,4 +303,241 @@ __device__ TB_INLINE void miller_accs_body(const uint4* __restrict__ lines, cons
   f_out[(size_t)j * seg_stride + g] = fp12_conj(f);
 }
 
+
+// ---------------------------------------------------------------------------
+// LDS-resident segmented accumulator (round 5, k_miller_accs_lds).  Same
+// segments, groups and output as miller_accs_body; two changes:
+//  * f lives in LDS (36 uint4 = 576 B per lane, 36,864 B per 64-lane
+//    workgroup, 147 KB per CU at one wave per SIMD): the products read f's
+//    Fp2 coefficients when they use them and write each new coefficient once
+//    it is final, so f no longer shares the register file with a line, the
+//    partial results and a product's temporaries.  Round 4's register-resident
+//    f spilled ~375 B of scratch per sparse line product (3.3 GB of scratch
+//    writes per 131k launch against 38 MB of output, profiles/pmc_traffic.json);
+//  * the valid pairs' lines of a step are multiplied together two at a time
+//    (6 Fp2 products: (A1 + B1 v + C1 vw)(A2 + B2 v + C2 vw) has an Fp6 part
+//    x0 + x1 v + x2 v^2 and a w part y1 v + y2 v^2) and f is multiplied by the
+//    product (17: f0 x0 + v f1 y, (f0 + f1)(x + y) - ...), 23 Fp2 products
+//    per two lines instead of 26; an odd line left over takes the sparse
+//    product (13).
+// Layout: element q of lane l at F[q * TB_BLOCK + l]; Fp2 k of f (fp12
+// order f0.c0 f0.c1 f0.c2 f1.c0 f1.c1 f1.c2) is elements 6k .. 6k + 5, so a
+// wave's 16-byte accesses are consecutive (no bank conflicts).
+// ---------------------------------------------------------------------------
+namespace {
+struct lds12 {
+  uint4* p;  // &F[threadIdx.x]
+  int k0;    // first Fp2 held: 0 (all of f), 3 (f1 only)
+  __device__ TB_INLINE fp2 ld(int k) const {
+    fp2 r;
+    k -= k0;
+    TB_UNROLL for (int j = 0; j < 3; j++) {
+      const uint4 a = p[(6 * k + j) * TB_BLOCK], b = p[(6 * k + 3 + j) * TB_BLOCK];
+      r.c0.l[4 * j] = a.x, r.c0.l[4 * j + 1] = a.y, r.c0.l[4 * j + 2] = a.z, r.c0.l[4 * j + 3] = a.w;
+      r.c1.l[4 * j] = b.x, r.c1.l[4 * j + 1] = b.y, r.c1.l[4 * j + 2] = b.z, r.c1.l[4 * j + 3] = b.w;
+    }
+    return r;
+  }
+  __device__ TB_INLINE void st(int k, const fp2& v) const {
+    k -= k0;
+    TB_UNROLL for (int j = 0; j < 3; j++) {
+      p[(6 * k + j) * TB_BLOCK] = make_uint4(v.c0.l[4 * j], v.c0.l[4 * j + 1], v.c0.l[4 * j + 2], v.c0.l[4 * j + 3]);
+      p[(6 * k + 3 + j) * TB_BLOCK] = make_uint4(v.c1.l[4 * j], v.c1.l[4 * j + 1], v.c1.l[4 * j + 2], v.c1.l[4 * j + 3]);
+    }
+    asm volatile("" ::: "memory");  // keep later uses reading LDS, not a forwarded register copy
+  }
+  __device__ TB_INLINE fp6 ld6(int h) const { return {ld(3 * h), ld(3 * h + 1), ld(3 * h + 2)}; }
+  __device__ TB_INLINE void st6(int h, const fp6& v) const {
+    st(3 * h, v.c0);
+    st(3 * h + 1, v.c1);
+    st(3 * h + 2, v.c2);
+  }
+};
+
+// a * b with a's coefficients produced on use (a(i), i < 3: an LDS read or a
+// sum of two), b in registers; Karatsuba, 6 fenced Fp2 products
+template <class A>
+__device__ TB_INLINE fp6 fp6_mul_g(const A& a, const fp6& b) {
+  const fp2 t0 = m2(a(0), b.c0);
+  const fp2 t1 = m2(a(1), b.c1);
+  const fp2 t2 = m2(a(2), b.c2);
+  const fp2 c0 = fp2_add(t0, fp2_mul_xi(fp2_sub(m2(fp2_add_nr(a(1), a(2)), fp2_add_nr(b.c1, b.c2)), fp2_add(t1, t2))));
+  const fp2 c1 = fp2_add(fp2_sub(m2(fp2_add_nr(a(0), a(1)), fp2_add_nr(b.c0, b.c1)), fp2_add(t0, t1)), fp2_mul_xi(t2));
+  const fp2 c2 = fp2_add(fp2_sub(m2(fp2_add_nr(a(0), a(2)), fp2_add_nr(b.c0, b.c2)), fp2_add(t0, t2)), t1);
+  return {c0, c1, c2};
+}
+
+// a * (b0 + b1 v), 5 products
+template <class A>
+__device__ TB_INLINE fp6 fp6_mul_by_01_g(const A& a, const fp2& b0, const fp2& b1) {
+  const fp2 t0 = m2(a(0), b0);
+  const fp2 t1 = m2(a(1), b1);
+  const fp2 c0 = fp2_add(t0, fp2_mul_xi(m2(a(2), b1)));
+  const fp2 c1 = fp2_sub(fp2_sub(m2(fp2_add_nr(a(0), a(1)), fp2_add_nr(b0, b1)), t0), t1);
+  const fp2 c2 = fp2_add(t1, m2(a(2), b0));
+  return {c0, c1, c2};
+}
+
+// a * (y1 v + y2 v^2), 5 products: xi (a1 y2 + a2 y1) + (a0 y1 + xi a2 y2) v + (a0 y2 + a1 y1) v^2
+template <class A>
+__device__ TB_INLINE fp6 fp6_mul_by_12_g(const A& a, const fp2& y1, const fp2& y2) {
+  const fp2 p1 = m2(a(1), y1);
+  const fp2 p2 = m2(a(2), y2);
+  const fp2 m = fp2_sub(m2(fp2_add_nr(a(1), a(2)), fp2_add_nr(y1, y2)), fp2_add(p1, p2));
+  const fp2 c1 = fp2_add(m2(a(0), y1), fp2_mul_xi(p2));
+  const fp2 c2 = fp2_add(m2(a(0), y2), p1);
+  return {fp2_mul_xi(m), c1, c2};
+}
+
+// the product of two lines, x0 + x1 v + x2 v^2 + (y1 v + y2 v^2) w (w^2 = v, v^3 = xi):
+// x0 = A1 A2 + xi C1 C2, x1 = A1 B2 + B1 A2, x2 = B1 B2, y1 = A1 C2 + C1 A2,
+// y2 = B1 C2 + C1 B2 -- 6 products (Karatsuba for the cross terms)
+struct line2 {
+  fp6 x;
+  fp2 y1, y2;
+};
+__device__ TB_INLINE line2 line_mul(const line3& l1, const line3& l2) {
+  const fp2 aa = m2(l1.a, l2.a), bb = m2(l1.b, l2.b), cc = m2(l1.c, l2.c);
+  line2 r;
+  r.x.c0 = fp2_add(aa, fp2_mul_xi(cc));
+  r.x.c1 = fp2_sub(m2(fp2_add_nr(l1.a, l1.b), fp2_add_nr(l2.a, l2.b)), fp2_add(aa, bb));
+  r.x.c2 = bb;
+  r.y1 = fp2_sub(m2(fp2_add_nr(l1.a, l1.c), fp2_add_nr(l2.a, l2.c)), fp2_add(aa, cc));
+  r.y2 = fp2_sub(m2(fp2_add_nr(l1.b, l1.c), fp2_add_nr(l2.b, l2.c)), fp2_add(bb, cc));
+  return r;
+}
+
+// f <- f^2 in LDS: ab = f0 f1, t = (f0 + f1)(f0 + v f1); f0 = t - ab - v ab, f1 = 2 ab (12 products)
+__device__ TB_INLINE void fp12_sqr_lds(const lds12& F) {
+  const fp6 f1 = F.ld6(1);
+  const fp6 ab = fp6_mul_g([&](int i) { return F.ld(i); }, f1);
+  const fp6 b = {fp2_add(F.ld(0), fp2_mul_xi(f1.c2)), fp2_add(F.ld(1), f1.c0), fp2_add(F.ld(2), f1.c1)};  // f0 + v f1
+  TB_FENCE();
+  const fp6 t = fp6_mul_g([&](int i) { return fp2_add(F.ld(i), F.ld(3 + i)); }, b);
+  F.st6(0, fp6_sub(fp6_sub(t, ab), fp6_mul_v(ab)));
+  F.st6(1, fp6_add(ab, ab));
+}
+
+// f <- f * line, line = (A + B v) + (C v) w, in LDS (13 products)
+__device__ TB_INLINE void fp12_mul_line_lds(const lds12& F, const line3& l) {
+  const fp6 t1 = {fp2_mul_xi(m2(F.ld(5), l.c)), m2(F.ld(3), l.c), m2(F.ld(4), l.c)};
+  const fp6 t0 = fp6_mul_by_01_g([&](int i) { return F.ld(i); }, l.a, l.b);
+  const fp6 u = fp6_mul_by_01_g([&](int i) { return fp2_add(F.ld(i), F.ld(3 + i)); }, l.a, fp2_add_nr(l.b, l.c));
+  F.st6(1, fp6_sub(fp6_sub(u, t0), t1));
+  F.st6(0, fp6_add(t0, fp6_mul_v(t1)));
+}
+
+// f <- f * (l1 l2), in LDS (17 products): c0 = f0 x + v (f1 y), c1 = (f0 + f1)(x + y) - f0 x - f1 y
+__device__ TB_INLINE void fp12_mul_line2_lds(const lds12& F, const line2& L) {
+  const fp6 p0 = fp6_mul_g([&](int i) { return F.ld(i); }, L.x);
+  const fp6 p1 = fp6_mul_by_12_g([&](int i) { return F.ld(3 + i); }, L.y1, L.y2);
+  const fp6 xy = {L.x.c0, fp2_add(L.x.c1, L.y1), fp2_add(L.x.c2, L.y2)};
+  TB_FENCE();
+  const fp6 s = fp6_mul_g([&](int i) { return fp2_add(F.ld(i), F.ld(3 + i)); }, xy);
+  F.st6(1, fp6_sub(fp6_sub(s, p0), p1));
+  F.st6(0, fp6_add(p0, fp6_mul_v(p1)));
+}
+}  // namespace
+
+// The same products with f0 in registers and only f1 in LDS (18,432 B per
+// workgroup, 73,728 B per CU at one wave per SIMD): a CU keeps LDS for a
+// concurrent kernel's workgroup beside four accumulator waves (the bucket-sum
+// pairs' k_miller_wave, 28 KB, runs beside the accumulator on the bucket-sum
+// stream; with all of f in LDS its workgroups pushed 64 accumulator
+// workgroups into a second round: 131k step 38.2 -> 43.9 ms,
+// profiles/r05_bench_acc_lds_ab.json).
+__device__ TB_INLINE const fp2& c6(const fp6& a, int i) { return i == 0 ? a.c0 : i == 1 ? a.c1 : a.c2; }
+
+__device__ TB_INLINE void fp12_sqr_h(fp6& f0, const lds12& F) {
+  const fp6 f1 = F.ld6(1);
+  const fp6 ab = fp6_mul_f(f0, f1);
+  const fp6 b = {fp2_add(f0.c0, fp2_mul_xi(f1.c2)), fp2_add(f0.c1, f1.c0), fp2_add(f0.c2, f1.c1)};  // f0 + v f1
+  const fp6 a = fp6_add_nr(f0, f1);
+  TB_FENCE();
+  const fp6 t = fp6_mul_f(a, b);
+  f0 = fp6_sub(fp6_sub(t, ab), fp6_mul_v(ab));
+  F.st6(1, fp6_add(ab, ab));
+}
+
+__device__ TB_INLINE void fp12_mul_line_h(fp6& f0, const lds12& F, const line3& l) {
+  const fp6 t1 = {fp2_mul_xi(m2(F.ld(5), l.c)), m2(F.ld(3), l.c), m2(F.ld(4), l.c)};
+  const fp6 t0 = fp6_mul_by_01_f(f0, l.a, l.b);
+  const fp6 u = fp6_mul_by_01_g([&](int i) { return fp2_add(c6(f0, i), F.ld(3 + i)); }, l.a, fp2_add_nr(l.b, l.c));
+  F.st6(1, fp6_sub(fp6_sub(u, t0), t1));
+  f0 = fp6_add(t0, fp6_mul_v(t1));
+}
+
+__device__ TB_INLINE void fp12_mul_line2_h(fp6& f0, const lds12& F, const line2& L) {
+  const fp6 p0 = fp6_mul_f(f0, L.x);
+  const fp6 p1 = fp6_mul_by_12_g([&](int i) { return F.ld(3 + i); }, L.y1, L.y2);
+  const fp6 xy = {L.x.c0, fp2_add(L.x.c1, L.y1), fp2_add(L.x.c2, L.y2)};
+  TB_FENCE();
+  const fp6 s = fp6_mul_g([&](int i) { return fp2_add(c6(f0, i), F.ld(3 + i)); }, xy);
+  F.st6(1, fp6_sub(fp6_sub(s, p0), p1));
+  f0 = fp6_add(p0, fp6_mul_v(p1));
+}
+
+template <bool HALF>
+__device__ TB_INLINE void miller_accs_lds_body(uint4* __restrict__ Fsh, const uint4* __restrict__ lines, const uint8_t* __restrict__ skip,
+                                               const uint8_t* __restrict__ code_a, const uint8_t* __restrict__ code_b, uint32_t n,
+                                               uint32_t per, uint32_t nseg, uint32_t g_pad, fp12* __restrict__ f_out, uint32_t seg_stride) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t j = t / g_pad, g = t % g_pad;
+  const uint32_t G = (n + per - 1) / per;
+  if (j >= nseg || g >= G) return;
+  const int s_lo = (int)(TB_LINE_STEPS * j / nseg), s_hi = (int)(TB_LINE_STEPS * (j + 1) / nseg);
+  const lds12 F{Fsh + threadIdx.x, HALF ? 3 : 0};
+  fp6 f0;  // HALF: f0 in registers
+  uint32_t usem = 0;  // group g owns pairs g, g + G, ... (coalesced line reads, as miller_accs_body)
+  for (uint32_t k = 0; k < per; k++) {
+    const uint32_t i = g + k * G;
+    if (i < n && skip[i] == 0 && code_a[i] == 0 && code_b[i] == 0) usem |= 1u << k;
+  }
+  bool fresh = true;  // f == 1 (not yet written)
+  TB_NOUNROLL for (int s = s_lo; s < s_hi; s++) {
+    if (!fresh && step_is_dbl(s)) {
+      if (HALF)
+        fp12_sqr_h(f0, F);
+      else
+        fp12_sqr_lds(F);
+    }
+    uint32_t m = usem;
+    TB_NOUNROLL while (m) {
+      const uint32_t k1 = __builtin_ctz(m);
+      m &= m - 1;
+      const line3 l1 = line_load(lines, n, g + k1 * G, s);
+      if (m) {  // two lines: their product first
+        const uint32_t k2 = __builtin_ctz(m);
+        m &= m - 1;
+        const line2 L = line_mul(l1, line_load(lines, n, g + k2 * G, s));
+        if (fresh) {
+          if (HALF)
+            f0 = L.x;
+          else
+            F.st6(0, L.x);
+          F.st6(1, {fp2_zero(), L.y1, L.y2});
+          fresh = false;
+        } else if (HALF) {
+          fp12_mul_line2_h(f0, F, L);
+        } else {
+          fp12_mul_line2_lds(F, L);
+        }
+      } else if (fresh) {
+        if (HALF)
+          f0 = {l1.a, l1.b, fp2_zero()};
+        else
+          F.st6(0, {l1.a, l1.b, fp2_zero()});
+        F.st6(1, {fp2_zero(), l1.c, fp2_zero()});
+        fresh = false;
+      } else if (HALF) {
+        fp12_mul_line_h(f0, F, l1);
+      } else {
+        fp12_mul_line_lds(F, l1);
+      }
+    }
+  }
+  fp12 f = fresh ? fp12_one() : fp12{HALF ? f0 : F.ld6(0), F.ld6(1)};
+  f_out[(size_t)j * seg_stride + g] = fp12_conj(f);
+}
+
 }  // namespace tb

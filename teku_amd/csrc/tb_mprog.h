@@ -16,9 +16,11 @@
 
 namespace tb {
 
-struct mprog_lds {
-  fp S[2 * MP_NSLOT];  // values, then their negations 2p - v (wprog_level)
+struct mprog_lds_g {  // tables read from global memory (k_miller_wave_g): 16,288 B of LDS
+  fp S[2 * MP_NSLOT];    // values, then their negations 2p - v (wprog_level)
   u13 part[64];
+};
+struct mprog_lds : mprog_lds_g {  // tables staged in LDS: 34,464 B
   uint16_t tab[MP_TAB_N];
 };
 
@@ -110,15 +112,15 @@ __device__ TB_INLINE void wprog_level(fp* S, u13* part, const uint16_t* tab, int
   __syncthreads();
 }
 
-__device__ TB_INLINE void mp_level(mprog_lds& L, int type) {
-  wprog_level<MP_AMAX, MP_BMAX, MP_QMAX, MP_OMAX, MP_NSLOT>(L.S, L.part, L.tab, MP_TYPE_OFF[type]);
-}
-
 // f_{|x|,Q}(P) (up to a factor in Fp), conjugated, into L.S[0..12) -- the
-// Fp12 coordinates in tb_fp12_wave.h order; whole workgroup of 64 lanes
-__device__ TB_INLINE void miller_loop_prog(mprog_lds& L, const g1a& P, const g2a& Q) {
+// Fp12 coordinates in tb_fp12_wave.h order; whole workgroup of 64 lanes.
+// tab: the level tables, staged in LDS (mprog_lds) or read in place from
+// global memory (the constant table MP_TAB, cached: k_miller_wave_g).
+template <class LDS>
+__device__ TB_INLINE void miller_loop_prog(LDS& L, const uint16_t* tab, const g1a& P, const g2a& Q) {
   const int l = threadIdx.x;
-  for (int i = l; i < MP_TAB_N; i += blockDim.x) L.tab[i] = MP_TAB[i];
+  if constexpr (sizeof(LDS) == sizeof(mprog_lds))
+    for (int i = l; i < MP_TAB_N; i += blockDim.x) reinterpret_cast<mprog_lds&>(L).tab[i] = MP_TAB[i];
   for (int i = l; i < MP_NSLOT; i += blockDim.x) L.S[i] = fp_zero();
   __syncthreads();
   if (l == 0) {
@@ -136,8 +138,14 @@ __device__ TB_INLINE void miller_loop_prog(mprog_lds& L, const g1a& P, const g2a
     L.S[MP_S_PY] = P.y;
   }
   wprog_negate_all<MP_NSLOT>(L.S);
-  for (int k = 0; k < MP_NLEVEL; k++) mp_level(L, MP_SEQ[k]);
+  for (int k = 0; k < MP_NLEVEL; k++) wprog_level<MP_AMAX, MP_BMAX, MP_QMAX, MP_OMAX, MP_NSLOT>(L.S, L.part, tab, MP_TYPE_OFF[MP_SEQ[k]]);
   w_conj(L.S + MP_S_F0, L.S + MP_S_F0);
+}
+
+// the tables staged in LDS (k_miller_wave, tests/native/k_test.hip)
+__device__ TB_INLINE void miller_loop_prog(mprog_lds& L, const g1a& P, const g2a& Q) { miller_loop_prog(L, L.tab, P, Q); }
+__device__ TB_INLINE void mp_level(mprog_lds& L, int type) {
+  wprog_level<MP_AMAX, MP_BMAX, MP_QMAX, MP_OMAX, MP_NSLOT>(L.S, L.part, L.tab, MP_TYPE_OFF[type]);
 }
 
 }  // namespace tb

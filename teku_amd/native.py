@@ -118,6 +118,11 @@ _SIGS = {
         ],
     ),
     "tbls_fast_aggregate_verify_many": (ctypes.c_int, [ctypes.POINTER(TblsSet), ctypes.c_size_t, ctypes.POINTER(ctypes.c_int)]),
+    "tbls_batch_verify_each": (
+        ctypes.c_int,
+        [ctypes.POINTER(TblsSet), ctypes.c_size_t, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int, ctypes.POINTER(ctypes.c_int),
+         ctypes.POINTER(ctypes.c_int), ctypes.POINTER(TblsTiming)],
+    ),
     "tbls_verify_each": (ctypes.c_int, [ctypes.POINTER(TblsSet), ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
     "tbls_pk_validate_many": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p]),
     "tbls_sig_validate_many": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_char_p]),

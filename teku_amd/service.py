@@ -10,13 +10,15 @@ BLS.batchVerify (batchVerifySignatures, l.188-205).
 The difference is the failure path.  The reference, when a batch fails,
 halves it recursively down to min_batch_size_to_split tasks and then verifies
 each remaining task alone (l.211-227, splitTasks l.230-233): O(bad * log n)
-extra batch verifications, each a full GPU round trip.  Here a failed batch
-costs ONE more device pass: tbls_verify_each returns every set's
-fastAggregateVerify verdict, and a task is valid iff all its sets are
+extra batch verifications, each a full GPU round trip.  Here the batch and its
+failure path are one call, tbls_batch_verify_each: when the batch fails, the
+library settles every set's fastAggregateVerify verdict from the batch's own
+Miller work on the same devices (group tests over 256- and 16-set groups, then
+single sets), and a task is valid iff all its sets are
 (BLSSignatureVerifier.SIMPLE.verify -> BLS.batchVerify over the task's sets,
 BLSSignatureVerifier.java:27-43, which is the same boolean with overwhelming
 probability).  `split_fallback=True` restores the reference's halving, for
-comparison.
+comparison; a custom batch_fn keeps the batch + per-set pass of round 4.
 
 Defaults follow the GPU: one submitting thread (the device queue serialises
 anyway; the reference uses up to #cores, P2POptions.java:324-359) and a large
@@ -72,6 +74,11 @@ def _hip_batch(sets, timing=None) -> bool:
 
 def _hip_each(sets) -> List[bool]:
     return SetArray.from_tuples(sets).verify_each()
+
+
+def _hip_batch_each(sets, timing=None):
+    """(batch verdict, per-set verdicts) in one device call (tbls_batch_verify_each)."""
+    return SetArray.from_tuples(sets).batch_verify_each(fast_multipliers(len(sets)), timing=timing)
 
 
 class AggregatingSignatureVerificationService:
@@ -186,6 +193,24 @@ class AggregatingSignatureVerificationService:
             t.result.set_result(False)
         tasks = [t for t in tasks if t.sets]
         if not tasks:
+            return
+        if self._batch_fn is _hip_batch and not self.split_fallback:
+            self.device_passes += 1
+            t = native.TblsTiming()
+            try:
+                ok, verdicts = _hip_batch_each(all_sets, timing=t)
+            except ValueError:
+                ok, verdicts = False, [False] * len(all_sets)
+            self.sets_verified += len(all_sets)
+            self.device_ms_total += t.device_ms
+            self.host_ms_total += t.total_ms
+            self.last_batch_timing = {"sets": len(all_sets), "device_ms": t.device_ms, "total_ms": t.total_ms, "n_devices": t.n_devices,
+                                      "settled": not ok}
+            k = 0
+            for task in tasks:
+                n = len(task.sets)
+                task.result.set_result(ok or all(verdicts[k : k + n]))
+                k += n
             return
         self.device_passes += 1
         if self._batch_timed(all_sets):

@@ -189,6 +189,22 @@ class SetArray:
         native.check(rc, "tbls_batch_verify")
         return ok.value == 1
 
+    def batch_verify_each(self, rands: Sequence[int], n_gpus: int = 0, timing: "native.TblsTiming" = None):
+        """(batch verdict, per-set verdicts): tbls_batch_verify_each -- the
+        randomized batch, and when it fails every set's verdict settled from
+        the batch's own work (per-set values are all True when it passes)."""
+        if isinstance(rands, np.ndarray):
+            assert rands.dtype == np.uint64 and rands.flags.c_contiguous and len(rands) >= self.n
+            rr = rands.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))
+        else:
+            rr = (ctypes.c_uint64 * max(1, self.n))(*rands)
+        ok = ctypes.c_int(0)
+        each = (ctypes.c_int * max(1, self.n))()
+        rc = native.lib().tbls_batch_verify_each(self.ptr, self.n, rr, n_gpus, ctypes.byref(ok), each,
+                                                  ctypes.byref(timing) if timing is not None else None)
+        native.check(rc, "tbls_batch_verify_each")
+        return ok.value == 1, [v == 1 for v in each[: self.n]]
+
     def fast_aggregate_verify_many(self) -> List[bool]:
         ok = (ctypes.c_int * max(1, self.n))()
         native.check(native.lib().tbls_fast_aggregate_verify_many(self.ptr, self.n, ok), "tbls_fast_aggregate_verify_many")

@@ -110,6 +110,18 @@ def main():
         sq_ = sum(sum(dbl[68 * j // nseg:68 * (j + 1) // nseg]) - dbl[68 * j // nseg] for j in range(nseg))
         accs = (sq_ * SQR12 + (per * 68 - nseg) * LINE12) / per
         res[f"miller_seg_{per}x{nseg}"] = res["miller"] - acc2 + accs
+    # k_miller_accs_lds (round 5): the valid pairs' lines of a step multiplied
+    # two at a time (line_mul: 6 Fp2 products = 18 M) and f by their product
+    # (fp12_mul_line2_lds: 17 = 51 M), an odd line left over by the sparse
+    # product (39 M); a segment's first step stores its first product (or line)
+    # as f.  miller_seg2_PxS.
+    PAIR12, LMUL = 51 + 18, 18
+    for per, nseg in ((2, 16), (4, 16), (8, 16), (16, 4), (16, 8), (16, 16), (32, 8)):
+        sq_ = sum(sum(dbl[68 * j // nseg:68 * (j + 1) // nseg]) - dbl[68 * j // nseg] for j in range(nseg))
+        step = (per // 2) * PAIR12 + (per % 2) * LINE12
+        first = (LMUL + ((per - 2) // 2) * PAIR12 + ((per - 2) % 2) * LINE12) if per >= 2 else 0
+        accs = (sq_ * SQR12 + (68 - nseg) * step + nseg * first) / per
+        res[f"miller_seg2_{per}x{nseg}"] = res["miller"] - acc2 + accs
     f = [tuple(tuple((i + j + k, 3 * i + 1) for k in range(3)) for j in range(2)) for i in range(2)]
     # one Fp12 product per accumulator, i.e. per two pairs
     res["fp12_prod"] = per_unit("FP12_MUL", [enc_fp12(f[0]) + enc_fp12(f[1])], units_per_rec=2, name="fp12_prod")
