@@ -20,6 +20,10 @@
 
 using namespace tb;
 
+#ifndef TB_HASH_SSWU_SEQ
+#define TB_HASH_SSWU_SEQ 0
+#endif
+
 namespace {
 // g2_clear_cofactor_nx in an order that keeps at most two points besides the
 // loop state live in registers, the caller's LDS slot *stash holding a third:
@@ -68,7 +72,14 @@ extern "C" __global__ void __launch_bounds__(TB_BLOCK, 2)
   fp2 u0, u1;
   hash_to_field_fp2(u0, u1, c);
   g2a q0, q1;
+#if TB_HASH_SSWU_SEQ
+  // the two maps one after the other (an inversion and two exponentiations
+  // each): one map's state and one window table live at a time
+  q0 = map_to_curve_sswu(u0);
+  q1 = map_to_curve_sswu(u1);
+#else
   map_to_curve_sswu2(q0, q1, u0, u1);
+#endif
   const g2j p = iso_map_jac(e2p_add_aff_aff(q0, q1));
   g2j h;
   if (!g2_clear_cofactor_nx_stash(h, p, &stash[threadIdx.x])) {

@@ -502,9 +502,10 @@ void launch_set_pk(hipStream_t s, uint32_t n, uint32_t n_entries, const uint32_t
 // product (tb_lines.h miller_accs_lds_body).  Measured at 131,072 sets
 // (profiles/r05_bench_acc_lds_ab.json): Miller stage alone 13.3 -> 12.6 ms
 // and scratch writes 3.3 -> 1.5 GB per launch, but beside the bucket-sum
-// stream's workgroups (k_msm_bucket_sum, 18 KB of LDS each) part of its
-// one-round grid (4 x 36,864 B per CU) found no CU with the LDS free and ran
-// a second round: 131k step 38.2 -> 43.9 ms; waiting for that stream first
+// stream's kernels part of its one-round grid (4 x 36,864 B of LDS per CU)
+// ran a second round -- most likely workgroups of that stream holding LDS on
+// the CUs (the bit-sum pairs' wave Miller loops moved to a 16 KB form did not
+// change it): 131k step 38.2 -> 43.9 ms; waiting for that stream first
 // (TBLS_ACC_JOIN=1) gives 38.5.  So by default it runs where nothing runs
 // beside it -- batches without bucket sums (< 20,480 sets: config 4) and the
 // per-set settling of a failed batch -- and the register-resident
