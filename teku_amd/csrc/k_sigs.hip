@@ -232,30 +232,66 @@ extern "C" __global__ void __launch_bounds__(64) k_msm_bucket_sum(const g2j* __r
   if (t == 0) bucket[b] = sh[0];
 }
 
+// Round 5: k_msm_bucket + k_msm_bucket_sum fused, without LDS.  Block
+// (w, d != 0), 64 lanes: lane c sums chunk c of bucket b's list (the chunks
+// of k_msm_bucket), then a 6-level tree across the lanes with the points moved
+// by lane shuffles (72 words per level) instead of an LDS array -- no 37.7 MB
+// partial-sum buffer written and read back, one launch fewer, and no 18 KB of
+// LDS per workgroup held beside the Miller accumulator (whose one-round grid
+// needs every CU's LDS when it keeps f there, tb_lib.hip acc_lds).  Same
+// bucket sums as the two kernels (the group law is associative and
+// commutative; the sums are made affine in k_msm_bitsum_pairs).
+__device__ TB_INLINE g2j shfl_down_g2j(const g2j& p, int s) {
+  g2j r;
+  const uint32_t* a = reinterpret_cast<const uint32_t*>(&p);
+  uint32_t* o = reinterpret_cast<uint32_t*>(&r);
+  TB_UNROLL for (int k = 0; k < (int)(sizeof(g2j) / 4); k++) o[k] = __shfl_down(a[k], s, 64);
+  return r;
+}
+
+extern "C" __global__ void __launch_bounds__(64)
+    k_msm_bucket_tree(const g2a* __restrict__ sig_aff, const uint8_t* __restrict__ use, const uint32_t* __restrict__ off,
+                      const uint32_t* __restrict__ idx, g2j* __restrict__ bucket) {
+  const uint32_t c = threadIdx.x;
+  const uint32_t w = blockIdx.x / (TB_MSM_NB - 1), d = blockIdx.x % (TB_MSM_NB - 1) + 1, b = w * TB_MSM_NB + d;
+  const uint32_t lo = off[b], hi = off[b + 1];
+  const uint32_t len = hi - lo, chunk = (len + TB_MSM_CHUNKS - 1) / TB_MSM_CHUNKS;
+  uint32_t s = lo + c * chunk, e = s + chunk;
+  if (e > hi) e = hi;
+  g2j acc = jac_inf<fp2>();
+  for (uint32_t k = s; k < e; k++) {
+    const uint32_t i = idx[k];
+    if (use[i]) acc = jac_add_aff(acc, sig_aff[i]);  // invalid sets fail the batch anyway; infinity adds nothing
+  }
+  for (int sh = 32; sh > 0; sh >>= 1) {
+    const g2j other = shfl_down_g2j(acc, sh);
+    if (c < (uint32_t)sh) acc = jac_add(acc, other);
+  }
+  if (c == 0) bucket[b] = acc;
+}
+
 // block j = 8w + k: V = sum of the 128 bucket sums B[w][d] whose digit d has
 // bit k set, so that sum_d d B[w][d] = sum_k 2^k V[w][k]; pair slot j =
 // (-(2^(8w+k)) g1, V) with the G1 point from the comb table (d = 2^k), skipped
 // when V is infinity.  Lane l sums the digits of rank l and l + 64 among the
-// 128 with bit k set, then a 64-lane LDS tree.
+// 128 with bit k set, then a 64-lane tree of lane shuffles (no LDS: see
+// k_msm_bucket_tree).
 extern "C" __global__ void __launch_bounds__(64)
     k_msm_bitsum_pairs(const g2j* __restrict__ bucket, const g1a* __restrict__ comb, g1a* __restrict__ P, g2a* __restrict__ Q,
                        uint8_t* __restrict__ skip) {
-  __shared__ g2j sh[64];
   const uint32_t t = threadIdx.x, w = blockIdx.x / 8, k = blockIdx.x % 8;
   g2j acc = jac_inf<fp2>();
   for (uint32_t r = t; r < 128; r += 64) {
     const uint32_t d = ((r >> k) << (k + 1)) | (1u << k) | (r & ((1u << k) - 1u));  // r-th digit with bit k set
     acc = jac_add(acc, bucket[w * TB_MSM_NB + d]);
   }
-  sh[t] = acc;
-  __syncthreads();
-  for (uint32_t s = 32; s > 0; s >>= 1) {
-    if (t < s) sh[t] = jac_add(sh[t], sh[t + s]);
-    __syncthreads();
+  for (int sh = 32; sh > 0; sh >>= 1) {
+    const g2j other = shfl_down_g2j(acc, sh);
+    if (t < (uint32_t)sh) acc = jac_add(acc, other);
   }
   if (t == 0) {
     g2a a;
-    const bool ok = jac_to_aff(a, sh[0]);
+    const bool ok = jac_to_aff(a, acc);
     if (!ok) {
       a.x = fp2_zero();
       a.y = fp2_zero();

@@ -20,8 +20,13 @@
 
 using namespace tb;
 
+// The two SSWU maps one after the other (1, default) or interleaved with a
+// shared inversion (0, map_to_curve_sswu2, rounds 2-4): at 256 registers the
+// interleaved pair's two states and two window tables spilled -- hash traffic
+// 11.2 -> 10.2 GB per 131k launch sequential, stage time unchanged (11.6 ms;
+// profiles/r05_bench_sswu_seq_ab.json).
 #ifndef TB_HASH_SSWU_SEQ
-#define TB_HASH_SSWU_SEQ 0
+#define TB_HASH_SSWU_SEQ 1
 #endif
 
 namespace {

@@ -416,7 +416,7 @@ struct ws_layout {
     msm_off = o;  o = align_up(o + (msm ? (TB_MSM_BUCKETS + 1) * 4 : 0));
     msm_cur = o;  o = align_up(o + (msm ? TB_MSM_BUCKETS * 4 : 0));
     msm_idx = o;  o = align_up(o + nm * 8 * 4);
-    msm_part = o; o = align_up(o + (msm ? (size_t)TB_MSM_PARTS * sizeof(g2j) : 0));
+    msm_part = o;  // (round 4's chunk sums: k_msm_bucket_tree keeps them in registers)
     msm_sum = o;  o = align_up(o + (msm ? (size_t)TB_MSM_BUCKETS * sizeof(g2j) : 0));
     mlist = o;    o = align_up(o + (size_t)n * 4);
     mcnt = o;     o = align_up(o + 4);
@@ -514,6 +514,8 @@ void launch_set_pk(hipStream_t s, uint32_t n, uint32_t n_entries, const uint32_t
 extern "C" __global__ void k_miller_accs_lds(const uint4* __restrict__ lines, const uint8_t* __restrict__ skip, const uint8_t* __restrict__ code_a,
                                              const uint8_t* __restrict__ code_b, uint32_t n, uint32_t per, uint32_t nseg, uint32_t g_pad,
                                              fp12* __restrict__ f_out, uint32_t seg_stride);
+extern "C" __global__ void k_msm_bucket_tree(const g2a* __restrict__ sig_aff, const uint8_t* __restrict__ use, const uint32_t* __restrict__ off,
+                                             const uint32_t* __restrict__ idx, g2j* __restrict__ bucket);  // k_sigs.hip
 extern "C" __global__ void k_miller_wave_g(const g1a* __restrict__ P, const g2a* __restrict__ Q, const uint8_t* __restrict__ skip,
                                            const uint8_t* __restrict__ code_a, const uint8_t* __restrict__ code_b, uint32_t n,
                                            fp12* __restrict__ f);  // k_mwave.hip: level tables from global memory
@@ -616,9 +618,8 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
   if (late_join) HIPCHK(hipEventRecord(c.e_sig, sb));
   TB_EV(8, sb);
   if (pp.msm) {
-    hipLaunchKernelGGL(k_msm_bucket, dim3(TB_MSM_PARTS / TB_BLOCK), blk, 0, sb, (const g2a*)(w + L.sig_aff), (const uint8_t*)(w + L.sig_use),
-                       (const uint32_t*)msm_off, (const uint32_t*)msm_idx, (g2j*)(w + L.msm_part));
-    hipLaunchKernelGGL(k_msm_bucket_sum, dim3(TB_MSM_NSUM), dim3(64), 0, sb, (const g2j*)(w + L.msm_part), (g2j*)(w + L.msm_sum));
+    hipLaunchKernelGGL(k_msm_bucket_tree, dim3(TB_MSM_NSUM), dim3(64), 0, sb, (const g2a*)(w + L.sig_aff), (const uint8_t*)(w + L.sig_use),
+                       (const uint32_t*)msm_off, (const uint32_t*)msm_idx, (g2j*)(w + L.msm_sum));
     hipLaunchKernelGGL(k_msm_bitsum_pairs, dim3(TB_MSM_XPAIRS), dim3(64), 0, sb, (const g2j*)(w + L.msm_sum), c.comb.as<const g1a>(),
                        P + n, Q + n, skip + n);
     if (pp.n_xwave)  // their Miller loops, one wave each, on this stream: f[n_f_main ..)
