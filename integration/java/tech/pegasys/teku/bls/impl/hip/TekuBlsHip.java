@@ -46,6 +46,11 @@ final class TekuBlsHip {
   static native int batchVerify(byte[] pks, int[] nPks, byte[] msgs, int[] msgOff, byte[] sigs, long[] rand,
                                 int nGpus, int[] ok); // tbls_batch_verify
 
+  /* batchVerify + every set's verdict when the batch fails, settled from the
+   * batch's own Miller work (okPerSet[n]; all 1 when ok[0] == 1) */
+  static native int batchVerifyEach(byte[] pks, int[] nPks, byte[] msgs, int[] msgOff, byte[] sigs, long[] rand,
+                                    int nGpus, int[] ok, int[] okPerSet); // tbls_batch_verify_each
+
   /* device-resident validator key table */
   static native int pkTableLoad(byte[] pks, int k, byte[] codes); // tbls_pk_table_load
   static native int batchVerifyIdx(int[] keyIdx, int[] nPks, byte[] msgs, int[] msgOff, byte[] sigs, long[] rand,

@@ -400,6 +400,37 @@ JNIEXPORT jint JNICALL JNAME(batchVerify)(JNIEnv* env, jclass c, jbyteArray pks,
   return rc;
 }
 
+/* batchVerify that also settles every set's verdict when the batch fails,
+ * from the batch's own Miller work (tbls_batch_verify_each): ok[0] the batch
+ * verdict, okPerSet[n] each set's fastAggregateVerify */
+JNIEXPORT jint JNICALL JNAME(batchVerifyEach)(JNIEnv* env, jclass c, jbyteArray pks, jintArray nPks, jbyteArray msgs,
+                                              jintArray msgOff, jbyteArray sigs, jlongArray rand, jint nGpus, jintArray okOut,
+                                              jintArray okPerSet) {
+  (void)c;
+  if (alen(env, okOut) < 1) return TBLS_BAD_ARGUMENT;
+  flat_sets f;
+  int rc = flat_in(env, &f, pks, NULL, nPks, msgs, msgOff, sigs);
+  if (rc == TBLS_SUCCESS && alen(env, okPerSet) < f.n) rc = TBLS_BAD_ARGUMENT;
+  int ok = 0;
+  if (rc == TBLS_SUCCESS) {
+    uint64_t* r = rand_in(env, rand, f.n, &rc);
+    tbls_set* sets = r ? sets_of(f.pk, f.np, f.m, f.mo, f.sg, (size_t)f.n) : NULL;
+    int* each = r ? (int*)calloc(f.n ? (size_t)f.n : 1, sizeof(int)) : NULL;
+    if (r && (!sets || !each)) {
+      rc = TBLS_DEVICE_ERROR;
+    } else if (r) {
+      rc = tbls_batch_verify_each(sets, (size_t)f.n, r, nGpus, &ok, each, NULL);
+      if (f.n) (*env)->SetIntArrayRegion(env, okPerSet, 0, f.n, (const jint*)each);
+    }
+    free(each);
+    free(sets);
+    free(r);
+  }
+  flat_free(&f);
+  set_int(env, okOut, ok);
+  return rc;
+}
+
 JNIEXPORT jint JNICALL JNAME(pkTableLoad)(JNIEnv* env, jclass c, jbyteArray pks, jint k, jbyteArray codes) {
   (void)c;
   jsize pl;

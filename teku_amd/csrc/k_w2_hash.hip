@@ -1,4 +1,5 @@
-// The throughput hash_to_G2 (batches above TB_HASH_PAIR_MAX sets) at two waves
+// The throughput hash_to_G2 (batches above hash_plan().duo_max =
+// TB_HASH_DUO_MAX = 32,768 sets, tb_lib.hip) at two waves
 // per SIMD.
 //
 // An outlined helper is compiled for the register bound of the kernels that

@@ -79,6 +79,20 @@ __device__ TB_INLINE g2j mul_xabs_aff(const g2a& Q, g2a* park) {
   return r;
 }
 
+// Scott's subgroup test on the chain's output: psi(Q) == -t for t = [|x|]Q
+// Jacobian and Q affine finite, with psi(Q) affine (no Z powers on its side):
+// t.X == psi(Q).x Z^2 and -t.Y == psi(Q).y Z^3; Z = 0 is unequal (the finite
+// psi(Q)), as jac_eq(g2_psi(jac_from_aff(Q)), jac_neg(t)).  3 products + the
+// two psi products, inline (jac_eq is an outlined call that spilled the
+// caller's live registers).
+__device__ TB_INLINE bool psi_eq_neg(const g2j& t, const g2a& Q) {
+  const fp2 Z2 = S(t.z);
+  const bool ex = fp2_is_zero(fp2_sub(M(M(fp2_conj(Q.x), fp2_from_const(PSI_CX)), Z2), t.x));
+  const fp2 Z3 = M(Z2, t.z);
+  const bool ey = fp2_is_zero(fp2_add(M(M(fp2_conj(Q.y), fp2_from_const(PSI_CY)), Z3), t.y));
+  return ex && ey && !fp2_is_zero(t.z);
+}
+
 #undef TB_LFENCE
 }  // namespace lean
 }  // namespace tb

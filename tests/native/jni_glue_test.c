@@ -129,6 +129,14 @@ int tbls_verify_each(const tbls_set* sets, size_t n, int g, int* ok) {
   for (size_t i = 0; i < n; i++) ok[i] = 1;
   FAKE_OK()
 }
+int tbls_batch_verify_each(const tbls_set* sets, size_t n, const uint64_t* r, int g, int* ok, int* each, tbls_timing* t) {
+  (void)g, (void)t;
+  for (size_t i = 0; i < n; i++) (void)r[i];
+  take_sets(sets, n);
+  for (size_t i = 0; i < n; i++) each[i] = (int)(i != 1);
+  *ok = n < 2;
+  FAKE_OK()
+}
 int tbls_pk_validate_many(const uint8_t* p, size_t n, uint8_t* c) { (void)p; memset(c, 0, n); FAKE_OK() }
 int tbls_sig_validate_many(const uint8_t* s, size_t n, uint8_t* c, uint8_t* inf) { (void)s; memset(c, 0, n); memset(inf, 0, n); FAKE_OK() }
 int tbls_aggregate_sigs_many(const uint8_t* s, const uint32_t* off, size_t g, uint8_t* o, int* st) {
@@ -144,6 +152,7 @@ int tbls_aggregate_sigs_many(const uint8_t* s, const uint32_t* off, size_t g, ui
 jint J(batchVerify)(JNIEnv*, jclass, jbyteArray, jintArray, jbyteArray, jintArray, jbyteArray, jlongArray, jint, jintArray);
 jint J(batchVerifyIdx)(JNIEnv*, jclass, jintArray, jintArray, jbyteArray, jintArray, jbyteArray, jlongArray, jint, jintArray);
 jint J(verifyEach)(JNIEnv*, jclass, jbyteArray, jintArray, jbyteArray, jintArray, jbyteArray, jint, jintArray);
+jint J(batchVerifyEach)(JNIEnv*, jclass, jbyteArray, jintArray, jbyteArray, jintArray, jbyteArray, jlongArray, jint, jintArray, jintArray);
 jint J(aggregateVerify)(JNIEnv*, jclass, jbyteArray, jbyteArray, jintArray, jbyteArray, jintArray);
 jint J(sign)(JNIEnv*, jclass, jbyteArray, jbyteArray, jbyteArray, jbyteArray);
 jint J(skToPk)(JNIEnv*, jclass, jbyteArray, jbyteArray);
@@ -240,6 +249,22 @@ int main(void) {
     calls = 0;
     CHECK(J(verifyEach)(&ENV, NULL, b.pks, b.npk, b.msgs, b.moff, b.sigs, 0, b.ok) == TBLS_BAD_ARGUMENT && calls == 0, "verifyEach out");
     b.ok->len = 3;
+    jobject ok1 = arr(1, 4);
+    calls = 0;
+    CHECK(J(batchVerifyEach)(&ENV, NULL, b.pks, b.npk, b.msgs, b.moff, b.sigs, b.rand, 0, ok1, b.ok) == TBLS_SUCCESS && calls == 1 &&
+              ((jint*)ok1->data)[0] == 0 && ((jint*)b.ok->data)[0] == 1 && ((jint*)b.ok->data)[1] == 0 && ((jint*)b.ok->data)[2] == 1,
+          "batchVerifyEach verdicts copied out");
+    b.ok->len = 2;
+    calls = 0;
+    CHECK(J(batchVerifyEach)(&ENV, NULL, b.pks, b.npk, b.msgs, b.moff, b.sigs, b.rand, 0, ok1, b.ok) == TBLS_BAD_ARGUMENT && calls == 0,
+          "batchVerifyEach per-set array short");
+    b.ok->len = 3;
+    b.rand->len = 2;
+    calls = 0;
+    CHECK(J(batchVerifyEach)(&ENV, NULL, b.pks, b.npk, b.msgs, b.moff, b.sigs, b.rand, 0, ok1, b.ok) == TBLS_BAD_ARGUMENT && calls == 0,
+          "batchVerifyEach rand short");
+    b.rand->len = 3;
+    arr_free(ok1);
     calls = 0;
     CHECK(J(batchVerifyIdx)(&ENV, NULL, b.idx, b.npk, b.msgs, b.moff, b.sigs, b.rand, 0, b.ok) == TBLS_SUCCESS && calls == 1, "idx valid");
     b.idx->len = 2;

@@ -5,13 +5,13 @@
 // messages and returns their affine H(m_i) (Montgomery limbs) and skip flags,
 // for tests/test_gpu_hash_variants.py to compare with the oracle.
 //   variant 0  k_set_hash          (one lane per set; batches above 32,768 sets)
-//   variant 2  k_hrow_* (5 launches: field, sswu, iso, cof, fix; 513 - 4,096);
+//   variant 2  k_hrow_* (5 launches: field, sswu, iso, cof, fix; 513 - 1,024);
 //              force_fix != 0 sends every set through the one-lane k_hrow_fix
 //   variant 3  k_set_hash_coop     (256-thread workgroup per set; <= 512)
 //   variant 4  k_set_hash_wave     (64-lane cofactor program; the coop fall-back)
 //   variant 5  k_set_hash_w2 + k_set_hash_fix (two waves per SIMD; above 32,768,
 //              the default); force_fix != 0 flags every set for k_set_hash_fix
-//   variant 6  k_set_hash_quad + k_set_hash_fix (one DPP quad per set; 4,097 -
+//   variant 6  k_set_hash_quad + k_set_hash_fix (one DPP quad per set; 1,025 -
 //              8,192); force_fix as variant 5
 //   variant 7  k_set_hash_duo + k_set_hash_fix (one lane pair per set; 8,193 -
 //              32,768); force_fix as variant 5

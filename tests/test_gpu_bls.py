@@ -372,18 +372,19 @@ def test_spi_prepare_complete_combinatorics(hip):
         eager.prepare_batch_verify(0, [pks[0]], msgs[0], bls.HipSignature(NOT_IN_G2))
 
 
-def test_large_batch_msm_path(hip):
+@pytest.mark.parametrize("n", [20480, 24576, 32768])
+def test_large_batch_msm_path(hip, n):
     """Batches of >= 20,480 sets take the bucket-MSM path for sum r_i sig_i
     (k_sig_check + k_msm_*) instead of per-set [r_i] sig_i, and from 32,768
     sets the two-wave per-set kernels (k_set_pk_w2: [r] pk with the window
-    table in LDS): valid -> True; a signature on the wrong message, an
+    table in LDS); 20,480 and 24,576 are the bucket-sum sizes below the
+    two-wave kernels: valid -> True; a signature on the wrong message, an
     infinity signature, a non-G2 point, another signer's key and the
     infinity key -> False; a duplicated signature pair (bucket doubling
     case) -> True.
     Keys / signatures come from the GPU generators (interop keys), which
     test_hash_sign_keys_bit_exact pins to the oracle."""
     bls, native, L, impl = hip
-    n = 32768
     nk = 512
     sks = b"".join(interop_sk(i % nk).to_bytes(32, "big") for i in range(n))
     pk_out = ctypes.create_string_buffer(48 * nk)
@@ -411,7 +412,7 @@ def test_large_batch_msm_path(hip):
     bad[3] = pks[4]
     assert not _raw(bls, bad, msgs, sigs, rands)
     bad = list(pks)
-    bad[30000] = bytes([0xC0]) + bytes(47)
+    bad[n * 11 // 12] = bytes([0xC0]) + bytes(47)
     assert not _raw(bls, bad, msgs, sigs, rands)
     # the same (pk, msg, sig) twice with the same randomizer: equal points in one bucket
     dup_p, dup_m, dup_s, dup_r = list(pks), list(msgs), list(sigs), list(rands)

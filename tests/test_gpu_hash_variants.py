@@ -1,11 +1,12 @@
 """Byte-level parity of the batch hash_to_G2 kernels.
 
 batchVerify hashes with one of five kernels by batch size (tb_lib.hip
-launch_partial, hash_plan): k_set_hash_w2 + k_set_hash_fix (> 32,768 sets;
+launch_partial, hash_plan(): TB_HASH_ROW_MAX / TB_HASH_QUAD_MAX /
+TB_HASH_DUO_MAX): k_set_hash_w2 + k_set_hash_fix (> 32,768 sets;
 k_set_hash is its one-wave A/B twin), k_set_hash_duo + k_set_hash_fix
 (8,193 - 32,768),
-k_set_hash_quad + k_set_hash_fix (4,097 - 8,192), the row pipeline k_hrow_*
-(513 - 4,096) and k_set_hash_coop (<= 512; k_set_hash_wave is its
+k_set_hash_quad + k_set_hash_fix (1,025 - 8,192), the row pipeline k_hrow_*
+(513 - 1,024) and k_set_hash_coop (<= 512; k_set_hash_wave is its
 fall-back).  Each one runs here on the same 640
 messages -- empty, 200-byte, random lengths up to 256 bytes -- under the
 Ethereum POP DST and the NUL DST (BLSTest.java:375-391), through the test

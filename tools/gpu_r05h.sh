@@ -1,0 +1,23 @@
+#!/bin/bash
+# Round 5: inline psi(Q) == -t comparison in the signature check; per-kernel
+# exclusive times of every stage at 131k (stage profile under rocprofv3);
+# FETCH/WRITE of the same probe.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+TAG=${TAG:-r05h}
+echo "== pytest -m gpu"
+timeout -k 10 900 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread > gpurun_out/pytest_$TAG.log 2>&1
+rc=$?; tail -3 gpurun_out/pytest_$TAG.log; [ $rc -eq 0 ] || exit $rc
+P="tools/probe.py stages 131072 3"
+echo "== stages trace" && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG}_stages -o run --output-format csv -- python3 $P > gpurun_out/prof_${TAG}_stages.log 2>&1 || exit $?
+tail -1 gpurun_out/prof_${TAG}_stages.log
+echo "== pmc" && timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_${TAG}_fetch -o run --output-format csv -- python3 $P > gpurun_out/pmc_${TAG}_fetch.log 2>&1 || exit $?
+timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_${TAG}_write -o run --output-format csv -- python3 $P > gpurun_out/pmc_${TAG}_write.log 2>&1 || exit $?
+ARGS="--steps 10 --warmup 2 --lat-reps 0 --no-cpu-baseline --no-1m --no-kzg --no-extra"
+timeout -k 10 300 python bench.py $ARGS > gpurun_out/bench_${TAG}.json 2> gpurun_out/bench_${TAG}.err || exit $?
+python3 -c "
+import json; d = json.load(open('gpurun_out/bench_${TAG}.json'))
+print(round(d['value']), round(d['ms_per_step'], 2), {k: round(v, 2) for k, v in d['stage_ms_exclusive'].items()})"
+echo done

@@ -3,6 +3,9 @@ are read once per process):
 
     python tools/probe.py partial N [reps]      tbls_dev_batch_partial of N single-signer sets
     python tools/probe.py multikey S K [reps]   tbls_dev_batch_partial of S sets x K keys
+    python tools/probe.py stages N [reps]       one warm partial, then only the stage profile (every
+                                                stage alone on the stream: per-kernel exclusive times
+                                                under rocprofv3 --kernel-trace --stats)
 """
 
 import ctypes
@@ -25,7 +28,8 @@ def main():
     device = torch.device("cuda", 0)
     L = native.lib()
     stream = torch.cuda.current_stream(device).cuda_stream
-    if what == "partial":
+    stages_only = what == "stages"
+    if what in ("partial", "stages"):
         n = int(sys.argv[2])
         reps = int(sys.argv[3]) if len(sys.argv) > 3 else 5
         pks, msgs, sigs = synth.single_signer(0, n)
@@ -43,7 +47,8 @@ def main():
     for rep in range(reps + 1):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        native.check(L.tbls_dev_batch_partial(0, ctypes.byref(db.desc), stream, part.data_ptr()), "partial")
+        if not (stages_only and rep):
+            native.check(L.tbls_dev_batch_partial(0, ctypes.byref(db.desc), stream, part.data_ptr()), "partial")
         torch.cuda.synchronize()
         if rep:
             ts.append((time.perf_counter() - t0) * 1e3)
