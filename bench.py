@@ -65,9 +65,9 @@ STAGE_KERNEL = {
     "set_pk": "k_set_pk_w2",
     "set_sig": "k_sig_check_w2",
     "set_hash": "k_set_hash_w2 + k_set_hash_fix",
-    "g2_sum": "k_msm_bucket + k_msm_bucket_sum + k_msm_bitsum_pairs",
-    "miller": "k_miller_lines_w2 + k_miller_acc2",
-    "fp12_prod": "k_fp12_prod_wave",
+    "g2_sum": "k_msm_bucket_tree + k_msm_bitsum_pairs + 64 x k_miller_wave",
+    "miller": "k_miller_lines_w2 + k_miller_accs",
+    "fp12_prod": "k_fp12_prod_wave_seg + k_fp12_seg_combine_coop",
 }
 STAGE_UNITS = {"pk_decompress": "keys", "set_pk": "sets", "set_sig": "sets", "set_hash": "sets", "g2_sum": "sets", "miller": "pairs", "fp12_prod": "pairs"}
 _MC = os.path.join(ROOT, "tools", "mul_counts.json")

@@ -111,8 +111,8 @@ extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_MIN_WAVES)
 //   k_msm_hist     per set: bucket counts (window w, digit d = byte w of r);
 //   k_msm_scan     exclusive scan -> bucket offsets          (randomizers only:
 //   k_msm_scatter  per set: set index into its 8 bucket lists  run beside k_sig_check)
-//   k_msm_bucket   per (bucket, chunk): sum of the chunk's affine signatures
-//   k_msm_bucket_sum    per bucket: 64-lane LDS tree over its chunk sums
+//   k_msm_bucket_tree   per bucket: chunk sums of its list on 32 lanes, then a
+//                  lane-shuffle tree
 //   k_msm_bitsum_pairs  per (window, bit): 128-bucket sum, affine, the pair
 //                  (-C[w][2^k], V[w][k])
 // Any invalid signature fails the whole batch (n_bad), so only valid, finite
@@ -120,7 +120,6 @@ extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_MIN_WAVES)
 // ---------------------------------------------------------------------------
 #define TB_MSM_W 8          // windows
 #define TB_MSM_NB 256       // buckets per window (digit 0 unused)
-#define TB_MSM_CHUNKS 64    // chunks per bucket list (131072 threads at 2048 buckets)
 
 // thread (w, d): comb[w * 256 + d] = (d 2^(8w)) g1, affine (d = 0: unused)
 extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_MIN_WAVES) k_g1_comb_init(g1a* __restrict__ comb) {
@@ -199,63 +198,34 @@ extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_MIN_WAVES)
   }
 }
 
-// thread (bucket b, chunk c): sum of the affine signatures of chunk c of list b
-extern "C" __global__ void __launch_bounds__(TB_BLOCK, TB_MIN_WAVES)
-    k_msm_bucket(const g2a* __restrict__ sig_aff, const uint8_t* __restrict__ use, const uint32_t* __restrict__ off,
-                 const uint32_t* __restrict__ idx, g2j* __restrict__ part) {
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= TB_MSM_W * TB_MSM_NB * TB_MSM_CHUNKS) return;
-  const uint32_t b = t / TB_MSM_CHUNKS, c = t % TB_MSM_CHUNKS;
-  const uint32_t lo = off[b], hi = off[b + 1];
-  const uint32_t len = hi - lo, chunk = (len + TB_MSM_CHUNKS - 1) / TB_MSM_CHUNKS;
-  uint32_t s = lo + c * chunk, e = s + chunk;
-  if (e > hi) e = hi;
-  g2j acc = jac_inf<fp2>();
-  for (uint32_t k = s; k < e; k++) {
-    const uint32_t i = idx[k];
-    if (use[i]) acc = jac_add_aff(acc, sig_aff[i]);  // invalid sets fail the batch anyway; infinity adds nothing
-  }
-  part[t] = acc;
-}
-
-// block (w, d != 0): B[w][d] = sum of the bucket's 64 chunk sums (LDS tree)
-extern "C" __global__ void __launch_bounds__(64) k_msm_bucket_sum(const g2j* __restrict__ part, g2j* __restrict__ bucket) {
-  __shared__ g2j sh[64];
-  const uint32_t t = threadIdx.x;
-  const uint32_t w = blockIdx.x / (TB_MSM_NB - 1), d = blockIdx.x % (TB_MSM_NB - 1) + 1, b = w * TB_MSM_NB + d;
-  sh[t] = part[b * TB_MSM_CHUNKS + t];
-  __syncthreads();
-  for (uint32_t s = 32; s > 0; s >>= 1) {
-    if (t < s) sh[t] = jac_add(sh[t], sh[t + s]);
-    __syncthreads();
-  }
-  if (t == 0) bucket[b] = sh[0];
-}
-
-// Round 5: k_msm_bucket + k_msm_bucket_sum fused, without LDS.  Block
-// (w, d != 0), 64 lanes: lane c sums chunk c of bucket b's list (the chunks
-// of k_msm_bucket), then a 6-level tree across the lanes with the points moved
-// by lane shuffles (72 words per level) instead of an LDS array -- no 37.7 MB
-// partial-sum buffer written and read back, one launch fewer, and no 18 KB of
-// LDS per workgroup held beside the Miller accumulator (whose one-round grid
-// needs every CU's LDS when it keeps f there, tb_lib.hip acc_lds).  Same
-// bucket sums as the two kernels (the group law is associative and
-// commutative; the sums are made affine in k_msm_bitsum_pairs).
-__device__ TB_INLINE g2j shfl_down_g2j(const g2j& p, int s) {
+// Bucket sums B[w][d] (d != 0), one launch, no LDS.  A bucket's list is split
+// into TB_MSM_LANES chunks; lane c sums chunk c with mixed additions, then a
+// tree across the bucket's lanes with the points moved by lane shuffles (72
+// words per level).  Two buckets per 64-lane workgroup: the 1,020 waves of
+// the 2,040 buckets fill every SIMD once at one wave per SIMD (64 lanes per
+// bucket, round 5's first form: 2,040 waves, two rounds -- 2.0 ms at 131,072
+// sets; 32 lanes: 16 mixed additions and 5 tree levels per lane instead of 8
+// and 6, one round).  Round 4 wrote the 64 chunk sums to a 37.7 MB buffer and
+// summed them in a second kernel with an LDS tree.  The sums are made affine
+// in k_msm_bitsum_pairs.
+#define TB_MSM_LANES 32u
+static_assert(64 % TB_MSM_LANES == 0 && (TB_MSM_W * (TB_MSM_NB - 1)) % (64 / TB_MSM_LANES) == 0, "whole buckets per workgroup");
+__device__ TB_INLINE g2j shfl_down_g2j(const g2j& p, int s, int width) {
   g2j r;
   const uint32_t* a = reinterpret_cast<const uint32_t*>(&p);
   uint32_t* o = reinterpret_cast<uint32_t*>(&r);
-  TB_UNROLL for (int k = 0; k < (int)(sizeof(g2j) / 4); k++) o[k] = __shfl_down(a[k], s, 64);
+  TB_UNROLL for (int k = 0; k < (int)(sizeof(g2j) / 4); k++) o[k] = __shfl_down(a[k], s, width);
   return r;
 }
 
 extern "C" __global__ void __launch_bounds__(64)
     k_msm_bucket_tree(const g2a* __restrict__ sig_aff, const uint8_t* __restrict__ use, const uint32_t* __restrict__ off,
                       const uint32_t* __restrict__ idx, g2j* __restrict__ bucket) {
-  const uint32_t c = threadIdx.x;
-  const uint32_t w = blockIdx.x / (TB_MSM_NB - 1), d = blockIdx.x % (TB_MSM_NB - 1) + 1, b = w * TB_MSM_NB + d;
+  const uint32_t c = threadIdx.x % TB_MSM_LANES;
+  const uint32_t q = blockIdx.x * (64 / TB_MSM_LANES) + threadIdx.x / TB_MSM_LANES;  // bucket rank among the 2,040
+  const uint32_t w = q / (TB_MSM_NB - 1), d = q % (TB_MSM_NB - 1) + 1, b = w * TB_MSM_NB + d;
   const uint32_t lo = off[b], hi = off[b + 1];
-  const uint32_t len = hi - lo, chunk = (len + TB_MSM_CHUNKS - 1) / TB_MSM_CHUNKS;
+  const uint32_t len = hi - lo, chunk = (len + TB_MSM_LANES - 1) / TB_MSM_LANES;
   uint32_t s = lo + c * chunk, e = s + chunk;
   if (e > hi) e = hi;
   g2j acc = jac_inf<fp2>();
@@ -263,8 +233,8 @@ extern "C" __global__ void __launch_bounds__(64)
     const uint32_t i = idx[k];
     if (use[i]) acc = jac_add_aff(acc, sig_aff[i]);  // invalid sets fail the batch anyway; infinity adds nothing
   }
-  for (int sh = 32; sh > 0; sh >>= 1) {
-    const g2j other = shfl_down_g2j(acc, sh);
+  for (int sh = TB_MSM_LANES / 2; sh > 0; sh >>= 1) {
+    const g2j other = shfl_down_g2j(acc, sh, TB_MSM_LANES);
     if (c < (uint32_t)sh) acc = jac_add(acc, other);
   }
   if (c == 0) bucket[b] = acc;
@@ -286,7 +256,7 @@ extern "C" __global__ void __launch_bounds__(64)
     acc = jac_add(acc, bucket[w * TB_MSM_NB + d]);
   }
   for (int sh = 32; sh > 0; sh >>= 1) {
-    const g2j other = shfl_down_g2j(acc, sh);
+    const g2j other = shfl_down_g2j(acc, sh, 64);
     if (t < (uint32_t)sh) acc = jac_add(acc, other);
   }
   if (t == 0) {

@@ -66,12 +66,10 @@ extern "C" __global__ void k_aggregate_pks(const g1a* __restrict__ pk_aff, const
 extern "C" __global__ void k_sk_to_pk(const uint64_t* __restrict__ sks, uint32_t n, uint8_t* __restrict__ out);
 extern "C" __global__ void k_g1_comb_init(g1a* __restrict__ comb);
 extern "C" __global__ void k_sig_check(const uint8_t* __restrict__ sigs, uint32_t n, g2a* __restrict__ sig_aff, uint8_t* __restrict__ sig_use, uint8_t* __restrict__ sig_code, uint32_t* __restrict__ n_bad, uint32_t skip_mode);
-extern "C" __global__ void k_msm_bucket_sum(const g2j* __restrict__ part, g2j* __restrict__ bucket);
 extern "C" __global__ void k_msm_bitsum_pairs(const g2j* __restrict__ bucket, const g1a* __restrict__ comb, g1a* __restrict__ P, g2a* __restrict__ Q, uint8_t* __restrict__ skip);
 extern "C" __global__ void k_msm_hist(const uint64_t* __restrict__ rand, uint32_t n, uint32_t* __restrict__ cnt);
 extern "C" __global__ void k_msm_scan(const uint32_t* __restrict__ cnt, uint32_t* __restrict__ off, uint32_t* __restrict__ cur);
 extern "C" __global__ void k_msm_scatter(const uint64_t* __restrict__ rand, uint32_t n, uint32_t* __restrict__ cur, uint32_t* __restrict__ idx);
-extern "C" __global__ void k_msm_bucket(const g2a* __restrict__ sig_aff, const uint8_t* __restrict__ use, const uint32_t* __restrict__ off, const uint32_t* __restrict__ idx, g2j* __restrict__ part);
 extern "C" __global__ void k_aggregate_sigs(const uint8_t* __restrict__ sigs, uint32_t K, uint8_t* __restrict__ out, int* __restrict__ status);
 extern "C" __global__ void k_sig_validate(const uint8_t* __restrict__ sigs, uint32_t n, uint32_t* __restrict__ out);
 extern "C" __global__ void k_set_hash(const uint8_t* __restrict__ msgs, const uint32_t* __restrict__ msg_off, const uint8_t* __restrict__ dst, uint32_t dlen, uint32_t n, g2a* __restrict__ Q, uint8_t* __restrict__ skip);

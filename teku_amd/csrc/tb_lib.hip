@@ -237,9 +237,9 @@ static uint32_t msm_min() {
 }
 #define TB_HASH_WAVE_MAX 512u  // k_set_hash_wave (one workgroup per set) up to this many sets: at 1024 its waves fill every SIMD and the key / signature stages can no longer run beside it (measured 9.8 vs 8.8 ms partial)
 #define TB_MSM_BUCKETS 2048u  // 8 windows x 256 digits (digit 0 unused)
-#define TB_MSM_NSUM 2040u     // 8 x 255 bucket sums (k_msm_bucket_sum)
+#define TB_MSM_NSUM 2040u     // 8 x 255 bucket sums
+#define TB_MSM_TREE_WG (TB_MSM_NSUM / 2u)  // k_msm_bucket_tree workgroups: two buckets of 32 lanes each (k_sigs.hip)
 #define TB_MSM_XPAIRS 64u     // 8 windows x 8 digit bits: the signature side's pairs
-#define TB_MSM_PARTS (TB_MSM_BUCKETS * 64u)  // buckets x 64 chunks (k_msm_bucket)
 // Split Miller loop (k_miller_lines + k_miller_acc*, k_lines.hip): pairs per
 // line-buffer chunk (19,584 B of lines per pair: 5.1 GB per chunk), and the
 // pair count from which two pairs share an accumulator (the GPU is full at one
@@ -393,7 +393,7 @@ static int line_group(uint32_t n_main) {
 
 struct ws_layout {
   size_t pk_aff, pk_code, P, Q, skip, set_code, sig_code, f, fpart, fpart2, segv, n_bad, result;
-  size_t sig_aff, sig_use, msm_cnt, msm_off, msm_cur, msm_idx, msm_part, msm_sum, mlist, mcnt, lines, hrow, total;
+  size_t sig_aff, sig_use, msm_cnt, msm_off, msm_cur, msm_idx, msm_sum, mlist, mcnt, lines, hrow, total;
   uint32_t nb_f;
   ws_layout() : total(0) {}
   ws_layout(const pair_plan& pp, uint32_t K) {
@@ -416,7 +416,6 @@ struct ws_layout {
     msm_off = o;  o = align_up(o + (msm ? (TB_MSM_BUCKETS + 1) * 4 : 0));
     msm_cur = o;  o = align_up(o + (msm ? TB_MSM_BUCKETS * 4 : 0));
     msm_idx = o;  o = align_up(o + nm * 8 * 4);
-    msm_part = o;  // (round 4's chunk sums: k_msm_bucket_tree keeps them in registers)
     msm_sum = o;  o = align_up(o + (msm ? (size_t)TB_MSM_BUCKETS * sizeof(g2j) : 0));
     mlist = o;    o = align_up(o + (size_t)n * 4);
     mcnt = o;     o = align_up(o + 4);
@@ -618,7 +617,7 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
   if (late_join) HIPCHK(hipEventRecord(c.e_sig, sb));
   TB_EV(8, sb);
   if (pp.msm) {
-    hipLaunchKernelGGL(k_msm_bucket_tree, dim3(TB_MSM_NSUM), dim3(64), 0, sb, (const g2a*)(w + L.sig_aff), (const uint8_t*)(w + L.sig_use),
+    hipLaunchKernelGGL(k_msm_bucket_tree, dim3(TB_MSM_TREE_WG), dim3(64), 0, sb, (const g2a*)(w + L.sig_aff), (const uint8_t*)(w + L.sig_use),
                        (const uint32_t*)msm_off, (const uint32_t*)msm_idx, (g2j*)(w + L.msm_sum));
     hipLaunchKernelGGL(k_msm_bitsum_pairs, dim3(TB_MSM_XPAIRS), dim3(64), 0, sb, (const g2j*)(w + L.msm_sum), c.comb.as<const g1a>(),
                        P + n, Q + n, skip + n);

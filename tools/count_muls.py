@@ -62,8 +62,8 @@ def main():
     res["set_hash"] = per_unit("STAGE_SET_HASH", [enc_h2c(m) for m in msgs], name="set_hash")
     q = [O.g2_decompress(s)[1] for s in sigs]
     # Large batches: the signature side as bucket sums by randomizer byte
-    # (k_msm_bucket: one mixed addition per nonzero byte, 8 windows), a
-    # 64-lane tree per bucket (k_msm_bucket_sum: 63 additions), then 64 bit
+    # (k_msm_bucket_tree: one mixed addition per nonzero byte, 8 windows, and
+    # a 32-lane tree per bucket: 31 additions), then 64 bit
     # sums of 128 buckets each (k_msm_bitsum_pairs: 2 + 63 additions, affine)
     # whose 64 extra Miller pairs are spread over the accumulators
     # (k_sigs.hip, k_lines.hip), per set at n = MSM_N.  Point-operation costs in
@@ -71,7 +71,7 @@ def main():
     # 2): madd-2007-bl 7M+4S = 29, add-2007-bl 11M+5S = 43; the Fp2 affine
     # conversion (binary-GCD inversion ~65 + norm/products) ~81.
     MADD, ADD, AFF2, MSM_N, NSUM, XP = 29, 43, 81, 131072, 2040, 64
-    adds = NSUM * 63 + XP * 65
+    adds = NSUM * 31 + XP * 65
     res["g2_sum"] = 8 * 255 / 256 * MADD + (adds * ADD + XP * AFF2) / MSM_N
     sq["g2_sum"] = 8 * 255 / 256 * 4 * 2 + adds * 5 * 2 / MSM_N
     f2["g2_sum"] = 8 * 255 / 256 * 7 + adds * 11 / MSM_N
