@@ -12,12 +12,13 @@
 // 256-register bound too, and a second wave per SIMD hides the latency the
 // one-wave kernels stall on (MAD issue: 5.4 cycles per wave64 instruction at
 // one wave per SIMD, 4.5 at two, tools/microbench/mad_peak.hip).  The cofactor
-// clearing is the branch-free g2_clear_cofactor_nx_stash (one point parked in
-// LDS across the second [|x|] chain); a set whose chain meets an
+// clearing is the branch-free g2_clear_cofactor_lean (affine addends parked in
+// LDS, register-lean formulas of tb_lean.h); a set whose chain meets an
 // exceptional case (Z = 0) is flagged skip = 2 and recomputed with the exact
 // formulas by k_set_hash_fix (k_hash.hip) on the same stream, so the results
 // are k_set_hash's.
 #include "tb_kdecl.h"
+#include "tb_lean.h"
 
 using namespace tb;
 
@@ -31,34 +32,45 @@ using namespace tb;
 #endif
 
 namespace {
-// g2_clear_cofactor_nx in an order that keeps at most two points besides the
-// loop state live in registers, the caller's LDS slot *stash holding a third:
-//   stash = psi(P); t1 = [|x|]P; u = stash - t1 (= psi(P) - t1); stash = u;
-//   w = psi^2(2P) - P - stash (= t1 + A, A = psi^2(2P) - P - psi(P));
-//   u = stash; stash = w; t3 = [|x|]u; out = stash - t3.
-// The same point (the group law is associative and commutative); an
-// exceptional case anywhere ends at Z = 0 as in g2_clear_cofactor_nx.  The
-// empty asm statements with a memory clobber keep the compiler from
-// forwarding a parked point back into registers.  (Round 4: with t1, psi(P),
-// u and A live together the straight-line part spilled ~6,500 scratch
-// accesses per set, profiles/pmc_traffic.json.)
+// Cofactor clearing h(P) = e - [|x| + 1]u with e = psi^2(2P) - P and
+// u = psi(P) - [|x|]P (Budroni-Pintore in the order of g2_clear_cofactor_nx:
+// the same point, by associativity and commutativity), on the register-lean
+// chains of tb_lean.h, every chain addend affine:
+//   P -> affine (one inversion), parked in the lane's LDS slot;
+//   t1 = [|x|]P (mixed additions with the parked P);
+//   u = psi(P) - t1 (psi of an affine point is affine: one mixed addition),
+//   e = psi^2(2P) - P (a doubling and a mixed addition);
+//   u and e -> affine (an inversion each: batching the two with Montgomery's
+//   trick keeps both Jacobian points live and measured 3,466 static scratch
+//   accesses against 2,5xx); u parked, e kept in the output slot Q[i] (this
+//   lane's own 192 B) across
+//   t3 = [|x| + 1]u (the +1 is a sixth mixed addition);
+//   out = e - t3 (a mixed addition), affine.
+// Round 4 / early round 5 took P and u Jacobian: every scalar-chain addition
+// was a general one with two Jacobian points live, and those outside the
+// doubling loops -- straight-line code -- were most of the kernel's 4,867
+// static scratch accesses (6,288 B per lane, ~10 GB per 131k launch).  Any
+// exceptional case ends at Z = 0 (sticky, tb_lean.h) and returns false:
+// k_set_hash_fix recomputes the set with the exact formulas.
 #define TB_PARK() asm volatile("" ::: "memory")
-__device__ TB_INLINE bool g2_clear_cofactor_nx_stash(g2j& out, const g2j& p, g2j* stash) {
-  *stash = g2_psi(p);
+__device__ TB_INLINE bool g2_clear_cofactor_lean(g2a& out, const g2j& p, g2a* park, g2a* keep) {
+  g2a pa;
+  if (!lean::to_aff(pa, p)) return false;
+  const g2j t1 = lean::mul_xabs_aff(pa, park);
+  pa = *park;
+  g2a ua, ea;
+  if (!lean::to_aff(ua, lean::madd(jac_neg(t1), lean::psi_aff(pa)))) return false;
+  *keep = ua;
   TB_PARK();
-  g2j u = jac_mul_xabs_nx(p);
-  u = jac_add_nx(*stash, jac_neg(u));
-  *stash = u;
+  pa = *park;
+  if (!lean::to_aff(ea, lean::madd(g2_psi2(jac_dbl_i(jac_from_aff(pa))), lean::neg_aff(pa)))) return false;
+  ua = *keep;
+  *keep = ea;
   TB_PARK();
-  g2j w = jac_add_nx(g2_psi2(jac_dbl_i(p)), jac_neg(p));
-  w = jac_add_nx(w, jac_neg(*stash));
-  u = *stash;
+  const g2j t3 = lean::mul_xabs_aff<true>(ua, park);
   TB_PARK();
-  *stash = w;
-  TB_PARK();
-  const g2j t3 = jac_mul_xabs_nx(u);
-  out = jac_add_nx(jac_neg(t3), *stash);
-  return !fp2_is_zero(out.z);
+  ea = *keep;
+  return lean::to_aff(out, lean::madd(jac_neg(t3), ea));
 }
 #undef TB_PARK
 
@@ -67,7 +79,7 @@ __device__ TB_INLINE bool g2_clear_cofactor_nx_stash(g2j& out, const g2j& p, g2j
 extern "C" __global__ void __launch_bounds__(TB_BLOCK, 2)
     k_set_hash_w2(const uint8_t* __restrict__ msgs, const uint32_t* __restrict__ msg_off, const uint8_t* __restrict__ dst,
                   uint32_t dlen, uint32_t n, g2a* __restrict__ Q, uint8_t* __restrict__ skip) {
-  __shared__ g2j stash[TB_BLOCK];  // 288 B per lane: 147 KB per CU at two waves per SIMD
+  __shared__ g2a park[TB_BLOCK];  // 192 B per lane: 98 KB per CU at two waves per SIMD
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   xmd_ctx c;
@@ -87,13 +99,11 @@ extern "C" __global__ void __launch_bounds__(TB_BLOCK, 2)
   map_to_curve_sswu2(q0, q1, u0, u1);
 #endif
   const g2j p = iso_map_jac(e2p_add_aff_aff(q0, q1));
-  g2j h;
-  if (!g2_clear_cofactor_nx_stash(h, p, &stash[threadIdx.x])) {
-    skip[i] = 2;  // k_set_hash_fix: the exact formulas
+  g2a a;
+  if (!g2_clear_cofactor_lean(a, p, &park[threadIdx.x], &Q[i])) {
+    skip[i] = 2;  // k_set_hash_fix: the exact formulas (it rewrites Q[i])
     return;
   }
-  g2a a;
-  (void)jac_to_aff(a, h);  // Z != 0 here
   Q[i] = a;
   skip[i] = 0;
 }

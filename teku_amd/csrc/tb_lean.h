@@ -1,11 +1,13 @@
-// G2 point formulas ordered for the two-waves-per-SIMD kernels (256
-// registers per lane), where a Jacobian G2 point (72 registers) beside a
-// formula's temporaries and an Fp2 product's own (~150) already fills the
-// file: each step computes the value that lets the most inputs die first,
+// G2 scalar chains for the two-waves-per-SIMD kernels (256 registers per
+// lane), where a Jacobian G2 point (72 registers) beside a formula's
+// temporaries and an Fp2 product's own (~150) already fills the file: the
+// addend of every chain addition is an affine point parked in the lane's LDS
+// slot (a mixed addition, with only the running point register-live), and the
+// mixed addition computes the value that lets the most inputs die first,
 // with a scheduling fence after every product so the compiler does not hoist
 // the next product's operands above it.  Same results as tb_curve.h's
-// jac_dbl_i / jac_add_aff_i without branches (the sticky Z = 0 rule of
-// jac_add_nx).  Included by the k_w2_*.hip translation units only.
+// jac_add_aff_i without branches (the sticky Z = 0 rule of jac_add_nx).
+// Included by the k_w2_*.hip translation units only.
 #pragma once
 #include "tb_curve.h"
 
@@ -29,23 +31,6 @@ __device__ TB_INLINE fp2 S(const fp2& a) {
   return r;
 }
 
-// dbl-2009-l (a = 0) in the order Z3 = 2YZ (Y, Z dead after B), B = Y^2,
-// A = X^2, s = (X + B)^2 (X dead), C = B^2 (B dead), D = 2(s - A - C),
-// E = 3A, F = E^2, X3 = F - 2D, Y3 = E(D - X3) - 8C.  Z = 0 stays 0.
-__device__ TB_INLINE g2j dbl(const g2j& p) {
-  g2j r;
-  r.z = M(fp2_dbl(p.y), p.z);
-  const fp2 B = S(p.y);
-  const fp2 A = S(p.x);
-  const fp2 s = S(fp2_add_nr(p.x, B));
-  const fp2 C = S(B);
-  const fp2 D = fp2_dbl(fp2_sub(fp2_sub(s, A), C));
-  const fp2 E = fp2_add_nr(fp2_dbl(A), A);  // < 4p: a product operand only
-  r.x = fp2_sub(S(E), fp2_dbl(D));
-  r.y = fp2_sub(M(E, fp2_sub(D, r.x)), fp2_dbl(fp2_dbl(fp2_dbl(C))));
-  return r;
-}
-
 // madd-2007-bl, p Jacobian + q affine (finite), no branches: p = O (Z1 = 0)
 // or p = +-q (H = 0) give Z3 = (Z1 + H)^2 - Z1^2 - H^2 = 0, which doubling and
 // addition keep, as jac_add_nx.
@@ -64,19 +49,51 @@ __device__ TB_INLINE g2j madd(const g2j& p, const g2a& q) {
   return o;
 }
 
-// [|x|]Q for affine Q, branch-free, Q parked in the lane's LDS slot across
-// the doubling runs (XRUN_DBL of tb_curve.h: 1, 2, 3, 9, 32, 16 doublings,
-// an addition after each of the first five)
+// [|x|]Q (PLUS1: [|x| + 1]Q) for affine Q, branch-free, Q parked in the
+// lane's LDS slot across the doubling runs (XRUN_DBL of tb_curve.h: 1, 2, 3,
+// 9, 32, 16 doublings, an addition after each of the first five, and after
+// the last for PLUS1).  The doubling is tb_curve.h's jac_dbl_i (Z last): a
+// fenced Z-first order measured more scratch in the loop (41 / 56 accesses
+// per step in the signature / hash kernels against 16 / 18).
+template <bool PLUS1 = false>
 __device__ TB_INLINE g2j mul_xabs_aff(const g2a& Q, g2a* park) {
   *park = Q;
   asm volatile("" ::: "memory");
   g2j r = jac_from_aff(Q);
   TB_NOUNROLL for (int k = 0; k < 6; k++) {
     const int nd = k == 0 ? 1 : k == 1 ? 2 : k == 2 ? 3 : k == 3 ? 9 : k == 4 ? 32 : 16;
-    TB_NOUNROLL for (int i = 0; i < nd; i++) r = dbl(r);
-    if (k < 5) r = madd(r, *park);
+    TB_NOUNROLL for (int i = 0; i < nd; i++) r = jac_dbl_i(r);
+    if (PLUS1 || k < 5) r = madd(r, *park);
   }
   return r;
+}
+
+// affine form; false (o untouched) when Z = 0
+__device__ TB_INLINE bool to_aff(g2a& o, const g2j& p) {
+  if (fp2_is_zero(p.z)) return false;
+  const fp2 zi = fp2_inv(p.z);
+  const fp2 zi2 = S(zi);
+  o.x = M(p.x, zi2);
+  o.y = M(M(p.y, zi2), zi);
+  return true;
+}
+// both affine with one inversion (Montgomery's trick); false when either Z = 0
+__device__ TB_INLINE bool to_aff2(g2a& a, g2a& b, const g2j& p, const g2j& q) {
+  const fp2 z = M(p.z, q.z);
+  if (fp2_is_zero(z)) return false;
+  const fp2 zi = fp2_inv(z);
+  const fp2 zp = M(zi, q.z), zq = M(zi, p.z);
+  const fp2 zp2 = S(zp), zq2 = S(zq);
+  a.x = M(p.x, zp2);
+  a.y = M(M(p.y, zp2), zp);
+  b.x = M(q.x, zq2);
+  b.y = M(M(q.y, zq2), zq);
+  return true;
+}
+__device__ TB_INLINE g2a neg_aff(const g2a& q) { return {q.x, fp2_neg(q.y)}; }
+// psi of an affine point is affine: (conj(x) cx, conj(y) cy)
+__device__ TB_INLINE g2a psi_aff(const g2a& q) {
+  return {M(fp2_conj(q.x), fp2_from_const(PSI_CX)), M(fp2_conj(q.y), fp2_from_const(PSI_CY))};
 }
 
 // Scott's subgroup test on the chain's output: psi(Q) == -t for t = [|x|]Q
