@@ -527,6 +527,14 @@ static bool acc_lds(bool msm_beside = false) {
   const int e = acc_lds_env();
   return e < 0 ? !msm_beside : e == 1;
 }
+// TBLS_SIG_PRIO=1 (A/B): the signature stream -- signature checks, then the
+// bucket sums and the bit-sum pairs' wave Miller loops -- at the hash
+// stream's high priority, so that the bucket-sum chain runs during the hash
+// instead of beside the Miller accumulator (read at tbls_init)
+static bool sig_prio() {
+  static const bool v = getenv("TBLS_SIG_PRIO") && getenv("TBLS_SIG_PRIO")[0] == '1';
+  return v;
+}
 // TBLS_ACC_JOIN=1: the accumulator waits for the bucket-sum stream (its
 // k_miller_wave workgroups hold LDS the accumulator's one-round grid needs)
 static bool acc_join() {
@@ -1327,8 +1335,8 @@ extern "C" int tbls_init(int n_devices, uint32_t flags) {
     int prio_lo = 0, prio_hi = 0;
     if (hipSetDevice(d) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->aux[0], hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->aux[1], hipStreamNonBlocking) != hipSuccess ||
         hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess ||
+        hipStreamCreateWithPriority(&c->aux[1], hipStreamNonBlocking, sig_prio() ? prio_hi : prio_lo) != hipSuccess ||
         hipStreamCreateWithPriority(&c->aux[2], hipStreamNonBlocking, prio_hi) != hipSuccess ||
         hipEventCreateWithFlags(&c->e_join[2], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->e_fork, hipEventDisableTiming) != hipSuccess ||
