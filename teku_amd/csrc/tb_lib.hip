@@ -87,7 +87,7 @@ struct dev_ctx {
   dbuf in, ws;  // device input staging, pipeline workspace
   dbuf fin;     // the synchronous final verification's verdict word (under the device lock)
   dbuf dstb;    // default DST for the device-resident API
-  hipStream_t aux[3] = {nullptr, nullptr, nullptr};  // concurrent per-set stages (aux[2]: high priority, hash_to_G2)
+  hipStream_t aux[3] = {nullptr, nullptr, nullptr};  // concurrent per-set stages (aux[1] signatures + bucket sums, aux[2] hash_to_G2: high priority)
   dbuf tab_aff, tab_code;                    // device-resident public-key table (tbls_pk_table_load)
   uint32_t tab_n = 0;
   hipEvent_t e_fork = nullptr, e_join[3] = {nullptr, nullptr, nullptr}, e_sig = nullptr;
@@ -441,8 +441,10 @@ struct ws_layout {
 #define TB_NSTAGE 7
 #define TB_NSTAGE_EV (2 * TB_NSTAGE)
 // Streams: keys on aux[0], signatures (+ bucket sums) on aux[1], hash_to_G2
-// on aux[2] (high priority); all three join the caller's stream before the
-// Miller loops (the bucket-sum pairs only before the product tree).  `serial`
+// on aux[2]; aux[1] and aux[2] at high priority (sig_prio); all three join
+// the caller's stream before the Miller loops (the bucket-sum chain before
+// the accumulator, acc_join; without acc_join only before the product
+// tree).  `serial`
 // (the stage-profile API) runs everything on the caller's stream, for
 // exclusive per-stage timings.
 
@@ -500,24 +502,20 @@ void launch_set_pk(hipStream_t s, uint32_t n, uint32_t n_entries, const uint32_t
 // k_lines.hip: the segmented accumulator with f in LDS and two lines per
 // product (tb_lines.h miller_accs_lds_body).  Measured at 131,072 sets
 // (profiles/r05_bench_acc_lds_ab.json): Miller stage alone 13.3 -> 12.6 ms
-// and scratch writes 3.3 -> 1.5 GB per launch, but beside the bucket-sum
-// stream's kernels part of its one-round grid (4 x 36,864 B of LDS per CU)
-// ran a second round -- most likely workgroups of that stream holding LDS on
-// the CUs (the bit-sum pairs' wave Miller loops moved to a 16 KB form did not
-// change it): 131k step 38.2 -> 43.9 ms; waiting for that stream first
-// (TBLS_ACC_JOIN=1) gives 38.5.  So by default it runs where nothing runs
-// beside it -- batches without bucket sums (< 20,480 sets: config 4) and the
-// per-set settling of a failed batch -- and the register-resident
-// k_miller_accs where the bucket sums may still run.  TBLS_ACC_LDS=0 / 1
-// forces one kernel everywhere (A/B).
+// and scratch writes 3.3 -> 1.5 GB per launch.  Its grid is one round of
+// workgroups at full LDS (4 x 36,864 B per CU), so a workgroup of the
+// bucket-sum stream still resident on a CU pushes part of it into a second
+// round: beside that stream the 131k step went 38.2 -> 43.9 ms.  The bucket
+// sums now run on the high-priority signature stream (sig_prio) and the
+// accumulator waits for that stream (acc_join): with both, the LDS kernel
+// runs at every batch size -- 131k step 37.3 -> 36.1-36.6 ms
+// (profiles/r05_bench_prio_join.json).  TBLS_ACC_LDS=0 / 1 forces one kernel
+// everywhere (A/B; auto = LDS unless the bucket sums may run beside it).
 extern "C" __global__ void k_miller_accs_lds(const uint4* __restrict__ lines, const uint8_t* __restrict__ skip, const uint8_t* __restrict__ code_a,
                                              const uint8_t* __restrict__ code_b, uint32_t n, uint32_t per, uint32_t nseg, uint32_t g_pad,
                                              fp12* __restrict__ f_out, uint32_t seg_stride);
 extern "C" __global__ void k_msm_bucket_tree(const g2a* __restrict__ sig_aff, const uint8_t* __restrict__ use, const uint32_t* __restrict__ off,
                                              const uint32_t* __restrict__ idx, g2j* __restrict__ bucket);  // k_sigs.hip
-extern "C" __global__ void k_miller_wave_g(const g1a* __restrict__ P, const g2a* __restrict__ Q, const uint8_t* __restrict__ skip,
-                                           const uint8_t* __restrict__ code_a, const uint8_t* __restrict__ code_b, uint32_t n,
-                                           fp12* __restrict__ f);  // k_mwave.hip: level tables from global memory
 static int acc_lds_env() {  // -1 auto, 0 never, 1 always
   static const int v = getenv("TBLS_ACC_LDS") ? (getenv("TBLS_ACC_LDS")[0] == '0' ? 0 : 1) : -1;
   return v;
@@ -527,18 +525,19 @@ static bool acc_lds(bool msm_beside = false) {
   const int e = acc_lds_env();
   return e < 0 ? !msm_beside : e == 1;
 }
-// TBLS_SIG_PRIO=1 (A/B): the signature stream -- signature checks, then the
-// bucket sums and the bit-sum pairs' wave Miller loops -- at the hash
-// stream's high priority, so that the bucket-sum chain runs during the hash
-// instead of beside the Miller accumulator (read at tbls_init)
+// The signature stream -- signature checks, then the bucket sums and the
+// bit-sum pairs' wave Miller loops -- at the hash stream's high priority, so
+// that the bucket-sum chain runs during the hash instead of beside the Miller
+// accumulator (TBLS_SIG_PRIO=0: normal priority, A/B; read at tbls_init)
 static bool sig_prio() {
-  static const bool v = getenv("TBLS_SIG_PRIO") && getenv("TBLS_SIG_PRIO")[0] == '1';
+  static const bool v = !(getenv("TBLS_SIG_PRIO") && getenv("TBLS_SIG_PRIO")[0] == '0');
   return v;
 }
-// TBLS_ACC_JOIN=1: the accumulator waits for the bucket-sum stream (its
-// k_miller_wave workgroups hold LDS the accumulator's one-round grid needs)
+// The accumulator waits for the bucket-sum stream, so that nothing of that
+// stream holds LDS or registers its one-round grid needs (TBLS_ACC_JOIN=0:
+// it starts after the signature checks only, A/B)
 static bool acc_join() {
-  static const bool v = getenv("TBLS_ACC_JOIN") && getenv("TBLS_ACC_JOIN")[0] == '1';
+  static const bool v = !(getenv("TBLS_ACC_JOIN") && getenv("TBLS_ACC_JOIN")[0] == '0');
   return v;
 }
 extern "C" __global__ void k_set_hash_wave(const uint8_t* __restrict__ msgs, const uint32_t* __restrict__ msg_off,
@@ -630,7 +629,7 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
     hipLaunchKernelGGL(k_msm_bitsum_pairs, dim3(TB_MSM_XPAIRS), dim3(64), 0, sb, (const g2j*)(w + L.msm_sum), c.comb.as<const g1a>(),
                        P + n, Q + n, skip + n);
     if (pp.n_xwave)  // their Miller loops, one wave each, on this stream: f[n_f_main ..)
-      hipLaunchKernelGGL(acc_lds(!acc_join()) ? k_miller_wave_g : k_miller_wave, dim3(pp.n_xwave), dim3(64), 0, sb, (const g1a*)P + n,
+      hipLaunchKernelGGL(k_miller_wave, dim3(pp.n_xwave), dim3(64), 0, sb, (const g1a*)P + n,
                          (const g2a*)Q + n,
                          (const uint8_t*)skip + n,
                          (const uint8_t*)(w + L.set_code + n), (const uint8_t*)(w + L.sig_code + n), pp.n_xwave, (fp12*)(w + L.f) + pp.n_f_main());

@@ -16,7 +16,7 @@
 
 namespace tb {
 
-struct mprog_lds_g {  // tables read from global memory (k_miller_wave_g): 16,288 B of LDS
+struct mprog_lds_g {  // the slots (tables read from global memory by the caller's choice): 16,288 B of LDS
   fp S[2 * MP_NSLOT];    // values, then their negations 2p - v (wprog_level)
   u13 part[64];
 };
@@ -115,7 +115,8 @@ __device__ TB_INLINE void wprog_level(fp* S, u13* part, const uint16_t* tab, int
 // f_{|x|,Q}(P) (up to a factor in Fp), conjugated, into L.S[0..12) -- the
 // Fp12 coordinates in tb_fp12_wave.h order; whole workgroup of 64 lanes.
 // tab: the level tables, staged in LDS (mprog_lds) or read in place from
-// global memory (the constant table MP_TAB, cached: k_miller_wave_g).
+// global memory (the constant table MP_TAB, cached; round 5 measured that
+// form, 16 KB of LDS per workgroup, as the bit-sum pairs' kernel: no gain).
 template <class LDS>
 __device__ TB_INLINE void miller_loop_prog(LDS& L, const uint16_t* tab, const g1a& P, const g2a& Q) {
   const int l = threadIdx.x;
