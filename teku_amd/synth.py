@@ -132,6 +132,9 @@ def fast_multipliers(n: int) -> np.ndarray:
 
 
 # ---- contiguous C-ABI set arrays (no per-set Python buffers) -------------------
+def _addr(p: ctypes.c_char_p) -> int:
+    return ctypes.cast(p, ctypes.c_void_p).value
+
 _SET_DTYPE = np.dtype([("pks", "<u8"), ("n_pks", "<u4"), ("msg", "<u8"), ("msg_len", "<u4"), ("sig", "<u8")], align=True)
 assert _SET_DTYPE.itemsize == ctypes.sizeof(native.TblsSet)
 
@@ -142,19 +145,19 @@ class SetArray:
 
     def __init__(self, pks: bytes, n_pks: Sequence[int], msgs: bytes, msg_lens: Sequence[int], sigs: bytes):
         n = len(n_pks)
-        self._pks = ctypes.create_string_buffer(pks or b"\0", max(1, len(pks)))
-        self._msgs = ctypes.create_string_buffer(msgs or b"\0", max(1, len(msgs)))
-        self._sigs = ctypes.create_string_buffer(sigs or b"\0", max(1, len(sigs)))
+        # the blobs in place (the library only reads them): a c_char_p keeps its
+        # bytes object alive and points at its data, no copy
+        self._pks, self._msgs, self._sigs = (ctypes.c_char_p(bytes(x) if x else b"\0") for x in (pks, msgs, sigs))
         k = np.asarray(n_pks, dtype=np.uint64)
         ml = np.asarray(msg_lens, dtype=np.uint64)
         k_off = np.concatenate([[0], np.cumsum(k)[:-1]]).astype(np.uint64) if n else k
         m_off = np.concatenate([[0], np.cumsum(ml)[:-1]]).astype(np.uint64) if n else ml
         a = np.zeros(n, dtype=_SET_DTYPE)
-        a["pks"] = ctypes.addressof(self._pks) + 48 * k_off
+        a["pks"] = _addr(self._pks) + 48 * k_off
         a["n_pks"] = k
-        a["msg"] = ctypes.addressof(self._msgs) + m_off
+        a["msg"] = _addr(self._msgs) + m_off
         a["msg_len"] = ml
-        a["sig"] = ctypes.addressof(self._sigs) + 96 * np.arange(n, dtype=np.uint64)
+        a["sig"] = _addr(self._sigs) + 96 * np.arange(n, dtype=np.uint64)
         self._arr = a
         self.n = n
         self.ptr = ctypes.cast(a.ctypes.data, ctypes.POINTER(native.TblsSet))
