@@ -533,6 +533,10 @@ static bool sig_prio() {
   static const bool v = !(getenv("TBLS_SIG_PRIO") && getenv("TBLS_SIG_PRIO")[0] == '0');
   return v;
 }
+static bool sig_first() {
+  static const bool v = !(getenv("TBLS_SIG_FIRST") && getenv("TBLS_SIG_FIRST")[0] == '0');
+  return v;
+}
 // The accumulator waits for the bucket-sum stream, so that nothing of that
 // stream holds LDS or registers its one-round grid needs (TBLS_ACC_JOIN=0:
 // it starts after the signature checks only, A/B)
@@ -666,6 +670,16 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
   // priority its waves are dispatched first and the shorter key / signature
   // stages fill the SIMDs around them, instead of its last waves running
   // alone after the others finish.
+  // Bucket-sum batches: the hash waits for the signature checks.  Every
+  // large per-set kernel is one round of register-full waves, so whichever
+  // starts first holds the whole chip until it ends: with the hash first the
+  // signature checks, and the bucket-sum chain behind them, ran after it, and
+  // the bit-sum pairs' 64 wave Miller loops ended up after the line kernel,
+  // where the accumulator waited ~1.4 ms for them with the chip nearly idle
+  // (rocprof trace of the 131k step, profiles/r05_kernel_trace_step.txt).
+  // Signatures first, the bucket-sum chain overlaps the hash instead
+  // (TBLS_SIG_FIRST=0: the previous order, A/B).
+  if (late_join && sig_first()) HIPCHK(hipStreamWaitEvent(sh, c.e_sig, 0));
   TB_EV(6, sh);
   if (n && n <= TB_HASH_WAVE_MAX && coop())  // one 256-thread workgroup per set: coop SSWU chains and cofactor program
     hipLaunchKernelGGL(k_set_hash_coop, dim3(n), dim3(256), 0, sh, b.msgs, b.msg_off, dst, dlen, n, Q, skip, (const uint64_t*)nullptr);
