@@ -533,8 +533,8 @@ static bool sig_prio() {
   static const bool v = !(getenv("TBLS_SIG_PRIO") && getenv("TBLS_SIG_PRIO")[0] == '0');
   return v;
 }
-static bool sig_first() {
-  static const bool v = !(getenv("TBLS_SIG_FIRST") && getenv("TBLS_SIG_FIRST")[0] == '0');
+static int sig_first() {  // 0: hash first; 1: after the signature checks; 2: after the whole bucket-sum chain
+  static const int v = getenv("TBLS_SIG_FIRST") ? atoi(getenv("TBLS_SIG_FIRST")) : 1;
   return v;
 }
 // The accumulator waits for the bucket-sum stream, so that nothing of that
@@ -679,7 +679,7 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
   // (rocprof trace of the 131k step, profiles/r05_kernel_trace_step.txt).
   // Signatures first, the bucket-sum chain overlaps the hash instead
   // (TBLS_SIG_FIRST=0: the previous order, A/B).
-  if (late_join && sig_first()) HIPCHK(hipStreamWaitEvent(sh, c.e_sig, 0));
+  if (late_join && sig_first()) HIPCHK(hipStreamWaitEvent(sh, sig_first() == 2 ? c.e_join[1] : c.e_sig, 0));
   TB_EV(6, sh);
   if (n && n <= TB_HASH_WAVE_MAX && coop())  // one 256-thread workgroup per set: coop SSWU chains and cofactor program
     hipLaunchKernelGGL(k_set_hash_coop, dim3(n), dim3(256), 0, sh, b.msgs, b.msg_off, dst, dlen, n, Q, skip, (const uint64_t*)nullptr);
