@@ -534,7 +534,7 @@ static bool sig_prio() {
   return v;
 }
 static int sig_first() {  // 0: hash first; 1: after the signature checks; 2: after the whole bucket-sum chain
-  static const int v = getenv("TBLS_SIG_FIRST") ? atoi(getenv("TBLS_SIG_FIRST")) : 1;
+  static const int v = getenv("TBLS_SIG_FIRST") ? atoi(getenv("TBLS_SIG_FIRST")) : 0;
   return v;
 }
 // The accumulator waits for the bucket-sum stream, so that nothing of that
