@@ -533,9 +533,17 @@ static bool sig_prio() {
   static const bool v = !(getenv("TBLS_SIG_PRIO") && getenv("TBLS_SIG_PRIO")[0] == '0');
   return v;
 }
-static int sig_first() {  // 0: hash first; 1: after the signature checks; 2: after the whole bucket-sum chain
-  static const int v = getenv("TBLS_SIG_FIRST") ? atoi(getenv("TBLS_SIG_FIRST")) : 0;
-  return v;
+// Bucket-sum batches: when the hash starts.  0: at once (beside the key
+// decompression and the signature checks); 1: after the signature checks;
+// 2: after the whole bucket-sum chain.  Measured at 131,072 sets
+// (profiles/r05_bench_sig_first.json): keys as bytes 36.4-36.7 ms (0) /
+// 37.8-37.9 (1) / 38.5-38.9 (2); keys from the device table 3.61-3.65 /
+// 3.87-3.90 / 3.70-3.74 M sigs/s.  So 1 with the key table (no key
+// decompression beside the signature checks), else 0.  TBLS_SIG_FIRST
+// forces one (A/B).
+static int sig_first(bool key_table) {
+  static const int v = getenv("TBLS_SIG_FIRST") ? atoi(getenv("TBLS_SIG_FIRST")) : -1;
+  return v >= 0 ? v : key_table ? 1 : 0;
 }
 // The accumulator waits for the bucket-sum stream, so that nothing of that
 // stream holds LDS or registers its one-round grid needs (TBLS_ACC_JOIN=0:
@@ -670,16 +678,17 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
   // priority its waves are dispatched first and the shorter key / signature
   // stages fill the SIMDs around them, instead of its last waves running
   // alone after the others finish.
-  // Bucket-sum batches: the hash waits for the signature checks.  Every
-  // large per-set kernel is one round of register-full waves, so whichever
-  // starts first holds the whole chip until it ends: with the hash first the
-  // signature checks, and the bucket-sum chain behind them, ran after it, and
-  // the bit-sum pairs' 64 wave Miller loops ended up after the line kernel,
-  // where the accumulator waited ~1.4 ms for them with the chip nearly idle
-  // (rocprof trace of the 131k step, profiles/r05_kernel_trace_step.txt).
-  // Signatures first, the bucket-sum chain overlaps the hash instead
-  // (TBLS_SIG_FIRST=0: the previous order, A/B).
-  if (late_join && sig_first()) HIPCHK(hipStreamWaitEvent(sh, sig_first() == 2 ? c.e_join[1] : c.e_sig, 0));
+  // Bucket-sum batches with the key table: the hash waits for the signature
+  // checks (sig_first).  Every large per-set kernel is one round of
+  // register-full waves, so whichever starts first holds the whole chip until
+  // it ends: with the hash first, the signature checks and the bucket-sum
+  // chain behind them ran after it, and the bit-sum pairs' 64 wave Miller
+  // loops ended up after the line kernel, where the accumulator waited
+  // ~1.4 ms for them with the chip nearly idle (rocprof trace of the 131k
+  // step, profiles/r05_kernel_trace_step.txt).  With key decompression in
+  // the batch the hash-first order still measured faster.
+  const int sf = sig_first(use_tab);
+  if (late_join && sf) HIPCHK(hipStreamWaitEvent(sh, sf == 2 ? c.e_join[1] : c.e_sig, 0));
   TB_EV(6, sh);
   if (n && n <= TB_HASH_WAVE_MAX && coop())  // one 256-thread workgroup per set: coop SSWU chains and cofactor program
     hipLaunchKernelGGL(k_set_hash_coop, dim3(n), dim3(256), 0, sh, b.msgs, b.msg_off, dst, dlen, n, Q, skip, (const uint64_t*)nullptr);
