@@ -286,7 +286,7 @@ static void acc_env(int& e_per, int& e_seg) {
     return;
   }
   int p = 0, g = 0;
-  if (sscanf(v, "%d,%d", &p, &g) == 2 && p >= 1 && p <= TB_ACC_PER_MAX && (p & (p - 1)) == 0 && g >= 1 && g <= TB_ACC_NSEG_MAX) {
+  if (sscanf(v, "%d,%d", &p, &g) == 2 && p >= 1 && p <= 32 && (p & (p - 1)) == 0 && g >= 1 && g <= TB_ACC_NSEG_MAX) {  // per <= 32: one mask bit per pair
     e_per = p;
     e_seg = g;
   }
@@ -310,7 +310,7 @@ static void acc_plan(uint32_t n_main, uint32_t& per, uint32_t& nseg) {
   double best = 0;
   per = 1;
   nseg = 1;
-  for (uint32_t p = 1; p <= (uint32_t)TB_ACC_PER_MAX; p *= 2) {
+  for (uint32_t p = 1; p <= (uint32_t)std::max(TB_ACC_PER_MAX, e_per); p *= 2) {
     if (e_per > 0 && (int)p != e_per) continue;
     for (uint32_t sg = 1; sg <= (uint32_t)TB_ACC_NSEG_MAX; sg++) {
       if (e_seg > 0 ? (int)sg != e_seg : (sg & (sg - 1)) != 0) continue;
