@@ -420,6 +420,50 @@ def test_large_batch_msm_path(hip, n):
     assert _raw(bls, dup_p, dup_m, dup_s, dup_r)
 
 
+@pytest.mark.parametrize("n", [24576, 32768])
+def test_key_table_bucket_sum_batches(hip, n):
+    """Key-table batches large enough for the bucket-sum signature side: the
+    library starts their hash after the signature checks (tb_lib.hip
+    sig_first, keys from the table) instead of beside them.  Verdicts equal
+    the same batches by key bytes (test_large_batch_msm_path's order) for a
+    valid batch, a swapped signature, a non-G2 signature and a wrong key
+    index."""
+    bls, native, L, impl = hip
+    nk = 512
+    sks = b"".join(interop_sk(i % nk).to_bytes(32, "big") for i in range(n))
+    pk_out = ctypes.create_string_buffer(48 * nk)
+    native.check(L.tbls_sk_to_pk_many(sks[: 32 * nk], nk, pk_out), "sk_to_pk_many")
+    msgs = [i.to_bytes(4, "little") * 8 for i in range(n)]
+    off = (ctypes.c_uint32 * (n + 1))(*[32 * j for j in range(n + 1)])
+    sig_out = ctypes.create_string_buffer(96 * n)
+    dst = b"BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_POP_"
+    native.check(L.tbls_sign_many(sks, b"".join(msgs), off, n, dst, len(dst), sig_out), "sign_many")
+    keys = [pk_out.raw[48 * k : 48 * k + 48] for k in range(nk)]
+    sigs = [sig_out.raw[96 * i : 96 * i + 96] for i in range(n)]
+    table = bls.ValidatorKeyTable(keys)
+    assert table.codes == [0] * nk
+    rng = random.Random(11)
+    rands = [rng.getrandbits(64) | 1 for _ in range(n)]
+    sets = [([i % nk], msgs[i], sigs[i]) for i in range(n)]
+
+    def both(batch):
+        by_idx = table.batch_verify(batch, rands)
+        by_bytes = _raw(bls, [keys[ks[0]] for ks, _, _ in batch], [m for _, m, _ in batch], [sg for _, _, sg in batch], rands)
+        assert by_idx is by_bytes
+        return by_idx
+
+    assert both(sets) is True
+    bad = list(sets)
+    bad[12345] = (bad[12345][0], msgs[12345], sigs[12346])
+    assert both(bad) is False
+    bad = list(sets)
+    bad[5] = (bad[5][0], msgs[5], NOT_IN_G2)
+    assert both(bad) is False
+    bad = list(sets)
+    bad[n - 7] = ([(n - 6) % nk], msgs[n - 7], sigs[n - 7])
+    assert both(bad) is False
+
+
 def test_validator_key_table(hip, sets8):
     """Device-resident key table (tbls_pk_table_load / tbls_batch_verify_idx,
     SURVEY.md 8(f) rank 1): per-key codes as tbls_pk_validate; batches by key
