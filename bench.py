@@ -93,11 +93,8 @@ def plan_counts(S):
     (tools/count_muls.py miller_seg_PxS), the unsegmented k_miller_acc2 among 2."""
     per, nseg, split = acc_plan(S)
     mc = dict(M_PER_UNIT)
-    # the library's accumulator (tb_lib.hip acc_lds): f in LDS and lines paired unless the bucket-sum
-    # stream may still run beside it (bucket sums without the join, acc_join: TBLS_ACC_JOIN=0)
-    env = os.environ.get("TBLS_ACC_LDS")
-    msm = S >= int(os.environ.get("TBLS_MSM_MIN", 20480))
-    lds = (env != "0") if env is not None else (not msm or os.environ.get("TBLS_ACC_JOIN") != "0")
+    # the library's accumulator (tb_lib.hip acc_lds): f in LDS and lines paired; TBLS_ACC_LDS=0: registers
+    lds = os.environ.get("TBLS_ACC_LDS") != "0"
     key = f"miller_seg2_{per}x{nseg}" if lds else f"miller_seg_{per}x{nseg}"
     seg = split and (nseg > 1 or per > 2)
     if seg and key in mc:

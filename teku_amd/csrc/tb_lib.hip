@@ -441,10 +441,9 @@ struct ws_layout {
 #define TB_NSTAGE 7
 #define TB_NSTAGE_EV (2 * TB_NSTAGE)
 // Streams: keys on aux[0], signatures (+ bucket sums) on aux[1], hash_to_G2
-// on aux[2]; aux[1] and aux[2] at high priority (sig_prio); all three join
-// the caller's stream before the Miller loops (the bucket-sum chain before
-// the accumulator, acc_join; without acc_join only before the product
-// tree).  `serial`
+// on aux[2]; aux[1] and aux[2] at high priority; all three join the
+// caller's stream before the Miller loops (the bucket-sum chain before the
+// accumulator, acc_lds).  `serial`
 // (the stage-profile API) runs everything on the caller's stream, for
 // exclusive per-stage timings.
 
@@ -505,32 +504,20 @@ void launch_set_pk(hipStream_t s, uint32_t n, uint32_t n_entries, const uint32_t
 // and scratch writes 3.3 -> 1.5 GB per launch.  Its grid is one round of
 // workgroups at full LDS (4 x 36,864 B per CU), so a workgroup of the
 // bucket-sum stream still resident on a CU pushes part of it into a second
-// round: beside that stream the 131k step went 38.2 -> 43.9 ms.  The bucket
-// sums now run on the high-priority signature stream (sig_prio) and the
-// accumulator waits for that stream (acc_join): with both, the LDS kernel
-// runs at every batch size -- 131k step 37.3 -> 36.1-36.6 ms
-// (profiles/r05_bench_prio_join.json).  TBLS_ACC_LDS=0 / 1 forces one kernel
-// everywhere (A/B; auto = LDS unless the bucket sums may run beside it).
+// round: beside that stream the 131k step went 38.2 -> 43.9 ms.  So the
+// bucket sums run on a high-priority stream (the signature stream, created
+// at the hash stream's priority in tbls_init) and the accumulator waits for
+// that stream: with both, the LDS kernel runs at every batch size -- 131k
+// step 37.3 -> 36.1-36.6 ms (profiles/r05_bench_prio_join.json; the two
+// were A/B switches in round 5, TBLS_SIG_PRIO / TBLS_ACC_JOIN).
+// TBLS_ACC_LDS=0 selects the register-resident k_miller_accs (A/B).
 extern "C" __global__ void k_miller_accs_lds(const uint4* __restrict__ lines, const uint8_t* __restrict__ skip, const uint8_t* __restrict__ code_a,
                                              const uint8_t* __restrict__ code_b, uint32_t n, uint32_t per, uint32_t nseg, uint32_t g_pad,
                                              fp12* __restrict__ f_out, uint32_t seg_stride);
 extern "C" __global__ void k_msm_bucket_tree(const g2a* __restrict__ sig_aff, const uint8_t* __restrict__ use, const uint32_t* __restrict__ off,
                                              const uint32_t* __restrict__ idx, g2j* __restrict__ bucket);  // k_sigs.hip
-static int acc_lds_env() {  // -1 auto, 0 never, 1 always
-  static const int v = getenv("TBLS_ACC_LDS") ? (getenv("TBLS_ACC_LDS")[0] == '0' ? 0 : 1) : -1;
-  return v;
-}
-// the LDS accumulator for a launch with (msm_beside) or without the bucket-sum stream running beside it
-static bool acc_lds(bool msm_beside = false) {
-  const int e = acc_lds_env();
-  return e < 0 ? !msm_beside : e == 1;
-}
-// The signature stream -- signature checks, then the bucket sums and the
-// bit-sum pairs' wave Miller loops -- at the hash stream's high priority, so
-// that the bucket-sum chain runs during the hash instead of beside the Miller
-// accumulator (TBLS_SIG_PRIO=0: normal priority, A/B; read at tbls_init)
-static bool sig_prio() {
-  static const bool v = !(getenv("TBLS_SIG_PRIO") && getenv("TBLS_SIG_PRIO")[0] == '0');
+static bool acc_lds() {
+  static const bool v = !(getenv("TBLS_ACC_LDS") && getenv("TBLS_ACC_LDS")[0] == '0');
   return v;
 }
 // Bucket-sum batches: when the hash starts.  0: at once (beside the key
@@ -544,13 +531,6 @@ static bool sig_prio() {
 static int sig_first(bool key_table) {
   static const int v = getenv("TBLS_SIG_FIRST") ? atoi(getenv("TBLS_SIG_FIRST")) : -1;
   return v >= 0 ? v : key_table ? 1 : 0;
-}
-// The accumulator waits for the bucket-sum stream, so that nothing of that
-// stream holds LDS or registers its one-round grid needs (TBLS_ACC_JOIN=0:
-// it starts after the signature checks only, A/B)
-static bool acc_join() {
-  static const bool v = !(getenv("TBLS_ACC_JOIN") && getenv("TBLS_ACC_JOIN")[0] == '0');
-  return v;
 }
 extern "C" __global__ void k_set_hash_wave(const uint8_t* __restrict__ msgs, const uint32_t* __restrict__ msg_off,
                                            const uint8_t* __restrict__ dst, uint32_t dlen, uint32_t n, g2a* __restrict__ Q,
@@ -745,10 +725,10 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
           hipLaunchKernelGGL(k_miller_lines_w2, dim3((m + TB_BLOCK - 1) / TB_BLOCK), blk, 0, s,
                              (const g1a*)P + lo, (const g2a*)Q + lo, (const uint8_t*)skip + lo, ca + lo, cb + lo, m, lines);
         if (settle) continue;  // settle_sets accumulates per set from these lines
-        if (late_join && acc_join() && lo == 0) HIPCHK(hipStreamWaitEvent(s, c.e_join[1], 0));
+        if (late_join && lo == 0) HIPCHK(hipStreamWaitEvent(s, c.e_join[1], 0));  // the bucket-sum stream first (acc_lds)
         if (pp.seg()) {
           const uint32_t g_pad = (mt + TB_BLOCK - 1) / TB_BLOCK * TB_BLOCK;
-          hipLaunchKernelGGL(acc_lds(pp.msm && !acc_join()) ? k_miller_accs_lds : k_miller_accs, dim3(pp.nseg * g_pad / TB_BLOCK), blk, 0, s,
+          hipLaunchKernelGGL(acc_lds() ? k_miller_accs_lds : k_miller_accs, dim3(pp.nseg * g_pad / TB_BLOCK), blk, 0, s,
                              (const uint4*)lines,
                              (const uint8_t*)skip + lo,
                              ca + lo, cb + lo, m, pp.per, pp.nseg, g_pad, f + lo / pp.per, pp.n_groups());
@@ -1358,7 +1338,7 @@ extern "C" int tbls_init(int n_devices, uint32_t flags) {
     if (hipSetDevice(d) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->aux[0], hipStreamNonBlocking) != hipSuccess ||
         hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess ||
-        hipStreamCreateWithPriority(&c->aux[1], hipStreamNonBlocking, sig_prio() ? prio_hi : prio_lo) != hipSuccess ||
+        hipStreamCreateWithPriority(&c->aux[1], hipStreamNonBlocking, prio_hi) != hipSuccess ||
         hipStreamCreateWithPriority(&c->aux[2], hipStreamNonBlocking, prio_hi) != hipSuccess ||
         hipEventCreateWithFlags(&c->e_join[2], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->e_fork, hipEventDisableTiming) != hipSuccess ||
