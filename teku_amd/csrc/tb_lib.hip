@@ -1338,7 +1338,7 @@ extern "C" int tbls_init(int n_devices, uint32_t flags) {
     if (hipSetDevice(d) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->aux[0], hipStreamNonBlocking) != hipSuccess ||
         hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess ||
-        hipStreamCreateWithPriority(&c->aux[1], hipStreamNonBlocking, getenv("TBLS_SIG_PRIO") && getenv("TBLS_SIG_PRIO")[0] == '0' ? prio_lo : prio_hi) != hipSuccess ||
+        hipStreamCreateWithPriority(&c->aux[1], hipStreamNonBlocking, prio_hi) != hipSuccess ||
         hipStreamCreateWithPriority(&c->aux[2], hipStreamNonBlocking, prio_hi) != hipSuccess ||
         hipEventCreateWithFlags(&c->e_join[2], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->e_fork, hipEventDisableTiming) != hipSuccess ||
