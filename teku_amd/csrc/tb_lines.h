@@ -120,8 +120,9 @@ __device__ TB_INLINE void line_store(uint4* __restrict__ lines, uint32_t n, uint
 __device__ TB_INLINE line3 line_load(const uint4* __restrict__ lines, uint32_t n, uint32_t i, int s) {
   line3 l;
   fp* c[6] = {&l.a.c0, &l.a.c1, &l.b.c0, &l.b.c1, &l.c.c0, &l.c.c1};
+  const uint4* __restrict__ row = lines + (size_t)(s * TB_LINE_G) * n;  // wave-uniform where s is
   TB_UNROLL for (int g = 0; g < TB_LINE_G; g++) {
-    const uint4 v = lines[(size_t)(s * TB_LINE_G + g) * n + i];
+    const uint4 v = row[(uint32_t)(g * n + i)];  // g n + i < TB_LINE_G x TB_LINE_CHUNK < 2^32
     const int w = 4 * g;
     c[(w + 0) / 12]->l[(w + 0) % 12] = v.x;
     c[(w + 1) / 12]->l[(w + 1) % 12] = v.y;
@@ -268,8 +269,12 @@ __device__ TB_INLINE fp12 line_fp12(const line3& l) { return {{l.a, l.b, fp2_zer
 __device__ TB_INLINE void miller_accs_body(const uint4* __restrict__ lines, const uint8_t* __restrict__ skip,
                                            const uint8_t* __restrict__ code_a, const uint8_t* __restrict__ code_b, uint32_t n, uint32_t per,
                                            uint32_t nseg, uint32_t g_pad, fp12* __restrict__ f_out, uint32_t seg_stride) {
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t j = t / g_pad, g = t % g_pad;
+  // segment and group from the block index (g_pad is a multiple of the
+  // block): j, and with it the step counter, is wave-uniform, so a line
+  // load's row base is scalar (round 5: scratch 484 -> 324 B per lane in
+  // k_miller_accs_lds, 544 -> 392 in k_miller_accs)
+  const uint32_t bps = g_pad / TB_BLOCK;
+  const uint32_t j = blockIdx.x / bps, g = (blockIdx.x % bps) * TB_BLOCK + threadIdx.x;
   const uint32_t G = (n + per - 1) / per;
   if (j >= nseg || g >= G) return;
   const int s_lo = (int)(TB_LINE_STEPS * j / nseg), s_hi = (int)(TB_LINE_STEPS * (j + 1) / nseg);
@@ -481,8 +486,12 @@ template <bool HALF>
 __device__ TB_INLINE void miller_accs_lds_body(uint4* __restrict__ Fsh, const uint4* __restrict__ lines, const uint8_t* __restrict__ skip,
                                                const uint8_t* __restrict__ code_a, const uint8_t* __restrict__ code_b, uint32_t n,
                                                uint32_t per, uint32_t nseg, uint32_t g_pad, fp12* __restrict__ f_out, uint32_t seg_stride) {
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t j = t / g_pad, g = t % g_pad;
+  // segment and group from the block index (g_pad is a multiple of the
+  // block): j, and with it the step counter, is wave-uniform, so a line
+  // load's row base is scalar (round 5: scratch 484 -> 324 B per lane in
+  // k_miller_accs_lds, 544 -> 392 in k_miller_accs)
+  const uint32_t bps = g_pad / TB_BLOCK;
+  const uint32_t j = blockIdx.x / bps, g = (blockIdx.x % bps) * TB_BLOCK + threadIdx.x;
   const uint32_t G = (n + per - 1) / per;
   if (j >= nseg || g >= G) return;
   const int s_lo = (int)(TB_LINE_STEPS * j / nseg), s_hi = (int)(TB_LINE_STEPS * (j + 1) / nseg);
