@@ -3,7 +3,10 @@ bench's order) vs cold: runs the KZG leg, then ~LOAD_S seconds of 131k-set
 device partials, then the KZG leg again; prints both and the SCLK the driver
 reports (rocm-smi, read-only) before and after the load.
 
-    python tools/kzg_after_load.py [load_seconds]
+    python tools/kzg_after_load.py [load_seconds] [bls_first]
+
+bls_first: initialise the BLS library and run one partial before the KZG
+context exists (the bench's order).
 """
 
 import ctypes
@@ -33,9 +36,15 @@ def sclk():
 
 def main():
     load_s = float(sys.argv[1]) if len(sys.argv) > 1 else 60.0
+    bls_first = len(sys.argv) > 2 and sys.argv[2] == "bls_first"
     device = torch.device("cuda", 0)
     torch.cuda.set_device(0)
-    res = {"cold": None, "after_load": None}
+    res = {"cold": None, "after_load": None, "bls_first": bls_first}
+    if bls_first:
+        L0 = native.lib()
+        pks, msgs, sigs = synth.single_signer(0, 128)
+        arr = synth.SetArray.single(pks, msgs, sigs)
+        assert arr.batch_verify(synth.fast_multipliers(128))
     res["sclk_cold"] = sclk()
     res["cold"] = {k: v for k, v in bench.kzg_leg(device, 20, False).items() if k in ("p50_ms_1", "p50_ms_6")}
     L = native.lib()
