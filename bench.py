@@ -66,7 +66,7 @@ STAGE_KERNEL = {
     "set_sig": "k_sig_check_w2",
     "set_hash": "k_set_hash_w2 + k_set_hash_fix",
     "g2_sum": "k_msm_bucket_tree + k_msm_bitsum_pairs + 64 x k_miller_wave",
-    "miller": "k_miller_lines_w2 + k_miller_accs",
+    "miller": "k_miller_lines_w2 + k_miller_accs_lds",
     "fp12_prod": "k_fp12_prod_wave_seg + k_fp12_seg_combine_coop",
 }
 STAGE_UNITS = {"pk_decompress": "keys", "set_pk": "sets", "set_sig": "sets", "set_hash": "sets", "g2_sum": "sets", "miller": "pairs", "fp12_prod": "pairs"}
@@ -89,13 +89,12 @@ def acc_plan(S):
 
 def plan_counts(S):
     """M_PER_UNIT with the Miller work of the plan the library runs at S sets:
-    the segmented accumulator (k_miller_accs) shares one f^2 among `per` pairs
-    (tools/count_muls.py miller_seg_PxS), the unsegmented k_miller_acc2 among 2."""
+    the segmented accumulator (k_miller_accs_lds: f in LDS, lines paired)
+    shares one f^2 among `per` pairs (tools/count_muls.py miller_seg2_PxS), the
+    unsegmented k_miller_acc2 among 2."""
     per, nseg, split = acc_plan(S)
     mc = dict(M_PER_UNIT)
-    # the library's accumulator (tb_lib.hip acc_lds): f in LDS and lines paired; TBLS_ACC_LDS=0: registers
-    lds = os.environ.get("TBLS_ACC_LDS") != "0"
-    key = f"miller_seg2_{per}x{nseg}" if lds else f"miller_seg_{per}x{nseg}"
+    key = f"miller_seg2_{per}x{nseg}"
     seg = split and (nseg > 1 or per > 2)
     if seg and key in mc:
         d = mc[key] - mc["miller"]
@@ -109,7 +108,7 @@ def plan_counts(S):
     if os.environ.get("TBLS_W2") == "0":  # the library's kernel selection (tb_lib.hip w2)
         kern.update(set_pk="k_set_pk", set_sig="k_sig_check", set_hash="k_set_hash")
     lines_k = "k_miller_lines_w2"
-    acc_k = ("k_miller_accs_lds" if lds else "k_miller_accs") if seg else f"k_miller_acc{2 if per == 2 else 1}"
+    acc_k = "k_miller_accs_lds" if seg else f"k_miller_acc{2 if per == 2 else 1}"
     kern["miller"] = f"{lines_k} + {acc_k}"
     return mc, kern, {"per": per, "nseg": nseg, "kernel": acc_k}
 

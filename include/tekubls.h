@@ -47,7 +47,13 @@ enum {
 
 /* Library lifecycle.  n_devices = -1 uses every visible device.
  * Replaces BlstLoader.INSTANCE (impl/blst/BlstLoader.java:32-51): a loader
- * that gets an error here yields Optional.empty(). */
+ * that gets an error here yields Optional.empty().
+ * flags: TBLS_INIT_SHARE_DEVICES makes n_devices (<= 32) library devices over
+ * the visible hardware devices round-robin, each with its own streams,
+ * workspace and lock -- so a one-GPU host runs the multi-device paths
+ * (sharding, the record gather, per-shard settling) for tests; the gather of
+ * devices that share hardware uses peer copies instead of RCCL. */
+enum { TBLS_INIT_SHARE_DEVICES = 1u };
 int tbls_init(int n_devices, uint32_t flags);
 void tbls_shutdown(void);
 int tbls_device_count(void);
@@ -123,7 +129,7 @@ typedef struct {
 
 typedef struct {
   double total_ms;     /* API entry -> result, host clock */
-  double device_ms;    /* sum over devices of the kernel pipeline, HIP events */
+  double device_ms;    /* sum over devices of the batch's kernel pipeline, HIP events (a settle after a failed batch is in total_ms only) */
   uint32_t n_devices;  /* devices used */
 } tbls_timing;
 
@@ -133,7 +139,8 @@ typedef struct {
  * .nextBatchRandomMultiplier (l.191-195) -- the caller owns the RNG.  n_gpus:
  * at most that many devices (0 = all initialised devices); the batch goes to
  * the least-loaded device, or is sharded over several idle ones when it has at
- * least 2 x tbls_shard_min() sets (tbls_place_plan); each device produces one Fp12
+ * least 2 x tbls_shard_min() sets, or 2 x tbls_shard_knee() sets when every
+ * device is idle (tbls_place_plan); each device produces one Fp12
  * partial product, gathered for one final exponentiation.  *ok = 1 iff every set is valid and the pairing product is
  * 1.  n == 0 -> *ok = 0 (BLS.java:240-241).  A set with n_pks == 0 ->
  * TBLS_BAD_ARGUMENT (BlstPublicKey.aggregate checkArgument, l.56). */
@@ -265,15 +272,21 @@ int tbls_acc_plan(uint32_t n, uint32_t* per, uint32_t* nseg, int* split);
  * ties broken round-robin from rr, in ascending order in dev_out[0..G) (the
  * first is the gather root); with no idle device, the least-loaded one --
  * with contiguous shards balanced by key count: device dev_out[k] gets sets
- * [cut_out[k], cut_out[k+1]) (cut_out: G + 1 entries).  Returns G >= 1, or
+ * [cut_out[k], cut_out[k+1]) (cut_out: G + 1 entries).  When EVERY device is
+ * idle, shard_knee_sets (if nonzero and smaller) replaces shard_min_sets: a
+ * lone batch on an idle node shards down to the latency knee (a lone
+ * 16,384-set batch: 4 devices of 4,096).  Returns G >= 1, or
  * -TBLS_BAD_ARGUMENT.  A concurrent caller of the live library sees the
  * devices other batches hold as loaded, so N service workers with
  * config-4-sized batches land on N different devices, one each
- * (AggregatingSignatureVerificationService.java:121-132, 202-205). */
+ * (AggregatingSignatureVerificationService.java:121-132, 202-205); a service
+ * that has more batches waiting passes n_gpus = 1. */
 int tbls_place_plan(size_t n, const uint32_t* n_pks, int n_devices, int n_gpus, const int* load, uint32_t rr, uint32_t shard_min_sets,
-                    int* dev_out, size_t* cut_out);
-/* The live shard_min_sets (32768, or TBLS_SHARD_MIN). */
+                    uint32_t shard_knee_sets, int* dev_out, size_t* cut_out);
+/* The live shard_min_sets (32768) and shard_knee_sets (4096); TBLS_SHARD_MIN =
+ * "min[,knee]" overrides them (a lone min also caps the knee at min). */
 uint32_t tbls_shard_min(void);
+uint32_t tbls_shard_knee(void);
 
 /* Multiply g partial records (device memory, contiguous) and run the final
  * exponentiation: *ok = 1 iff no invalid set and the product is 1. */

@@ -220,3 +220,13 @@ extern "C" __global__ void __launch_bounds__(CFE_THREADS)
   const bool one = cfe::final_exp_is_one(L, R);
   if (threadIdx.x == 0) out[blockIdx.x] = one ? 1 : 0;
 }
+
+// Before settling a failed batch (tb_lib.hip settle_sets): a set whose key
+// check failed (set_code[g] != 0) is invalid from its code alone, so its
+// signature pair n + g is skipped too, and the set contributes 1 to its 16-
+// and 256-set groups instead of failing them (which pushed every set of
+// those groups down to single-set final exponentiations).
+extern "C" __global__ void __launch_bounds__(256) k_settle_mask(const uint8_t* __restrict__ set_code, uint32_t n, uint8_t* __restrict__ skip) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g < n && set_code[g] != 0) skip[n + g] = 1;
+}

@@ -19,7 +19,7 @@ __device__ TB_INLINE void coef_store(uint4* __restrict__ lines, uint32_t n, uint
   const uint32_t* w = &v.c0.l[0];
   static_assert(sizeof(fp2) == 96, "fp2 is 24 consecutive words");
   TB_UNROLL for (int g = 0; g < 6; g++)
-    lines[(size_t)(s * TB_LINE_G + 6 * k + g) * n + i] = make_uint4(w[4 * g], w[4 * g + 1], w[4 * g + 2], w[4 * g + 3]);
+    line_st16(&lines[(size_t)(s * TB_LINE_G + 6 * k + g) * n + i], make_uint4(w[4 * g], w[4 * g + 1], w[4 * g + 2], w[4 * g + 3]));
 }
 
 // tb_lines.h dbl_step_f, reordered: the same T and line

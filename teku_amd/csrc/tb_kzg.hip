@@ -50,6 +50,13 @@ int fail(int rc, const char* fmt, ...) {
 
 size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
 
+// Device allocations of the KZG context are rounded up to TKZG_ALLOC_ROUND
+// bytes (0: as requested; A/B of the allocation-order slowdown).
+#ifndef TKZG_ALLOC_ROUND
+#define TKZG_ALLOC_ROUND 0
+#endif
+size_t dev_round(size_t nb) { return TKZG_ALLOC_ROUND ? (nb + TKZG_ALLOC_ROUND - 1) / TKZG_ALLOC_ROUND * TKZG_ALLOC_ROUND : nb; }
+
 struct growbuf {
   void* p = nullptr;
   size_t cap = 0;
@@ -57,7 +64,7 @@ struct growbuf {
   int ensure(size_t bytes) {
     if (bytes <= cap) return 0;
     release();
-    const size_t nb = bytes < 65536 ? 65536 : bytes + bytes / 4;
+    const size_t nb = host ? (bytes < 65536 ? 65536 : bytes + bytes / 4) : dev_round(bytes < 65536 ? 65536 : bytes + bytes / 4);
     const hipError_t e = host ? hipHostMalloc(&p, nb, hipHostMallocDefault) : hipMalloc(&p, nb);
     if (e != hipSuccess) {
       p = nullptr;
@@ -139,7 +146,7 @@ pair_ws take_pair_ws(carve& c) {
 void launch_pairing(kzg_state& g, const g1j* T, uint32_t n, const pair_ws& p, int* ok, hipStream_t s) {
   hipLaunchKernelGGL(k_kzg_pair_sums, dim3(1), dim3(256), 0, s, T, n, (const g2a*)(g.g2 + 1), p.P, p.Q, p.skip, p.zero);
   const uint8_t* z8 = reinterpret_cast<const uint8_t*>(p.zero);
-  hipLaunchKernelGGL(k_miller_wave, dim3(2), dim3(64), 0, s, (const g1a*)p.P, (const g2a*)p.Q, (const uint8_t*)p.skip, z8, z8, 2u, p.f);
+  hipLaunchKernelGGL(k_miller_coop, dim3(2), dim3(256), 0, s, (const g1a*)p.P, (const g2a*)p.Q, (const uint8_t*)p.skip, z8, z8, 2u, p.f);
   if (tb_final_coop())
     hipLaunchKernelGGL(k_final_verify_coop, dim3(1), dim3(TB_CFE_THREADS), 0, s, (const fp12*)p.f, 2u, (const uint32_t*)p.zero, ok);
   else
@@ -395,7 +402,7 @@ extern "C" int tkzg_load_trusted_setup(const uint8_t* g1_monomial, size_t g1_mon
   // device: [lag | lag_inf | roots | g2 | g2_inf]  scratch: [bytes in | codes]
   const size_t persist = align16(N * sizeof(g1a)) + align16(N) + align16(N * sizeof(fr)) + align16(NG2 * sizeof(g2a)) + align16(NG2);
   void* p = nullptr;
-  KCHK(hipMalloc(&p, persist));
+  KCHK(hipMalloc(&p, dev_round(persist)));
   carve c{static_cast<uint8_t*>(p)};
   g.lag = c.take<g1a>(N);
   g.lag_inf = c.take<uint8_t>(N);

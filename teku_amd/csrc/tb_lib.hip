@@ -140,19 +140,48 @@ size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
 // whatever their load: a 16,384-set batch took all 8 devices and concurrent
 // workers serialized on them -- about 2.5 M sigs/s for the node where one
 // batch per device gives about 13.9 M)
-// TBLS_SHARD_MIN overrides shard_min (0: every allowed idle device).
-// tbls_place_plan exposes the same function for CPU tests.
+//  * on an IDLE NODE (no batch in flight on any device) a lone batch may
+//    shard further, down to the latency knee of TB_SHARD_KNEE = 4,096 sets
+//    per device (the same sweep: the device partial is 5.5 ms at 1,024 sets,
+//    5.8 at 4,096, 6.5 at 8,192, 8.6 at 16,384), so a lone config-4 batch of
+//    16,384 sets runs as 4 shards of 4,096: modelled latency 8.6 + 0.8 (final)
+//    -> 5.8 + 0.8 ms plus the record gather.  Under load the rule above
+//    holds: one device per batch.  A service that knows more batches are
+//    waiting passes n_gpus = 1 (teku_amd/service.py, and the Java mirror
+//    HipAggregatingSignatureVerificationService), so the first of several
+//    queued batches does not take the whole idle node.
+// TBLS_SHARD_MIN = "min[,knee]" overrides shard_min and the knee (min 0:
+// every allowed idle device).  tbls_place_plan exposes the same function for
+// CPU tests.
 // ---------------------------------------------------------------------------
 #define TB_SHARD_MIN 32768u
-uint32_t shard_min() {
-  static const uint32_t v = getenv("TBLS_SHARD_MIN") ? (uint32_t)atoi(getenv("TBLS_SHARD_MIN")) : TB_SHARD_MIN;
+#define TB_SHARD_KNEE 4096u
+struct shard_env_t {
+  uint32_t smin, knee;
+};
+static const shard_env_t& shard_env() {
+  static const shard_env_t v = [] {
+    shard_env_t e{TB_SHARD_MIN, TB_SHARD_KNEE};
+    const char* s = getenv("TBLS_SHARD_MIN");
+    if (s) {
+      unsigned a = 0, b = 0;
+      const int k = sscanf(s, "%u,%u", &a, &b);
+      if (k >= 1) e.smin = a;
+      e.knee = k == 2 ? b : std::min(e.smin, (uint32_t)TB_SHARD_KNEE);
+    }
+    return e;
+  }();
   return v;
 }
+uint32_t shard_min() { return shard_env().smin; }
+uint32_t shard_knee() { return shard_env().knee; }
 
 // n sets (keys(i) keys each) over D devices with loads load[0..D): returns G
 // and fills dev[0..G) (ascending) and cut[0..G] (cut[0] = 0, cut[G] = n).
+// knee (0: none): the shard size floor when every device is idle.
 template <class KEYS>
-int place_plan(size_t n, const KEYS& keys, int D, int n_gpus, const int* load, uint32_t rr, uint32_t smin, int* dev, size_t* cut) {
+int place_plan(size_t n, const KEYS& keys, int D, int n_gpus, const int* load, uint32_t rr, uint32_t smin, uint32_t knee, int* dev,
+               size_t* cut) {
   if (D < 1) return 0;
   const int Gmax = (n_gpus > 0 && n_gpus < D) ? n_gpus : D;
   std::vector<int> order(D);
@@ -165,6 +194,7 @@ int place_plan(size_t n, const KEYS& keys, int D, int n_gpus, const int* load, u
   });
   int idle = 0;
   while (idle < D && (!load || load[order[idle]] == 0)) idle++;
+  if (idle == D && knee && smin && knee < smin) smin = knee;  // idle node: shard down to the latency knee
   const size_t g = smin ? n / smin : (size_t)Gmax;
   int G = (int)std::min<size_t>(std::max<size_t>(g, 1), (size_t)std::min(Gmax, std::max(idle, 1)));
   if ((size_t)G > n) G = n ? (int)n : 1;
@@ -200,19 +230,19 @@ struct placed {
   }
 };
 template <class KEYS>
-void place_batch(placed& pl, size_t n, const KEYS& keys, int n_gpus, uint32_t smin) {
+void place_batch(placed& pl, size_t n, const KEYS& keys, int n_gpus, uint32_t smin, uint32_t knee) {
   std::lock_guard<std::mutex> lk(g_place_mu);
   const int D = (int)g_ctx.size();
   std::vector<int> load(D);
   for (int d = 0; d < D; d++) load[d] = g_ctx[d]->load;
   pl.dev.assign(D, 0);
   pl.cut.assign(D + 1, 0);
-  pl.G = place_plan(n, keys, D, n_gpus, load.data(), g_place_rr++, smin, pl.dev.data(), pl.cut.data());
+  pl.G = place_plan(n, keys, D, n_gpus, load.data(), g_place_rr++, smin, knee, pl.dev.data(), pl.cut.data());
   for (int k = 0; k < pl.G; k++) g_ctx[pl.dev[k]]->load++;
 }
 // one device for a whole call (single verifications, helpers)
 void place_one(placed& pl) {
-  place_batch(pl, 1, [](size_t) { return 1u; }, 0, 1);
+  place_batch(pl, 1, [](size_t) { return 1u; }, 0, 1, 0);
 }
 
 // --------------------------------------------------------------------------
@@ -246,11 +276,36 @@ static uint32_t msm_min() {
 // accumulator wave per SIMD: 1024 waves x 64 lanes x 2 pairs).
 #define TB_LINE_CHUNK 262144u
 #define TB_MILLER_PER2_MIN 131072u
-// up to this many pairs, one pair per 64-lane workgroup (k_miller_wave);
-// TBLS_MILLER_WAVE_MAX overrides (tuning)
-static uint32_t miller_wave_max() {
-  static const uint32_t v = getenv("TBLS_MILLER_WAVE_MAX") ? (uint32_t)atoi(getenv("TBLS_MILLER_WAVE_MAX")) : 2048u;
+// up to this many pairs, one pair per workgroup: the level program on coop
+// rows (k_miller_coop, 256 threads: a pair's loop in ~1/4 of the wave
+// kernel's time) up to TB_MILLER_COOP_MAX pairs -- one wave round of
+// 4-wave workgroups -- else one 64-lane wave per pair (k_miller_wave);
+// TBLS_MILLER_WAVE_MAX = "wave_max[,coop_max]" overrides (tuning)
+#define TB_MILLER_COOP_MAX 512u
+struct miller_env_t {
+  uint32_t wave_max, coop_max;
+};
+static const miller_env_t& miller_env() {
+  static const miller_env_t v = [] {
+    miller_env_t e{2048u, TB_MILLER_COOP_MAX};
+    const char* s = getenv("TBLS_MILLER_WAVE_MAX");
+    unsigned a = 0, b = 0;
+    const int k = s ? sscanf(s, "%u,%u", &a, &b) : 0;
+    if (k >= 1) e.wave_max = a;
+    if (k == 2) e.coop_max = b;
+    return e;
+  }();
   return v;
+}
+static uint32_t miller_wave_max() { return miller_env().wave_max; }
+static bool miller_coop(uint32_t n_pairs) { return n_pairs <= miller_env().coop_max; }
+// the wave-shaped Miller kernels: a pair per workgroup
+static void launch_miller_pairs(hipStream_t s, uint32_t np, const g1a* P, const g2a* Q, const uint8_t* skip, const uint8_t* ca,
+                                const uint8_t* cb, fp12* f) {
+  if (miller_coop(np))
+    hipLaunchKernelGGL(k_miller_coop, dim3(np), dim3(256), 0, s, P, Q, skip, ca, cb, np, f);
+  else
+    hipLaunchKernelGGL(k_miller_wave, dim3(np), dim3(64), 0, s, P, Q, skip, ca, cb, np, f);
 }
 
 // Pairs of a batch of n sets: [0, n) the sets' (r_i apk_i, H(m_i)), then the
@@ -259,7 +314,7 @@ static uint32_t miller_wave_max() {
 // split Miller loop the bit-sum pairs run one 64-lane wave each (k_miller_wave,
 // n_xwave of them) on the bucket-sum stream, into the Miller values after the
 // accumulators'.
-// Segmented accumulator (k_lines.hip k_miller_accs): `per` pairs per thread,
+// Segmented accumulator (k_lines.hip k_miller_accs_lds): `per` pairs per thread,
 // the loop's 68 steps in `nseg` segments.  Chosen to minimize the modelled
 // accumulator time: per-thread latency (68 / nseg) (12 + 13 per) Fp2
 // products (one f^2, per sparse line products per step) times the wave rounds
@@ -343,7 +398,7 @@ struct pair_plan {
     per = 1;
     if (split) acc_plan(std::min(n_main, TB_LINE_CHUNK), per, nseg);  // the chunks launch one after another: plan one chunk's fill
   }
-  bool seg() const { return split && (nseg > 1 || per > 2); }  // k_miller_accs
+  bool seg() const { return split && (nseg > 1 || per > 2); }  // k_miller_accs_lds
   uint32_t n_groups() const { return (n_main + per - 1) / per; }
   uint32_t n_f_main() const { return nseg * n_groups(); }
   uint32_t n_f() const { return n_f_main() + n_xwave; }  // Miller values: accumulators (segment-major), then the wave pairs'
@@ -509,29 +564,22 @@ void launch_set_pk(hipStream_t s, uint32_t n, uint32_t n_entries, const uint32_t
 // at the hash stream's priority in tbls_init) and the accumulator waits for
 // that stream: with both, the LDS kernel runs at every batch size -- 131k
 // step 37.3 -> 36.1-36.6 ms (profiles/r05_bench_prio_join.json; the two
-// were A/B switches in round 5, TBLS_SIG_PRIO / TBLS_ACC_JOIN).
-// TBLS_ACC_LDS=0 selects the register-resident k_miller_accs (A/B).
+// were A/B switches in round 5, TBLS_SIG_PRIO / TBLS_ACC_JOIN).  Round 6
+// removed the register-resident k_miller_accs and its TBLS_ACC_LDS switch.
 extern "C" __global__ void k_miller_accs_lds(const uint4* __restrict__ lines, const uint8_t* __restrict__ skip, const uint8_t* __restrict__ code_a,
                                              const uint8_t* __restrict__ code_b, uint32_t n, uint32_t per, uint32_t nseg, uint32_t g_pad,
                                              fp12* __restrict__ f_out, uint32_t seg_stride);
 extern "C" __global__ void k_msm_bucket_tree(const g2a* __restrict__ sig_aff, const uint8_t* __restrict__ use, const uint32_t* __restrict__ off,
                                              const uint32_t* __restrict__ idx, g2j* __restrict__ bucket);  // k_sigs.hip
-static bool acc_lds() {
-  static const bool v = !(getenv("TBLS_ACC_LDS") && getenv("TBLS_ACC_LDS")[0] == '0');
-  return v;
-}
 // Bucket-sum batches: when the hash starts.  0: at once (beside the key
 // decompression and the signature checks); 1: after the signature checks;
 // 2: after the whole bucket-sum chain.  Measured at 131,072 sets
 // (profiles/r05_bench_sig_first.json): keys as bytes 36.4-36.7 ms (0) /
 // 37.8-37.9 (1) / 38.5-38.9 (2); keys from the device table 3.61-3.65 /
 // 3.87-3.90 / 3.70-3.74 M sigs/s.  So 1 with the key table (no key
-// decompression beside the signature checks), else 0.  TBLS_SIG_FIRST
-// forces one (A/B).
-static int sig_first(bool key_table) {
-  static const int v = getenv("TBLS_SIG_FIRST") ? atoi(getenv("TBLS_SIG_FIRST")) : -1;
-  return v >= 0 ? v : key_table ? 1 : 0;
-}
+// decompression beside the signature checks), else 0.  (The A/B switch
+// TBLS_SIG_FIRST and order 2 were removed in round 6.)
+static int sig_first(bool key_table) { return key_table ? 1 : 0; }
 extern "C" __global__ void k_set_hash_wave(const uint8_t* __restrict__ msgs, const uint32_t* __restrict__ msg_off,
                                            const uint8_t* __restrict__ dst, uint32_t dlen, uint32_t n, g2a* __restrict__ Q,
                                            uint8_t* __restrict__ skip);  // k_hwave.hip
@@ -621,10 +669,8 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
     hipLaunchKernelGGL(k_msm_bitsum_pairs, dim3(TB_MSM_XPAIRS), dim3(64), 0, sb, (const g2j*)(w + L.msm_sum), c.comb.as<const g1a>(),
                        P + n, Q + n, skip + n);
     if (pp.n_xwave)  // their Miller loops, one wave each, on this stream: f[n_f_main ..)
-      hipLaunchKernelGGL(k_miller_wave, dim3(pp.n_xwave), dim3(64), 0, sb, (const g1a*)P + n,
-                         (const g2a*)Q + n,
-                         (const uint8_t*)skip + n,
-                         (const uint8_t*)(w + L.set_code + n), (const uint8_t*)(w + L.sig_code + n), pp.n_xwave, (fp12*)(w + L.f) + pp.n_f_main());
+      launch_miller_pairs(sb, pp.n_xwave, (const g1a*)P + n, (const g2a*)Q + n, (const uint8_t*)skip + n, (const uint8_t*)(w + L.set_code + n),
+                          (const uint8_t*)(w + L.sig_code + n), (fp12*)(w + L.f) + pp.n_f_main());
   }
   TB_EV(9, sb);
   HIPCHK(hipEventRecord(c.e_join[1], sb));
@@ -668,7 +714,7 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
   // step, profiles/r05_kernel_trace_step.txt).  With key decompression in
   // the batch the hash-first order still measured faster.
   const int sf = sig_first(use_tab);
-  if (late_join && sf) HIPCHK(hipStreamWaitEvent(sh, sf == 2 ? c.e_join[1] : c.e_sig, 0));
+  if (late_join && sf) HIPCHK(hipStreamWaitEvent(sh, c.e_sig, 0));
   TB_EV(6, sh);
   if (n && n <= TB_HASH_WAVE_MAX && coop())  // one 256-thread workgroup per set: coop SSWU chains and cofactor program
     hipLaunchKernelGGL(k_set_hash_coop, dim3(n), dim3(256), 0, sh, b.msgs, b.msg_off, dst, dlen, n, Q, skip, (const uint64_t*)nullptr);
@@ -710,7 +756,7 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
     const uint8_t* cb = w + L.sig_code;
     fp12* f = (fp12*)(w + L.f);
     if (pp.wave) {
-      hipLaunchKernelGGL(k_miller_wave, dim3(np), dim3(64), 0, s, (const g1a*)P, (const g2a*)Q, (const uint8_t*)skip, ca, cb, np, f);
+      launch_miller_pairs(s, np, (const g1a*)P, (const g2a*)Q, (const uint8_t*)skip, ca, cb, f);
     } else {
       // chunks of the main pairs: G2 lines (P and T in LDS), then the Fp12
       // accumulator (segment-major values: segment j of group g at f[j * n_groups + g])
@@ -728,7 +774,7 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
         if (late_join && lo == 0) HIPCHK(hipStreamWaitEvent(s, c.e_join[1], 0));  // the bucket-sum stream first (acc_lds)
         if (pp.seg()) {
           const uint32_t g_pad = (mt + TB_BLOCK - 1) / TB_BLOCK * TB_BLOCK;
-          hipLaunchKernelGGL(acc_lds() ? k_miller_accs_lds : k_miller_accs, dim3(pp.nseg * g_pad / TB_BLOCK), blk, 0, s,
+          hipLaunchKernelGGL(k_miller_accs_lds, dim3(pp.nseg * g_pad / TB_BLOCK), blk, 0, s,
                              (const uint4*)lines,
                              (const uint8_t*)skip + lo,
                              ca + lo, cb + lo, m, pp.per, pp.nseg, g_pad, f + lo / pp.per, pp.n_groups());
@@ -992,6 +1038,7 @@ int verify_on_device(int d, const SET* sets, size_t n, const uint64_t* rand, con
 // ---------------------------------------------------------------------------
 extern "C" __global__ void k_group_test_coop(const fp12* __restrict__ vals, uint32_t stride, uint32_t nseg, const uint32_t* __restrict__ list,
                                              uint8_t* __restrict__ out);  // k_pair.hip
+extern "C" __global__ void k_settle_mask(const uint8_t* __restrict__ set_code, uint32_t n, uint8_t* __restrict__ skip);  // k_pair.hip
 #define TB_SETTLE_FAN 16u                  // sets per group and groups per group of the next level (k_fp12_prod_wave_seg chunk)
 #define TB_SETTLE_MAX (TB_LINE_CHUNK / 2u)  // sets per settle chunk: both pairs of every set in one line chunk
 
@@ -1051,7 +1098,8 @@ static int settle_sets(dev_ctx* c, const ws_layout& L, uint32_t n, uint8_t* ok) 
   fp12 *V = (fp12*)(sw + oV), *A = (fp12*)(sw + oA), *B = (fp12*)(sw + oB);
   hipStream_t s = c->stream;
   const uint32_t g_pad = (n + TB_BLOCK - 1) / TB_BLOCK * TB_BLOCK;
-  hipLaunchKernelGGL(acc_lds() ? k_miller_accs_lds : k_miller_accs, dim3(nseg * g_pad / TB_BLOCK), dim3(TB_BLOCK), 0, s,
+  hipLaunchKernelGGL(k_settle_mask, dim3((n + 255) / 256), dim3(256), 0, s, (const uint8_t*)(w + L.set_code), n, w + L.skip);
+  hipLaunchKernelGGL(k_miller_accs_lds, dim3(nseg * g_pad / TB_BLOCK), dim3(TB_BLOCK), 0, s,
                      (const uint4*)(w + L.lines), (const uint8_t*)(w + L.skip), (const uint8_t*)(w + L.set_code), (const uint8_t*)(w + L.sig_code),
                      2u * n, 2u, nseg, g_pad, V, n);
   hipLaunchKernelGGL(k_fp12_prod_wave_seg, dim3(nA, nseg), dim3(64), 0, s, (const fp12*)V, n, n, nseg, n, F, A, nA);
@@ -1175,6 +1223,14 @@ const std::vector<ncclComm_t>* rccl_comms_locked(const std::vector<int>& devs, i
 // (the caller's caller_device restores).
 int gather_partials(gather_mode mode, const std::vector<int>& devs, int G, const std::vector<uint8_t*>& dpart) {
   dev_ctx* c0 = ctx_for(devs[0]);
+  if (mode == GATHER_RCCL) {  // an RCCL communicator needs G distinct hardware devices (TBLS_INIT_SHARE_DEVICES)
+    uint64_t seen = 0;
+    for (int g = 0; g < G; g++) {
+      const int d = ctx_for(devs[g])->dev;
+      if (d < 64 && ((seen >> d) & 1)) mode = GATHER_PEER;
+      if (d < 64) seen |= 1ull << d;
+    }
+  }
   HIPCHK(hipSetDevice(c0->dev));
   if (c0->recs.ensure((size_t)G * TBLS_PARTIAL_BYTES)) return TBLS_DEVICE_ERROR;
   uint8_t* recv = c0->recs.as<uint8_t>();
@@ -1321,7 +1377,6 @@ bool sk_in_range(const uint8_t sk[32]) {
 // C ABI
 // ===========================================================================
 extern "C" int tbls_init(int n_devices, uint32_t flags) {
-  (void)flags;
   const caller_device keep;
   std::lock_guard<std::mutex> lk(g_mu);
   if (g_inited) return g_ctx.empty() ? TBLS_DEVICE_ERROR : TBLS_SUCCESS;
@@ -1330,10 +1385,14 @@ extern "C" int tbls_init(int n_devices, uint32_t flags) {
     g_inited = true;
     return TBLS_DEVICE_ERROR;
   }
-  if (n_devices > 0 && n_devices < count) count = n_devices;
+  const int hw = count;
+  if ((flags & TBLS_INIT_SHARE_DEVICES) && n_devices > 0 && n_devices <= 32)
+    count = n_devices;  // contexts over the hardware devices round-robin
+  else if (n_devices > 0 && n_devices < count)
+    count = n_devices;
   for (int d = 0; d < count; d++) {
     dev_ctx* c = new dev_ctx();
-    c->dev = d;
+    c->dev = d % hw;
     int prio_lo = 0, prio_hi = 0;
     if (hipSetDevice(d) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->aux[0], hipStreamNonBlocking) != hipSuccess ||
@@ -1412,7 +1471,7 @@ int batch_verify_impl(const SET* sets, size_t n, const uint64_t* rand, int n_gpu
   for (size_t i = 0; i < n; i++)
     if (sets[i].n_pks == 0) return TBLS_BAD_ARGUMENT;
   placed pl;  // the devices and shard cuts (place_plan), counted as busy until we return
-  place_batch(pl, n, [&](size_t i) { return sets[i].n_pks; }, n_gpus, shard_min());
+  place_batch(pl, n, [&](size_t i) { return sets[i].n_pks; }, n_gpus, shard_min(), shard_knee());
   const int G = pl.G;
   std::vector<double> dms(G, 0);
   int rc = TBLS_SUCCESS;
@@ -1488,7 +1547,7 @@ extern "C" int tbls_batch_verify_each(const tbls_set* sets_in, size_t n_in, cons
   const size_t n = sets.size();
   if (n == 0) return TBLS_SUCCESS;
   placed pl;
-  place_batch(pl, n, [&](size_t i) { return sets[i].n_pks; }, n_gpus, shard_min());
+  place_batch(pl, n, [&](size_t i) { return sets[i].n_pks; }, n_gpus, shard_min(), shard_knee());
   const int G = pl.G;
   std::vector<std::unique_lock<std::mutex>> locks;  // ascending device order: no deadlock
   for (int g = 0; g < G; g++) locks.emplace_back(ctx_for(pl.dev[g])->mu);
@@ -1520,6 +1579,17 @@ extern "C" int tbls_batch_verify_each(const tbls_set* sets_in, size_t n_in, cons
     if (!rc) rc = launch_final(*root, root->recs.p, (uint32_t)G, root->stream, ok);
   }
   if (rc) return rc;
+  // the batch pipeline's device time, read before any settle re-records the
+  // shards' events (re-staged settle chunks run shard_launch again)
+  double batch_dev_ms = 0;
+  for (int g = 0; g < G; g++) {
+    dev_ctx* c = ctx_for(pl.dev[g]);
+    float ms = 0;
+    (void)hipSetDevice(c->dev);
+    (void)hipStreamSynchronize(c->stream);
+    (void)hipEventElapsedTime(&ms, c->e_t0, c->e_t1);
+    batch_dev_ms += ms;
+  }
   std::vector<uint8_t> verdict(n, 1);
   if (!*ok) {
     auto settle = [&](int g) {
@@ -1538,14 +1608,7 @@ extern "C" int tbls_batch_verify_each(const tbls_set* sets_in, size_t n_in, cons
   if (n != n_in) *ok = 0;  // a set without keys fails the whole batch as well
   if (t) {
     t->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    t->device_ms = 0;
-    for (int g = 0; g < G; g++) {
-      dev_ctx* c = ctx_for(pl.dev[g]);
-      float ms = 0;
-      (void)hipSetDevice(c->dev);
-      (void)hipEventElapsedTime(&ms, c->e_t0, c->e_t1);
-      t->device_ms += ms;
-    }
+    t->device_ms = batch_dev_ms;  // the batch pass only; settling is in total_ms
     t->n_devices = (uint32_t)G;
   }
   return TBLS_SUCCESS;
@@ -1688,7 +1751,7 @@ extern "C" int tbls_verify_each(const tbls_set* sets, size_t n, int n_gpus, int*
   // one device per chunk, at most nchunks least-loaded devices (place_plan with
   // one-set "chunks"); chunk k runs on pl.dev[k % G], one host thread per device
   placed pl;
-  place_batch(pl, nchunks, [](size_t) { return 0u; }, n_gpus, 1);
+  place_batch(pl, nchunks, [](size_t) { return 0u; }, n_gpus, 1, 0);
   const int G = pl.G;
   std::vector<uint8_t> ok(n, 0);
   std::vector<int> rcs(G, 0);
@@ -2019,18 +2082,19 @@ extern "C" int tbls_dev_batch_stage_profile(int device, const tbls_dev_batch* b,
 }
 
 extern "C" int tbls_place_plan(size_t n, const uint32_t* n_pks, int n_devices, int n_gpus, const int* load, uint32_t rr,
-                               uint32_t shard_min_sets, int* dev_out, size_t* cut_out) {
+                               uint32_t shard_min_sets, uint32_t shard_knee_sets, int* dev_out, size_t* cut_out) {
   if (n_devices < 1 || n_devices > 32 || !dev_out || !cut_out) return -TBLS_BAD_ARGUMENT;
   std::vector<int> dev(n_devices);
   std::vector<size_t> cut(n_devices + 1);
-  const int G = place_plan(n, [&](size_t i) { return n_pks ? n_pks[i] : 1u; }, n_devices, n_gpus, load, rr, shard_min_sets, dev.data(),
-                           cut.data());
+  const int G = place_plan(n, [&](size_t i) { return n_pks ? n_pks[i] : 1u; }, n_devices, n_gpus, load, rr, shard_min_sets, shard_knee_sets,
+                           dev.data(), cut.data());
   for (int k = 0; k < G; k++) dev_out[k] = dev[k];
   for (int k = 0; k <= G; k++) cut_out[k] = cut[k];
   return G;
 }
 
 extern "C" uint32_t tbls_shard_min(void) { return shard_min(); }
+extern "C" uint32_t tbls_shard_knee(void) { return shard_knee(); }
 
 extern "C" int tbls_acc_plan(uint32_t n, uint32_t* per, uint32_t* nseg, int* split) {
   const pair_plan pp(n);

@@ -103,6 +103,33 @@ TB_HD TB_INLINE fp12 fp12_mul_by_line_i(const fp12& f, const fp2& A, const fp2& 
 #define TB_LINE_STEPS 68  // 63 doubling + 5 addition steps of |x| = 0xd201000000010000
 #define TB_LINE_G 18      // 16-byte groups per line (3 Fp2 = 72 words)
 
+// The line tables stream through L2 once (written by the line kernel, read
+// once by the accumulator): with TB_LINE_NT their loads and stores carry the
+// non-temporal hint, so the 2.6 GB per 131k launch does not evict the
+// kernels' own scratch lines (register spills) from L2 -- at one wave per
+// SIMD every scratch reload that misses L2 is exposed in full.
+#ifndef TB_LINE_NT
+#define TB_LINE_NT 1
+#endif
+typedef uint32_t tb_u32x4 __attribute__((ext_vector_type(4)));
+__device__ TB_INLINE uint4 line_ld16(const uint4* p) {
+#if TB_LINE_NT
+  const tb_u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const tb_u32x4*>(p));
+  return make_uint4(v.x, v.y, v.z, v.w);
+#else
+  return *p;
+#endif
+}
+__device__ TB_INLINE void line_st16(uint4* p, const uint4& v) {
+#if TB_LINE_NT
+  tb_u32x4 w;
+  w.x = v.x, w.y = v.y, w.z = v.z, w.w = v.w;
+  __builtin_nontemporal_store(w, reinterpret_cast<tb_u32x4*>(p));
+#else
+  *p = v;
+#endif
+}
+
 namespace {
 __device__ TB_INLINE void line_store(uint4* __restrict__ lines, uint32_t n, uint32_t i, int s, const line3& l) {
   const fp* c[6] = {&l.a.c0, &l.a.c1, &l.b.c0, &l.b.c1, &l.c.c0, &l.c.c1};
@@ -113,7 +140,7 @@ __device__ TB_INLINE void line_store(uint4* __restrict__ lines, uint32_t n, uint
     v.y = c[(w + 1) / 12]->l[(w + 1) % 12];
     v.z = c[(w + 2) / 12]->l[(w + 2) % 12];
     v.w = c[(w + 3) / 12]->l[(w + 3) % 12];
-    lines[(size_t)(s * TB_LINE_G + g) * n + i] = v;
+    line_st16(&lines[(size_t)(s * TB_LINE_G + g) * n + i], v);
   }
 }
 
@@ -122,7 +149,7 @@ __device__ TB_INLINE line3 line_load(const uint4* __restrict__ lines, uint32_t n
   fp* c[6] = {&l.a.c0, &l.a.c1, &l.b.c0, &l.b.c1, &l.c.c0, &l.c.c1};
   const uint4* __restrict__ row = lines + (size_t)(s * TB_LINE_G) * n;  // wave-uniform where s is
   TB_UNROLL for (int g = 0; g < TB_LINE_G; g++) {
-    const uint4 v = row[(uint32_t)(g * n + i)];  // g n + i < TB_LINE_G x TB_LINE_CHUNK < 2^32
+    const uint4 v = line_ld16(&row[(uint32_t)(g * n + i)]);  // g n + i < TB_LINE_G x TB_LINE_CHUNK < 2^32
     const int w = 4 * g;
     c[(w + 0) / 12]->l[(w + 0) % 12] = v.x;
     c[(w + 1) / 12]->l[(w + 1) % 12] = v.y;
@@ -262,56 +289,20 @@ constexpr step_mask DBL_STEPS = miller_dbl_steps();
 
 __device__ TB_INLINE bool step_is_dbl(int s) { return ((s < 64 ? (DBL_STEPS.lo >> s) : (DBL_STEPS.hi >> (s - 64))) & 1ull) != 0; }
 
-// the line (A + B v) + (C v) w as an Fp12
-__device__ TB_INLINE fp12 line_fp12(const line3& l) { return {{l.a, l.b, fp2_zero()}, {fp2_zero(), l.c, fp2_zero()}}; }
 }  // namespace
 
-__device__ TB_INLINE void miller_accs_body(const uint4* __restrict__ lines, const uint8_t* __restrict__ skip,
-                                           const uint8_t* __restrict__ code_a, const uint8_t* __restrict__ code_b, uint32_t n, uint32_t per,
-                                           uint32_t nseg, uint32_t g_pad, fp12* __restrict__ f_out, uint32_t seg_stride) {
-  // segment and group from the block index (g_pad is a multiple of the
-  // block): j, and with it the step counter, is wave-uniform, so a line
-  // load's row base is scalar (round 5: scratch 484 -> 324 B per lane in
-  // k_miller_accs_lds, 544 -> 392 in k_miller_accs)
-  const uint32_t bps = g_pad / TB_BLOCK;
-  const uint32_t j = blockIdx.x / bps, g = (blockIdx.x % bps) * TB_BLOCK + threadIdx.x;
-  const uint32_t G = (n + per - 1) / per;
-  if (j >= nseg || g >= G) return;
-  const int s_lo = (int)(TB_LINE_STEPS * j / nseg), s_hi = (int)(TB_LINE_STEPS * (j + 1) / nseg);
-  // group g owns pairs g, g + G, g + 2G, ...: the lanes of a wave then read
-  // consecutive pairs' lines (one 1 KB transaction per 16-byte group) instead
-  // of pairs `per` apart (a 128-byte line per lane, each line re-fetched per
-  // pair: 24 GB per 131k launch at per = 8, profiles/r03_probe_*)
-  const uint32_t i0 = g;
-  uint32_t usem = 0;
-  for (uint32_t k = 0; k < per; k++) {
-    const uint32_t i = g + k * G;
-    if (i < n && skip[i] == 0 && code_a[i] == 0 && code_b[i] == 0) usem |= 1u << k;
-  }
-  fp12 f = fp12_one();
-  bool fresh = true;  // f == 1
-  // (per <= 32: usem is one bit per owned pair; with every pair valid the
-  // lanes of a wave take the same path)
-  TB_NOUNROLL for (int s = s_lo; s < s_hi; s++) {
-    if (!fresh && step_is_dbl(s)) f = fp12_sqr_i(f);
-    TB_NOUNROLL for (uint32_t k = 0; k < per; k++) {
-      if (!((usem >> k) & 1u)) continue;
-      const line3 l = line_load(lines, n, i0 + k * G, s);
-      if (fresh) {
-        f = line_fp12(l);
-        fresh = false;
-      } else {
-        f = fp12_mul_by_line_i(f, l.a, l.b, l.c);
-      }
-    }
-  }
-  f_out[(size_t)j * seg_stride + g] = fp12_conj(f);
-}
-
+// Lines per f product in k_miller_accs_lds: 1 = two lines multiplied
+// together first (23 Fp2 products per two lines), 2 = the same with the
+// reordered product (fp12_mul_line2_lds_s1), 0 = one sparse product per line
+// (13 per line, fewer live registers).  A/B build switch.
+#ifndef TB_ACC_LINE2
+#define TB_ACC_LINE2 1
+#endif
 
 // ---------------------------------------------------------------------------
 // LDS-resident segmented accumulator (round 5, k_miller_accs_lds).  Same
-// segments, groups and output as miller_accs_body; two changes:
+// segmented plan as k_miller_acc1/2 generalised (segments, groups, output
+// layout); two changes from round 4's register-resident form:
 //  * f lives in LDS (36 uint4 = 576 B per lane, 36,864 B per 64-lane
 //    workgroup, 147 KB per CU at one wave per SIMD): the products read f's
 //    Fp2 coefficients when they use them and write each new coefficient once
@@ -432,6 +423,24 @@ __device__ TB_INLINE void fp12_mul_line_lds(const lds12& F, const line3& l) {
   F.st6(0, fp6_add(t0, fp6_mul_v(t1)));
 }
 
+// The same product ordered so that fewer Fp6 values are register-live
+// (TB_ACC_LINE2 = 2): s = (f0 + f1)(x + y) first; then p0 = f0 x, after which
+// f0's LDS half is dead and takes s - p0; then p1 = f1 y, after which f1's
+// half takes c1 = (s - p0) - p1, and f0's half c0 = p0 + v p1.  Live across a
+// product: at most one Fp6 result (s, then p0) beside the line product.
+__device__ TB_INLINE void fp12_mul_line2_lds_s1(const lds12& F, const line2& L) {
+  const fp6 xy = {L.x.c0, fp2_add(L.x.c1, L.y1), fp2_add(L.x.c2, L.y2)};
+  TB_FENCE();
+  const fp6 s = fp6_mul_g([&](int i) { return fp2_add(F.ld(i), F.ld(3 + i)); }, xy);
+  TB_FENCE();
+  const fp6 p0 = fp6_mul_g([&](int i) { return F.ld(i); }, L.x);
+  F.st6(0, fp6_sub(s, p0));
+  TB_FENCE();
+  const fp6 p1 = fp6_mul_by_12_g([&](int i) { return F.ld(3 + i); }, L.y1, L.y2);
+  F.st6(1, fp6_sub(F.ld6(0), p1));
+  F.st6(0, fp6_add(p0, fp6_mul_v(p1)));
+}
+
 // f <- f * (l1 l2), in LDS (17 products): c0 = f0 x + v (f1 y), c1 = (f0 + f1)(x + y) - f0 x - f1 y
 __device__ TB_INLINE void fp12_mul_line2_lds(const lds12& F, const line2& L) {
   const fp6 p0 = fp6_mul_g([&](int i) { return F.ld(i); }, L.x);
@@ -444,108 +453,58 @@ __device__ TB_INLINE void fp12_mul_line2_lds(const lds12& F, const line2& L) {
 }
 }  // namespace
 
-// The same products with f0 in registers and only f1 in LDS (18,432 B per
-// workgroup, 73,728 B per CU at one wave per SIMD): a CU keeps LDS for a
-// concurrent kernel's workgroup beside four accumulator waves (the bucket-sum
-// pairs' k_miller_wave, 28 KB, runs beside the accumulator on the bucket-sum
-// stream; with all of f in LDS its workgroups pushed 64 accumulator
-// workgroups into a second round: 131k step 38.2 -> 43.9 ms,
-// profiles/r05_bench_acc_lds_ab.json).
-__device__ TB_INLINE const fp2& c6(const fp6& a, int i) { return i == 0 ? a.c0 : i == 1 ? a.c1 : a.c2; }
-
-__device__ TB_INLINE void fp12_sqr_h(fp6& f0, const lds12& F) {
-  const fp6 f1 = F.ld6(1);
-  const fp6 ab = fp6_mul_f(f0, f1);
-  const fp6 b = {fp2_add(f0.c0, fp2_mul_xi(f1.c2)), fp2_add(f0.c1, f1.c0), fp2_add(f0.c2, f1.c1)};  // f0 + v f1
-  const fp6 a = fp6_add_nr(f0, f1);
-  TB_FENCE();
-  const fp6 t = fp6_mul_f(a, b);
-  f0 = fp6_sub(fp6_sub(t, ab), fp6_mul_v(ab));
-  F.st6(1, fp6_add(ab, ab));
-}
-
-__device__ TB_INLINE void fp12_mul_line_h(fp6& f0, const lds12& F, const line3& l) {
-  const fp6 t1 = {fp2_mul_xi(m2(F.ld(5), l.c)), m2(F.ld(3), l.c), m2(F.ld(4), l.c)};
-  const fp6 t0 = fp6_mul_by_01_f(f0, l.a, l.b);
-  const fp6 u = fp6_mul_by_01_g([&](int i) { return fp2_add(c6(f0, i), F.ld(3 + i)); }, l.a, fp2_add_nr(l.b, l.c));
-  F.st6(1, fp6_sub(fp6_sub(u, t0), t1));
-  f0 = fp6_add(t0, fp6_mul_v(t1));
-}
-
-__device__ TB_INLINE void fp12_mul_line2_h(fp6& f0, const lds12& F, const line2& L) {
-  const fp6 p0 = fp6_mul_f(f0, L.x);
-  const fp6 p1 = fp6_mul_by_12_g([&](int i) { return F.ld(3 + i); }, L.y1, L.y2);
-  const fp6 xy = {L.x.c0, fp2_add(L.x.c1, L.y1), fp2_add(L.x.c2, L.y2)};
-  TB_FENCE();
-  const fp6 s = fp6_mul_g([&](int i) { return fp2_add(c6(f0, i), F.ld(3 + i)); }, xy);
-  F.st6(1, fp6_sub(fp6_sub(s, p0), p1));
-  f0 = fp6_add(p0, fp6_mul_v(p1));
-}
-
-template <bool HALF>
 __device__ TB_INLINE void miller_accs_lds_body(uint4* __restrict__ Fsh, const uint4* __restrict__ lines, const uint8_t* __restrict__ skip,
                                                const uint8_t* __restrict__ code_a, const uint8_t* __restrict__ code_b, uint32_t n,
                                                uint32_t per, uint32_t nseg, uint32_t g_pad, fp12* __restrict__ f_out, uint32_t seg_stride) {
   // segment and group from the block index (g_pad is a multiple of the
   // block): j, and with it the step counter, is wave-uniform, so a line
-  // load's row base is scalar (round 5: scratch 484 -> 324 B per lane in
-  // k_miller_accs_lds, 544 -> 392 in k_miller_accs)
+  // load's row base is scalar (round 5: scratch 484 -> 324 B per lane)
   const uint32_t bps = g_pad / TB_BLOCK;
   const uint32_t j = blockIdx.x / bps, g = (blockIdx.x % bps) * TB_BLOCK + threadIdx.x;
   const uint32_t G = (n + per - 1) / per;
   if (j >= nseg || g >= G) return;
   const int s_lo = (int)(TB_LINE_STEPS * j / nseg), s_hi = (int)(TB_LINE_STEPS * (j + 1) / nseg);
-  const lds12 F{Fsh + threadIdx.x, HALF ? 3 : 0};
-  fp6 f0;  // HALF: f0 in registers
-  uint32_t usem = 0;  // group g owns pairs g, g + G, ... (coalesced line reads, as miller_accs_body)
+  const lds12 F{Fsh + threadIdx.x, 0};
+  // group g owns pairs g, g + G, g + 2G, ...: the lanes of a wave then read
+  // consecutive pairs' lines (one 1 KB transaction per 16-byte group) instead
+  // of pairs `per` apart (a 128-byte line per lane, each line re-fetched per
+  // pair: 24 GB per 131k launch at per = 8, profiles/r03_probe_*)
+  uint32_t usem = 0;  // per <= 32: one bit per owned pair
   for (uint32_t k = 0; k < per; k++) {
     const uint32_t i = g + k * G;
     if (i < n && skip[i] == 0 && code_a[i] == 0 && code_b[i] == 0) usem |= 1u << k;
   }
   bool fresh = true;  // f == 1 (not yet written)
   TB_NOUNROLL for (int s = s_lo; s < s_hi; s++) {
-    if (!fresh && step_is_dbl(s)) {
-      if (HALF)
-        fp12_sqr_h(f0, F);
-      else
-        fp12_sqr_lds(F);
-    }
+    if (!fresh && step_is_dbl(s)) fp12_sqr_lds(F);
     uint32_t m = usem;
     TB_NOUNROLL while (m) {
       const uint32_t k1 = __builtin_ctz(m);
       m &= m - 1;
       const line3 l1 = line_load(lines, n, g + k1 * G, s);
-      if (m) {  // two lines: their product first
+      if (TB_ACC_LINE2 && m) {  // two lines: their product first
         const uint32_t k2 = __builtin_ctz(m);
         m &= m - 1;
         const line2 L = line_mul(l1, line_load(lines, n, g + k2 * G, s));
         if (fresh) {
-          if (HALF)
-            f0 = L.x;
-          else
-            F.st6(0, L.x);
+          F.st6(0, L.x);
           F.st6(1, {fp2_zero(), L.y1, L.y2});
           fresh = false;
-        } else if (HALF) {
-          fp12_mul_line2_h(f0, F, L);
+        } else if (TB_ACC_LINE2 == 2) {
+          fp12_mul_line2_lds_s1(F, L);
         } else {
           fp12_mul_line2_lds(F, L);
         }
       } else if (fresh) {
-        if (HALF)
-          f0 = {l1.a, l1.b, fp2_zero()};
-        else
-          F.st6(0, {l1.a, l1.b, fp2_zero()});
+        F.st6(0, {l1.a, l1.b, fp2_zero()});
         F.st6(1, {fp2_zero(), l1.c, fp2_zero()});
         fresh = false;
-      } else if (HALF) {
-        fp12_mul_line_h(f0, F, l1);
       } else {
         fp12_mul_line_lds(F, l1);
       }
     }
   }
-  fp12 f = fresh ? fp12_one() : fp12{HALF ? f0 : F.ld6(0), F.ld6(1)};
+  fp12 f = fresh ? fp12_one() : fp12{F.ld6(0), F.ld6(1)};
   f_out[(size_t)j * seg_stride + g] = fp12_conj(f);
 }
 

@@ -174,8 +174,10 @@ _SIGS = {
     ),
     "tbls_acc_plan": (ctypes.c_int, [ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_int)]),
     "tbls_place_plan": (ctypes.c_int, [ctypes.c_size_t, ctypes.POINTER(ctypes.c_uint32), ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
-                                       ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_size_t)]),
+                                       ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_int),
+                                       ctypes.POINTER(ctypes.c_size_t)]),
     "tbls_shard_min": (ctypes.c_uint32, []),
+    "tbls_shard_knee": (ctypes.c_uint32, []),
     "tbls_sk_to_pk_many": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p]),
     "tbls_sign_many": (
         ctypes.c_int,
@@ -287,17 +289,19 @@ def acc_plan(n_sets):
     return per.value, nseg.value, split.value
 
 
-def place_plan(n, n_pks=None, n_devices=8, n_gpus=0, load=None, rr=0, shard_min=None):
+def place_plan(n, n_pks=None, n_devices=8, n_gpus=0, load=None, rr=0, shard_min=None, shard_knee=None):
     """The library's device placement of a batch (tbls_place_plan; no device
     needed): returns (devices, cuts) -- device devices[k] verifies sets
-    [cuts[k], cuts[k+1])."""
+    [cuts[k], cuts[k+1]).  shard_knee: the shard floor on an idle node
+    (default the library's; 0 = none)."""
     L = load_library() if _lib is None else _lib
     pk = (ctypes.c_uint32 * n)(*n_pks) if n_pks is not None else None
     ld = (ctypes.c_int * n_devices)(*load) if load is not None else None
     dev = (ctypes.c_int * n_devices)()
     cut = (ctypes.c_size_t * (n_devices + 1))()
     smin = L.tbls_shard_min() if shard_min is None else shard_min
-    G = L.tbls_place_plan(n, pk, n_devices, n_gpus, ld, rr, smin, dev, cut)
+    knee = L.tbls_shard_knee() if shard_knee is None else shard_knee
+    G = L.tbls_place_plan(n, pk, n_devices, n_gpus, ld, rr, smin, knee, dev, cut)
     if G < 1:
         raise NativeError(-G, "tbls_place_plan")
     return list(dev[:G]), list(cut[: G + 1])

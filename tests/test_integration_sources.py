@@ -52,3 +52,25 @@ def test_spi_classes_present():
         src = _read(J, "bls", "impl", "hip", f + ".java")
         assert re.search(r"\b(class|interface|record) " + f + r"\b", src)
     assert "implements KZG" in _read(J, "kzg", "HipKZG.java")
+
+
+def test_gpu_service_source_wired_to_batch_verify_each():
+    """the Java half of the GPU-aware service is a
+    committed source (not an INTEGRATION.md snippet): the service's
+    batchVerifySignatures makes one HipBatchVerifier.batchVerifyEach call,
+    sizes its workers to the device count and asks for one device while tasks
+    wait; HipBatchVerifier reaches the C ABI through the TekuBlsHip native
+    that the JNI glue binds to tbls_batch_verify_each."""
+    svc = _read(J, "statetransition", "validation", "signatures", "HipAggregatingSignatureVerificationService.java")
+    assert re.search(r"class HipAggregatingSignatureVerificationService extends SignatureVerificationService\b", svc)
+    body = svc[svc.index("void batchVerifySignatures("):]
+    assert body.count("HipBatchVerifier.batchVerifyEach(") == 1
+    code = svc[svc.index("public class"):]
+    assert "BLS.batchVerify" not in code and "splitTasks" not in code  # no halving fallback
+    assert "this.numThreads = HipBatchVerifier.deviceCount();" in svc
+    assert "queue.isEmpty() ? 0 : 1" in svc
+    ver = _read(J, "bls", "impl", "hip", "HipBatchVerifier.java")
+    assert "public static boolean batchVerifyEach(" in ver and "TekuBlsHip.batchVerifyEach(" in ver
+    assert "batchVerifyEach" in _natives(_read(J, "bls", "impl", "hip", "TekuBlsHip.java"))
+    c = _read(N, "tekubls_jni.c")
+    assert "batchVerifyEach" in _jni(c) and "tbls_batch_verify_each(" in c

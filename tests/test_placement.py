@@ -4,7 +4,10 @@ only into shards of at least shard_min = 32,768 sets (where one device's
 partial stops being a latency chain, profiles/r04_stage_sweep_final.json);
 with no idle device it goes whole to the least-loaded one, so concurrent
 callers land on different devices (SURVEY.md 8(e);
-AggregatingSignatureVerificationService.java:121-132, 202-205)."""
+AggregatingSignatureVerificationService.java:121-132, 202-205).  On an idle
+node (every device idle) a lone batch shards down to the latency knee of
+4,096 sets per device; a service with more batches
+waiting passes n_gpus = 1 (teku_amd/service.py)."""
 
 import random
 
@@ -13,10 +16,12 @@ import pytest
 from teku_amd import dist, native
 
 SMIN = 32768
+KNEE = 4096
 
 
 def test_shard_min_default():
     assert native.load_library().tbls_shard_min() == SMIN
+    assert native.load_library().tbls_shard_knee() == KNEE
 
 
 @pytest.mark.parametrize("D", [1, 2, 4, 8])
@@ -28,20 +33,47 @@ def test_config1_batch_stays_on_one_device(D):
 
 @pytest.mark.parametrize("D", [1, 2, 4, 8])
 def test_config4_batch_takes_one_device(D):
-    """16,384 sets is below shard_min: one device, whatever the node's load."""
+    """16,384 sets is below shard_min: one device when any device is busy
+    (here device (rr + 1) % D holds a batch), or with no knee."""
     for rr in range(D):
-        devs, cuts = native.place_plan(16384, n_devices=D, rr=rr, shard_min=SMIN)
+        devs, cuts = native.place_plan(16384, n_devices=D, rr=rr, shard_min=SMIN, shard_knee=0)
         assert devs == [rr % D] and cuts == [0, 16384]
+        if D > 1:
+            load = [0] * D
+            load[(rr + 1) % D] = 1
+            devs, cuts = native.place_plan(16384, n_devices=D, load=load, rr=rr, shard_min=SMIN)
+            assert devs == [rr % D] and cuts == [0, 16384]
+
+
+@pytest.mark.parametrize("D,G", [(1, 1), (2, 2), (4, 4), (8, 4)])
+def test_lone_config4_batch_on_idle_node_shards_to_the_knee(D, G):
+    """a lone 16,384-set batch on an idle node runs as
+    shards of 4,096 sets (modelled device latency 8.6 -> 5.8 ms plus the 0.8 ms
+    final exponentiation, profiles/r04_stage_sweep_final.json)."""
+    devs, cuts = native.place_plan(16384, n_devices=D, shard_min=SMIN)
+    assert len(devs) == G and cuts[0] == 0 and cuts[-1] == 16384
+    assert all(cuts[k + 1] - cuts[k] >= KNEE for k in range(G))
+    # 8 idle devices, but the caller allows one (a service with batches waiting)
+    devs, cuts = native.place_plan(16384, n_devices=D, n_gpus=1, shard_min=SMIN)
+    assert len(devs) == 1 and cuts == [0, 16384]
+
+
+@pytest.mark.parametrize("n,G", [(128, 1), (8191, 1), (8192, 2), (12288, 3), (16384, 4), (32768, 8), (131072, 8)])
+def test_idle_node_knee_counts(n, G):
+    devs, cuts = native.place_plan(n, n_devices=8, shard_min=SMIN)
+    assert len(devs) == G and cuts[-1] == n
 
 
 def test_eight_concurrent_config4_batches_get_eight_devices():
     """8 simulated devices, 8 service workers each
     placing a 16,384-set batch while the earlier ones are still in flight ->
-    8 distinct single devices (round 4: every batch took all 8)."""
+    8 distinct single devices (round 4: every batch took all 8).  The first
+    seven see more batches waiting in the service queue and pass n_gpus = 1;
+    the last finds the queue empty (n_gpus = 0) but the node busy."""
     load = [0] * 8
     got = []
     for w in range(8):
-        devs, cuts = native.place_plan(16384, n_devices=8, load=load, rr=3 * w + 1, shard_min=SMIN)
+        devs, cuts = native.place_plan(16384, n_devices=8, n_gpus=1 if w < 7 else 0, load=load, rr=3 * w + 1, shard_min=SMIN)
         assert len(devs) == 1 and cuts == [0, 16384]
         load[devs[0]] += 1
         got.append(devs[0])
@@ -54,9 +86,10 @@ def test_eight_concurrent_config4_batches_get_eight_devices():
 @pytest.mark.parametrize("n,D,G", [(32767, 8, 1), (65535, 8, 1), (65536, 8, 2), (131072, 8, 4), (131072, 4, 4), (131072, 2, 2),
                                    (262144, 8, 8), (1048576, 8, 8), (5, 8, 1)])
 def test_device_count_follows_shard_min(n, D, G):
-    """A lone batch on an idle node: 131,072 sets still shards (4 x 32,768),
-    config 5's 1,048,576 sets use all 8 devices."""
-    devs, cuts = native.place_plan(n, n_devices=D, shard_min=SMIN)
+    """The shard_min rule alone (no knee, as on a node with a device busy):
+    131,072 sets still shard (4 x 32,768), config 5's 1,048,576 sets use all 8
+    devices."""
+    devs, cuts = native.place_plan(n, n_devices=D, shard_min=SMIN, shard_knee=0)
     assert len(devs) == G and cuts[0] == 0 and cuts[-1] == n
     assert all(cuts[k] <= cuts[k + 1] for k in range(G))
     if G > 1:
@@ -77,6 +110,8 @@ def test_sharding_uses_idle_devices_only():
 def test_n_gpus_caps_and_shard_min_zero():
     devs, _ = native.place_plan(1048576, n_devices=8, n_gpus=2, shard_min=SMIN)
     assert len(devs) == 2
+    devs, _ = native.place_plan(16384, n_devices=8, n_gpus=2, shard_min=SMIN)
+    assert len(devs) == 2  # the knee on an idle node, capped by n_gpus
     devs, cuts = native.place_plan(6, n_devices=8, shard_min=0)
     assert len(devs) == 6 and cuts == list(range(7))  # never more devices than sets
     devs, _ = native.place_plan(100, n_devices=4, shard_min=0)
@@ -124,7 +159,7 @@ def test_bad_arguments():
 
     dev = (ctypes.c_int * 1)()
     cut = (ctypes.c_size_t * 2)()
-    assert L.tbls_place_plan(10, None, 0, 0, None, 0, 2048, dev, cut) < 0
+    assert L.tbls_place_plan(10, None, 0, 0, None, 0, 2048, 0, dev, cut) < 0
 
 
 @pytest.mark.parametrize("n,plan", [(131072, (16, 8)), (16384, (8, 16)), (1048576, (16, 4)), (3000, (2, 16))])
