@@ -1394,7 +1394,7 @@ extern "C" int tbls_init(int n_devices, uint32_t flags) {
     dev_ctx* c = new dev_ctx();
     c->dev = d % hw;
     int prio_lo = 0, prio_hi = 0;
-    if (hipSetDevice(d) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+    if (hipSetDevice(c->dev) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->aux[0], hipStreamNonBlocking) != hipSuccess ||
         hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess ||
         hipStreamCreateWithPriority(&c->aux[1], hipStreamNonBlocking, prio_hi) != hipSuccess ||
@@ -1416,6 +1416,7 @@ extern "C" int tbls_init(int n_devices, uint32_t flags) {
     }
     g_ctx.push_back(c);
   }
+  (void)hipGetLastError();  // a context that failed to set up leaves no sticky error for later calls' checks
   g_inited = true;
   return g_ctx.empty() ? TBLS_DEVICE_ERROR : TBLS_SUCCESS;
 }

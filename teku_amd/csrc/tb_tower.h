@@ -27,14 +27,135 @@ struct fp12 {
 TB_HD TB_INLINE fp2 fp2_zero() { return {fp_zero(), fp_zero()}; }
 TB_HD TB_INLINE fp2 fp2_one() { return {fp_one(), fp_zero()}; }
 TB_HD TB_INLINE fp2 fp2_from_const(const uint32_t (&c)[2][12]) { return {fp_from_const(c[0]), fp_from_const(c[1])}; }
-TB_HD TB_INLINE fp2 fp2_add(const fp2& a, const fp2& b) { return {fp_add(a.c0, b.c0), fp_add(a.c1, b.c1)}; }
-TB_HD TB_INLINE fp2 fp2_sub(const fp2& a, const fp2& b) { return {fp_sub(a.c0, b.c0), fp_sub(a.c1, b.c1)}; }
+
+// ---------------------------------------------------------------------------
+// Interleaved carry chains (TB_ASM_CARRY, device code).  On gfx950 a VALU
+// that reads an SGPR carry written by the previous VALU needs two wait
+// states, so a lone 12-limb chain compiles to v_addc / s_nop 1 / v_addc / ...
+// (10.2 cycles per link at one wave per SIMD against 5.8 with four chains
+// interleaved, tools/microbench/carry_chain.hip), and in the register-bound
+// kernels the scheduler keeps each Fp addition's chains apart.  Here an Fp2
+// addition / subtraction runs its four chains -- both coordinates' sum and
+// their conditional 2p correction, the latter one limb behind -- as one
+// interleaved instruction stream with a carry SGPR pair per chain, and the
+// 2p constants as VGPR operands (a VALU reading an SGPR source right after a
+// VALU SGPR write is a hazard too).  Same results as the C forms below
+// (fp_add / fp_sub), which the host build and TB_ASM_CARRY=0 use.
+// ---------------------------------------------------------------------------
+#ifndef TB_ASM_CARRY
+#define TB_ASM_CARRY 1
+#endif
+#if TB_ASM_CARRY && defined(__HIP_DEVICE_COMPILE__)
+#define TB_CC_ADD0(r, c, a, b) asm volatile("v_add_co_u32 %0, %1, %2, %3" : "=v"(r), "=s"(c) : "v"(a), "v"(b))
+#define TB_CC_ADDC(r, c, a, b) asm volatile("v_addc_co_u32 %0, %1, %2, %3, %1" : "=v"(r), "+s"(c) : "v"(a), "v"(b))
+#define TB_CC_SUB0(r, c, a, b) asm volatile("v_sub_co_u32 %0, %1, %2, %3" : "=v"(r), "=s"(c) : "v"(a), "v"(b))
+#define TB_CC_SUBB(r, c, a, b) asm volatile("v_subb_co_u32 %0, %1, %2, %3, %1" : "=v"(r), "+s"(c) : "v"(a), "v"(b))
+#define TB_CC_SEL(r, f, t, c) asm volatile("v_cndmask_b32 %0, %1, %2, %3" : "=v"(r) : "v"(f), "v"(t), "s"(c))
+
+// r0 = a0 + b0 mod 2p, r1 = a1 + b1 mod 2p (inputs [0, 2p), outputs [0, 2p))
+__device__ TB_INLINE void cc_add2(fp& r0, fp& r1, const fp& a0, const fp& b0, const fp& a1, const fp& b1) {
+  fp s0, s1, d0, d1;
+  uint64_t c0, c1, e0, e1;
+  TB_CC_ADD0(s0.l[0], c0, a0.l[0], b0.l[0]);
+  TB_CC_ADD0(s1.l[0], c1, a1.l[0], b1.l[0]);
+  TB_CC_SUB0(d0.l[0], e0, s0.l[0], P2_MOD[0]);
+  TB_CC_SUB0(d1.l[0], e1, s1.l[0], P2_MOD[0]);
+  TB_UNROLL for (int i = 1; i < 12; i++) {
+    TB_CC_ADDC(s0.l[i], c0, a0.l[i], b0.l[i]);
+    TB_CC_ADDC(s1.l[i], c1, a1.l[i], b1.l[i]);
+    TB_CC_SUBB(d0.l[i], e0, s0.l[i], P2_MOD[i]);
+    TB_CC_SUBB(d1.l[i], e1, s1.l[i], P2_MOD[i]);
+  }
+  // borrow out: s < 2p, keep s
+  TB_UNROLL for (int i = 0; i < 12; i++) TB_CC_SEL(r0.l[i], d0.l[i], s0.l[i], e0);
+  TB_UNROLL for (int i = 0; i < 12; i++) TB_CC_SEL(r1.l[i], d1.l[i], s1.l[i], e1);
+}
+
+// r0 = a0 - b0 mod 2p, r1 = a1 - b1 mod 2p: the differences and the
+// differences + 2p side by side, selected by the borrow
+__device__ TB_INLINE void cc_sub2(fp& r0, fp& r1, const fp& a0, const fp& b0, const fp& a1, const fp& b1) {
+  fp t0, t1, u0, u1;
+  uint64_t c0, c1, e0, e1;
+  TB_CC_SUB0(t0.l[0], c0, a0.l[0], b0.l[0]);
+  TB_CC_SUB0(t1.l[0], c1, a1.l[0], b1.l[0]);
+  TB_CC_ADD0(u0.l[0], e0, t0.l[0], P2_MOD[0]);
+  TB_CC_ADD0(u1.l[0], e1, t1.l[0], P2_MOD[0]);
+  TB_UNROLL for (int i = 1; i < 12; i++) {
+    TB_CC_SUBB(t0.l[i], c0, a0.l[i], b0.l[i]);
+    TB_CC_SUBB(t1.l[i], c1, a1.l[i], b1.l[i]);
+    TB_CC_ADDC(u0.l[i], e0, t0.l[i], P2_MOD[i]);
+    TB_CC_ADDC(u1.l[i], e1, t1.l[i], P2_MOD[i]);
+  }
+  // borrow out of a - b: the difference is negative, take it + 2p
+  TB_UNROLL for (int i = 0; i < 12; i++) TB_CC_SEL(r0.l[i], t0.l[i], u0.l[i], c0);
+  TB_UNROLL for (int i = 0; i < 12; i++) TB_CC_SEL(r1.l[i], t1.l[i], u1.l[i], c1);
+}
+
+// (a - b mod 2p, a + b mod 2p): xi (c0 + c1 u) = (c0 - c1) + (c0 + c1) u, four chains
+__device__ TB_INLINE void cc_subadd(fp& rs, fp& ra, const fp& a, const fp& b) {
+  fp t, u, s, d;
+  uint64_t ct, cu, cs, cd;
+  TB_CC_SUB0(t.l[0], ct, a.l[0], b.l[0]);
+  TB_CC_ADD0(s.l[0], cs, a.l[0], b.l[0]);
+  TB_CC_ADD0(u.l[0], cu, t.l[0], P2_MOD[0]);
+  TB_CC_SUB0(d.l[0], cd, s.l[0], P2_MOD[0]);
+  TB_UNROLL for (int i = 1; i < 12; i++) {
+    TB_CC_SUBB(t.l[i], ct, a.l[i], b.l[i]);
+    TB_CC_ADDC(s.l[i], cs, a.l[i], b.l[i]);
+    TB_CC_ADDC(u.l[i], cu, t.l[i], P2_MOD[i]);
+    TB_CC_SUBB(d.l[i], cd, s.l[i], P2_MOD[i]);
+  }
+  TB_UNROLL for (int i = 0; i < 12; i++) TB_CC_SEL(rs.l[i], t.l[i], u.l[i], ct);
+  TB_UNROLL for (int i = 0; i < 12; i++) TB_CC_SEL(ra.l[i], d.l[i], s.l[i], cd);
+}
+
+// a0 + b0, a1 + b1 without reduction (product operands): two chains
+__device__ TB_INLINE void cc_add2_nr(fp& r0, fp& r1, const fp& a0, const fp& b0, const fp& a1, const fp& b1) {
+  uint64_t c0, c1;
+  TB_CC_ADD0(r0.l[0], c0, a0.l[0], b0.l[0]);
+  TB_CC_ADD0(r1.l[0], c1, a1.l[0], b1.l[0]);
+  TB_UNROLL for (int i = 1; i < 12; i++) {
+    TB_CC_ADDC(r0.l[i], c0, a0.l[i], b0.l[i]);
+    TB_CC_ADDC(r1.l[i], c1, a1.l[i], b1.l[i]);
+  }
+}
+#define TB_CC_ON 1
+#else
+#define TB_CC_ON 0
+#endif
+
+TB_HD TB_INLINE fp2 fp2_add(const fp2& a, const fp2& b) {
+#if TB_CC_ON
+  fp2 r;
+  cc_add2(r.c0, r.c1, a.c0, b.c0, a.c1, b.c1);
+  return r;
+#else
+  return {fp_add(a.c0, b.c0), fp_add(a.c1, b.c1)};
+#endif
+}
+TB_HD TB_INLINE fp2 fp2_sub(const fp2& a, const fp2& b) {
+#if TB_CC_ON
+  fp2 r;
+  cc_sub2(r.c0, r.c1, a.c0, b.c0, a.c1, b.c1);
+  return r;
+#else
+  return {fp_sub(a.c0, b.c0), fp_sub(a.c1, b.c1)};
+#endif
+}
 // a + b without the reduction (< 4p for reduced a, b): only as an operand of
 // a product, which takes any coordinates < 2^383 (fp2_mul_lazy, fp2_sqr,
 // mont29) -- the Karatsuba pre-sums
-TB_HD TB_INLINE fp2 fp2_add_nr(const fp2& a, const fp2& b) { return {fp_add_nr(a.c0, b.c0), fp_add_nr(a.c1, b.c1)}; }
-TB_HD TB_INLINE fp2 fp2_dbl(const fp2& a) { return {fp_dbl(a.c0), fp_dbl(a.c1)}; }
-TB_HD TB_INLINE fp2 fp2_neg(const fp2& a) { return {fp_neg(a.c0), fp_neg(a.c1)}; }
+TB_HD TB_INLINE fp2 fp2_add_nr(const fp2& a, const fp2& b) {
+#if TB_CC_ON
+  fp2 r;
+  cc_add2_nr(r.c0, r.c1, a.c0, b.c0, a.c1, b.c1);
+  return r;
+#else
+  return {fp_add_nr(a.c0, b.c0), fp_add_nr(a.c1, b.c1)};
+#endif
+}
+TB_HD TB_INLINE fp2 fp2_dbl(const fp2& a) { return fp2_add(a, a); }
+TB_HD TB_INLINE fp2 fp2_neg(const fp2& a) { return fp2_sub(fp2_zero(), a); }
 TB_HD TB_INLINE fp2 fp2_conj(const fp2& a) { return {a.c0, fp_neg(a.c1)}; }
 TB_HD TB_INLINE bool fp2_is_zero(const fp2& a) { return fp_is_zero(a.c0) && fp_is_zero(a.c1); }
 TB_HD TB_INLINE bool fp2_eq(const fp2& a, const fp2& b) { return fp_eq(a.c0, b.c0) && fp_eq(a.c1, b.c1); }
@@ -195,7 +316,15 @@ TB_HD TB_INLINE fp2 fp2_sqr(fp2 a) {
 }
 
 // multiply by xi = 1 + u
-TB_HD TB_INLINE fp2 fp2_mul_xi(const fp2& a) { return {fp_sub(a.c0, a.c1), fp_add(a.c0, a.c1)}; }
+TB_HD TB_INLINE fp2 fp2_mul_xi(const fp2& a) {
+#if TB_CC_ON
+  fp2 r;
+  cc_subadd(r.c0, r.c1, a.c0, a.c1);
+  return r;
+#else
+  return {fp_sub(a.c0, a.c1), fp_add(a.c0, a.c1)};
+#endif
+}
 
 TB_HD TB_NOINLINE fp2 fp2_inv(const fp2& a) {
   fp n = fp_add(fp_sqr(a.c0), fp_sqr(a.c1));

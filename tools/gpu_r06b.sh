@@ -20,5 +20,11 @@ if [ -n "$KZG" ]; then
     timeout -k 10 300 python tools/kzg_order_probe.py $o 30 >> $O/kzg_order_$TAG.log 2>&1 || exit $?
     tail -1 $O/kzg_order_$TAG.log
   done
+  for V in $KZGVARS; do
+    for o in bls_first kzg_first; do
+      TBLS_LIB=$V timeout -k 10 300 python tools/kzg_order_probe.py $o 30 >> $O/kzg_order_$TAG.log 2>&1 || exit $?
+      tail -1 $O/kzg_order_$TAG.log
+    done
+  done
 fi
 echo done
