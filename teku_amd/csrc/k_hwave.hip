@@ -161,67 +161,3 @@ extern "C" __global__ void __launch_bounds__(256)
     }
   }
 }
-
-// ---------------------------------------------------------------------------
-// Miller loop on coop rows (round 6, the latency path): the level program of
-// k_miller_wave (tb_miller_prog.h, tools/gen_miller_prog.py: 148 levels, up
-// to 53 Fp products per level) through the coop level interpreter
-// (tb_cprog.h crow::level), 16 rows of a 256-thread workgroup, each row
-// running up to 4 of a level's products as 16-lane coop products (~1k cycles
-// each instead of one lane's ~7k).  One pair per workgroup; same Miller value
-// as k_miller_wave modulo p (conj(f) up to the program's factor in Fp, which
-// the final exponentiation removes).  Bounds: the program's operands sum at
-// most 147 |coef| slots (|v| < 2^390 with slots below 1.6 p after
-// creduce64 and the inputs below 2p), its outputs at most 38 (24 terms).
-// ---------------------------------------------------------------------------
-#include "tb_miller_prog.h"
-
-struct mcoop_lds {
-  cdig S[MP_NSLOT];
-  uint16_t tab[MP_TAB_N];
-  crow::rowbuf rb[12];
-};
-
-extern "C" __global__ void __launch_bounds__(256)
-    k_miller_coop(const g1a* __restrict__ P, const g2a* __restrict__ Q, const uint8_t* __restrict__ skip,
-                  const uint8_t* __restrict__ code_a, const uint8_t* __restrict__ code_b, uint32_t n, fp12* __restrict__ f) {
-  __shared__ mcoop_lds L;
-  const uint32_t i = blockIdx.x;
-  if (i >= n) return;
-  tb_latency_prio();
-  fp* out = reinterpret_cast<fp*>(f + i);
-  if (skip[i] != 0 || code_a[i] != 0 || code_b[i] != 0) {
-    if (threadIdx.x < 12) out[threadIdx.x] = threadIdx.x == 0 ? fp_one() : fp_zero();
-    return;
-  }
-  const coop::cctx K = coop::cctx_load();
-  const int g = crow::row(), d = crow::dig();
-  for (int j = threadIdx.x; j < MP_TAB_N; j += blockDim.x) L.tab[j] = MP_TAB[j];
-  for (int j = threadIdx.x; j < MP_NSLOT * 16; j += blockDim.x) (&L.S[0][0])[j] = 0;
-  __syncthreads();
-  if (g < 12) {  // the inputs: f = 1, T = (Q.x, Q.y, 1), Q, P
-    const uint32_t* w;
-    int slot;
-    switch (g) {
-      case 0: w = R1, slot = MP_S_F0; break;
-      case 1: w = Q[i].x.c0.l, slot = MP_S_X0; break;
-      case 2: w = Q[i].x.c1.l, slot = MP_S_X1; break;
-      case 3: w = Q[i].y.c0.l, slot = MP_S_Y0; break;
-      case 4: w = Q[i].y.c1.l, slot = MP_S_Y1; break;
-      case 5: w = R1, slot = MP_S_Z0; break;
-      case 6: w = Q[i].x.c0.l, slot = MP_S_QX0; break;
-      case 7: w = Q[i].x.c1.l, slot = MP_S_QX1; break;
-      case 8: w = Q[i].y.c0.l, slot = MP_S_QY0; break;
-      case 9: w = Q[i].y.c1.l, slot = MP_S_QY1; break;
-      case 10: w = P[i].x.l, slot = MP_S_PX; break;
-      default: w = P[i].y.l, slot = MP_S_PY; break;
-    }
-    L.S[slot][d] = coop::cfrom_words(w);
-  }
-  __syncthreads();
-  for (int k = 0; k < MP_NLEVEL; k++) crow::level<4, 2, MP_AMAX, MP_BMAX, MP_QMAX * MP_OMAX>(L.S, L.tab, MP_TYPE_OFF[MP_SEQ[k]], K);
-  if (g < 12) {  // conj(f): the w-odd half (coordinates 6..11) negated
-    const fp v = crow::to_fp(L.S[MP_S_F0 + g][d], L.rb[g].d, &L.rb[g].f);
-    if (d == 0) out[g] = g >= 6 ? fp_neg(v) : v;
-  }
-}

@@ -23,7 +23,7 @@
 //                     - [sum r^i y_i] G1   (B is the spec's C_minus_y_lincomb +
 //                     proof_z_lincomb, with the y-terms merged into one
 //                     generator multiple)
-//   k_kzg_pair_sums   tree sums of A and B; then the BLS path's k_miller_coop
+//   k_kzg_pair_sums   tree sums of A and B; then the BLS path's k_miller_wave
 //                     (one wave per pair) and k_final_verify_wave check
 //                     e(A, [tau]_2) e(-B, [1]_2) == 1
 // Prover side (blob_to_kzg_commitment, compute_kzg_proof_impl):

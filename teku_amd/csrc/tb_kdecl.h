@@ -89,7 +89,6 @@ extern "C" __global__ void k_fp12_prod_wave_seg(const fp12* __restrict__ in, uin
 extern "C" __global__ void k_fp12_seg_combine_coop(const fp12* __restrict__ vals, uint32_t nseg, uint32_t dpack, fp12* __restrict__ out);
 #define TB_LINE_BYTES_PER_PAIR (68u * 288u)  // k_miller_lines output per pair
 extern "C" __global__ void k_miller_wave(const g1a* __restrict__ P, const g2a* __restrict__ Q, const uint8_t* __restrict__ skip, const uint8_t* __restrict__ code_a, const uint8_t* __restrict__ code_b, uint32_t n, fp12* __restrict__ f);
-extern "C" __global__ void k_miller_coop(const g1a* __restrict__ P, const g2a* __restrict__ Q, const uint8_t* __restrict__ skip, const uint8_t* __restrict__ code_a, const uint8_t* __restrict__ code_b, uint32_t n, fp12* __restrict__ f);  // k_hwave.hip
 extern "C" __global__ void k_fp12_one(fp12* __restrict__ f);
 extern "C" __global__ void k_fp12_prod_wave(const fp12* __restrict__ in, uint32_t n, uint32_t chunk, fp12* __restrict__ out);
 extern "C" __global__ void k_final_verify_wave(const fp12* __restrict__ f, uint32_t g, const uint32_t* __restrict__ n_bad, int* __restrict__ result);

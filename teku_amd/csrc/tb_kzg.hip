@@ -146,7 +146,7 @@ pair_ws take_pair_ws(carve& c) {
 void launch_pairing(kzg_state& g, const g1j* T, uint32_t n, const pair_ws& p, int* ok, hipStream_t s) {
   hipLaunchKernelGGL(k_kzg_pair_sums, dim3(1), dim3(256), 0, s, T, n, (const g2a*)(g.g2 + 1), p.P, p.Q, p.skip, p.zero);
   const uint8_t* z8 = reinterpret_cast<const uint8_t*>(p.zero);
-  hipLaunchKernelGGL(k_miller_coop, dim3(2), dim3(256), 0, s, (const g1a*)p.P, (const g2a*)p.Q, (const uint8_t*)p.skip, z8, z8, 2u, p.f);
+  hipLaunchKernelGGL(k_miller_wave, dim3(2), dim3(64), 0, s, (const g1a*)p.P, (const g2a*)p.Q, (const uint8_t*)p.skip, z8, z8, 2u, p.f);
   if (tb_final_coop())
     hipLaunchKernelGGL(k_final_verify_coop, dim3(1), dim3(TB_CFE_THREADS), 0, s, (const fp12*)p.f, 2u, (const uint32_t*)p.zero, ok);
   else

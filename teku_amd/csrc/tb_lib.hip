@@ -276,36 +276,14 @@ static uint32_t msm_min() {
 // accumulator wave per SIMD: 1024 waves x 64 lanes x 2 pairs).
 #define TB_LINE_CHUNK 262144u
 #define TB_MILLER_PER2_MIN 131072u
-// up to this many pairs, one pair per workgroup: the level program on coop
-// rows (k_miller_coop, 256 threads: a pair's loop in ~1/4 of the wave
-// kernel's time) up to TB_MILLER_COOP_MAX pairs -- one wave round of
-// 4-wave workgroups -- else one 64-lane wave per pair (k_miller_wave);
-// TBLS_MILLER_WAVE_MAX = "wave_max[,coop_max]" overrides (tuning)
-#define TB_MILLER_COOP_MAX 512u
-struct miller_env_t {
-  uint32_t wave_max, coop_max;
-};
-static const miller_env_t& miller_env() {
-  static const miller_env_t v = [] {
-    miller_env_t e{2048u, TB_MILLER_COOP_MAX};
-    const char* s = getenv("TBLS_MILLER_WAVE_MAX");
-    unsigned a = 0, b = 0;
-    const int k = s ? sscanf(s, "%u,%u", &a, &b) : 0;
-    if (k >= 1) e.wave_max = a;
-    if (k == 2) e.coop_max = b;
-    return e;
-  }();
+// up to this many pairs, one pair per 64-lane workgroup (k_miller_wave);
+// TBLS_MILLER_WAVE_MAX overrides (tuning).  (Round 6 measured the level
+// program on 16 coop rows, k_miller_coop: one pair's loop 1.00 ms against
+// the wave kernel's 0.84 at 128 sets, profiles/r06_latency_128_coop_vs_wave.json;
+// not kept.)
+static uint32_t miller_wave_max() {
+  static const uint32_t v = getenv("TBLS_MILLER_WAVE_MAX") ? (uint32_t)atoi(getenv("TBLS_MILLER_WAVE_MAX")) : 2048u;
   return v;
-}
-static uint32_t miller_wave_max() { return miller_env().wave_max; }
-static bool miller_coop(uint32_t n_pairs) { return n_pairs <= miller_env().coop_max; }
-// the wave-shaped Miller kernels: a pair per workgroup
-static void launch_miller_pairs(hipStream_t s, uint32_t np, const g1a* P, const g2a* Q, const uint8_t* skip, const uint8_t* ca,
-                                const uint8_t* cb, fp12* f) {
-  if (miller_coop(np))
-    hipLaunchKernelGGL(k_miller_coop, dim3(np), dim3(256), 0, s, P, Q, skip, ca, cb, np, f);
-  else
-    hipLaunchKernelGGL(k_miller_wave, dim3(np), dim3(64), 0, s, P, Q, skip, ca, cb, np, f);
 }
 
 // Pairs of a batch of n sets: [0, n) the sets' (r_i apk_i, H(m_i)), then the
@@ -669,8 +647,8 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
     hipLaunchKernelGGL(k_msm_bitsum_pairs, dim3(TB_MSM_XPAIRS), dim3(64), 0, sb, (const g2j*)(w + L.msm_sum), c.comb.as<const g1a>(),
                        P + n, Q + n, skip + n);
     if (pp.n_xwave)  // their Miller loops, one wave each, on this stream: f[n_f_main ..)
-      launch_miller_pairs(sb, pp.n_xwave, (const g1a*)P + n, (const g2a*)Q + n, (const uint8_t*)skip + n, (const uint8_t*)(w + L.set_code + n),
-                          (const uint8_t*)(w + L.sig_code + n), (fp12*)(w + L.f) + pp.n_f_main());
+      hipLaunchKernelGGL(k_miller_wave, dim3(pp.n_xwave), dim3(64), 0, sb, (const g1a*)P + n, (const g2a*)Q + n, (const uint8_t*)skip + n,
+                         (const uint8_t*)(w + L.set_code + n), (const uint8_t*)(w + L.sig_code + n), pp.n_xwave, (fp12*)(w + L.f) + pp.n_f_main());
   }
   TB_EV(9, sb);
   HIPCHK(hipEventRecord(c.e_join[1], sb));
@@ -756,7 +734,7 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
     const uint8_t* cb = w + L.sig_code;
     fp12* f = (fp12*)(w + L.f);
     if (pp.wave) {
-      launch_miller_pairs(s, np, (const g1a*)P, (const g2a*)Q, (const uint8_t*)skip, ca, cb, f);
+      hipLaunchKernelGGL(k_miller_wave, dim3(np), dim3(64), 0, s, (const g1a*)P, (const g2a*)Q, (const uint8_t*)skip, ca, cb, np, f);
     } else {
       // chunks of the main pairs: G2 lines (P and T in LDS), then the Fp12
       // accumulator (segment-major values: segment j of group g at f[j * n_groups + g])

@@ -210,7 +210,26 @@ TB_HD TB_INLINE fp2 fp2_mul_lazy(const fp2& a, const fp2& b) {
       mad29(x0, m0[i], P29[k - i]);
       mad29(x2, m1[i], P29[k - i]);
     }
+#if TB_CC_ON
+    // t0 = x0 + c0 - c1 and t1 = x2 + c0 + c1 in one block: t1's two 64-bit
+    // adds sit between the halves of t0's subtraction, so the borrow is read
+    // two instructions after it is written (no s_nop; see TB_ASM_CARRY)
+    uint64_t t1;
+    uint32_t t0lo, t0hi;
+    {
+      const uint64_t u = x0 + c0;
+      uint64_t br;
+      asm("v_sub_co_u32 %0, %2, %4, %5\n\t"
+          "v_lshl_add_u64 %3, %6, 0, %7\n\t"
+          "v_lshl_add_u64 %3, %3, 0, %8\n\t"
+          "v_subb_co_u32 %1, %2, %9, %10, %2"
+          : "=&v"(t0lo), "=&v"(t0hi), "=&s"(br), "=&v"(t1)
+          : "v"((uint32_t)u), "v"((uint32_t)c1), "v"(x2), "v"(c0), "v"(c1), "v"((uint32_t)(u >> 32)), "v"((uint32_t)(c1 >> 32)));
+    }
+    uint64_t t0 = ((uint64_t)t0hi << 32) | t0lo;
+#else
     uint64_t t0 = x0 + c0 - c1, t1 = x2 + c0 + c1;
+#endif
     if (k < 14) {
       m0[k] = ((uint32_t)t0 * N0_29) & M29;
       m1[k] = ((uint32_t)t1 * N0_29) & M29;
