@@ -45,6 +45,7 @@ exceptionally with BlsException (BLS.batchVerify throws, BLS.java:235-237).
 
 import queue
 import threading
+from operator import attrgetter
 from typing import Callable, List, Optional, Sequence
 
 from . import bls as _bls
@@ -74,7 +75,7 @@ class TaskFuture:
     _PENDING, _DONE, _FAILED = 0, 1, 2
 
     def __init__(self, cond: Optional[threading.Condition] = None):
-        self._cond = cond if cond is not None else threading.Condition()
+        self._cond = cond if cond is not None else _SHARED_COND
         self._state = TaskFuture._PENDING
         self._value = None
         self._callbacks = None
@@ -128,18 +129,32 @@ class TaskFuture:
 
     @staticmethod
     def complete_all(futures: Sequence["TaskFuture"], values: Sequence[bool]):
-        """Complete a batch's futures (sharing one condition) with one wake-up."""
+        """Complete a batch's futures with one wake-up per condition they
+        wait on (normally one: the service's)."""
         if not futures:
             return
-        cond = futures[0]._cond
-        with cond:
+        conds = set(map(_get_cond, futures))
+        for c in conds:
+            c.acquire()
+        try:
             for f, v in zip(futures, values):
                 f._value = v
                 f._state = TaskFuture._DONE
-            cond.notify_all()
-        for f in futures:
-            if f._callbacks:
-                f._run_callbacks()
+            for c in conds:
+                c.notify_all()
+        finally:
+            for c in conds:
+                c.release()
+        if any(map(_get_callbacks, futures)):
+            for f in futures:
+                if f._callbacks:
+                    f._run_callbacks()
+
+
+_SHARED_COND = threading.Condition()  # futures made outside a service
+_get_result = attrgetter("result")
+_get_cond = attrgetter("_cond")
+_get_callbacks = attrgetter("_callbacks")
 
 
 class SignatureTask:
@@ -323,7 +338,7 @@ class AggregatingSignatureVerificationService:
             self.host_ms_total += t.total_ms
             self.last_batch_timing = {"sets": len(all_sets), "device_ms": t.device_ms, "total_ms": t.total_ms, "n_devices": t.n_devices,
                                       "settled": not ok}
-            futs = [task.result for task in tasks]
+            futs = list(map(_get_result, tasks))
             if ok:
                 vals = [True] * len(tasks)
             elif len(all_sets) == len(tasks):  # one set per task (gossip)
@@ -334,11 +349,7 @@ class AggregatingSignatureVerificationService:
                     n = len(task.sets)
                     vals.append(all(verdicts[k : k + n]))
                     k += n
-            if len(set(id(f._cond) for f in futs)) == 1:
-                TaskFuture.complete_all(futs, vals)
-            else:
-                for f, v in zip(futs, vals):
-                    f.set_result(v)
+            TaskFuture.complete_all(futs, vals)
             return
         self.device_passes += 1
         if self._batch_timed(all_sets):

@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import ctypes
 import hashlib
+from operator import itemgetter
 from typing import List, Sequence, Tuple
 
 import numpy as np
@@ -139,6 +140,9 @@ _SET_DTYPE = np.dtype([("pks", "<u8"), ("n_pks", "<u4"), ("msg", "<u8"), ("msg_l
 assert _SET_DTYPE.itemsize == ctypes.sizeof(native.TblsSet)
 
 
+_G0, _G1, _G2, _G3 = (itemgetter(k) for k in range(4))
+
+
 class SetArray:
     """tbls_set[n] over contiguous blobs: set i has keys pks[48 k_off[i] ..],
     message msgs[m_off[i] .. m_off[i+1]) and signature sigs[96 i ..]."""
@@ -176,8 +180,8 @@ class SetArray:
     @classmethod
     def from_tuples(cls, sets: Sequence[Tuple[bytes, int, bytes, bytes]]) -> "SetArray":
         """[(pk_blob, n_pks, msg, sig96)] (the tuples of bls.batch_verify_raw)."""
-        return cls(b"".join(s[0] for s in sets), [s[1] for s in sets], b"".join(s[2] for s in sets), [len(s[2]) for s in sets],
-                   b"".join(s[3] for s in sets))
+        msgs = list(map(_G2, sets))
+        return cls(b"".join(map(_G0, sets)), list(map(_G1, sets)), b"".join(msgs), list(map(len, msgs)), b"".join(map(_G3, sets)))
 
     def batch_verify(self, rands: Sequence[int], n_gpus: int = 0, timing: "native.TblsTiming" = None) -> bool:
         if isinstance(rands, np.ndarray):  # uint64 array (fast_multipliers): passed in place

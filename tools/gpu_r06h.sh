@@ -17,6 +17,6 @@ import json; d = json.load(open('$O/bench_$TAG.json')); c = d['configs']; k = d[
 print(round(d['value']), round(d['ms_per_step'], 2), 'p50', round(d['p50_latency_ms_128'], 3), '1m', round(d['value_1m']), 'kt', round(d['value_key_table']),
       {x: round(v['p50_ms'], 3) for x, v in c.items()}, 'fail', round(c['cfg4']['failure_settle_ms'], 2), 'svc', c['cfg4']['service_ms'], 'cpu', round(d['cpu_baseline']['value']),
       'kzg', round(k['p50_ms_1'], 3), round(k['p50_ms_6'], 3), 'frac', round(d['roofline']['frac'], 3), {x: round(v, 3) for x, v in d['stage_ms_exclusive'].items()})"
-TAG=$TAG bash tools/gpu_r06d.sh | head -20 || exit $?
+TAG=$TAG bash tools/gpu_r06d.sh > $O/lat_$TAG.txt 2>&1 || exit $?; tail -3 $O/lat_$TAG.txt
 [ -n "$KZGQ" ] && { bash tools/gpu_r06f.sh || exit $?; }
 echo done
