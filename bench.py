@@ -35,6 +35,16 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+# Hardware queues per process (read by the HIP runtime at its first use,
+# before torch or the library touch the device).  The BLS library opens four
+# streams per device (the caller's pipeline and three per-set stage streams);
+# with the runtime's default of four hardware queues the KZG context's two
+# streams, opened after them, share queues with them and the KZG pipeline ran
+# 12 % slower (profiles/r06_kzg_hw_queues.json).  A node
+# running both contexts on a GPU sets at least 8.  An
+# explicit setting is kept (the A/B against the default of four).
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
@@ -471,11 +481,12 @@ def facade_cfg4(pks, msgs, sigs, reps, raw_p50):
 
 
 def kzg_warm():
-    """Load the trusted setup and run one 6-blob verification before the BLS
-    legs, as a node loads the setup at boot: the KZG context's device buffers
-    are then allocated before the 131k-set BLS workspace.  Created after that
-    workspace they measured ~12 % slower kernels (1-blob p50 5.39 vs 4.71 ms,
-    tools/kzg_after_load.py, profiles/r05_kzg_after_load*.json)."""
+    """Load the trusted setup and run one 6-blob verification (the KZG
+    context created before the BLS library's: tools/kzg_order_probe.py's
+    kzg_first order).  Round 5 called it before the BLS legs to avoid the
+    KZG-after-BLS slowdown; round 6 found its cause (hardware queues shared
+    with the BLS streams, fixed by GPU_MAX_HW_QUEUES above) and the bench no
+    longer calls it."""
     from teku_amd import kzg
 
     ck = kzg.CKZG4844.get_instance()
@@ -585,8 +596,6 @@ def main():
         return
     if world > 1:
         dist.init_process_group("nccl", device_id=device)
-    if not args.no_kzg and rank == 0:
-        kzg_warm()
     L = native.lib()
 
     S = args.sets_per_gpu
@@ -731,7 +740,8 @@ def main():
     extra = {} if args.no_extra else extra_configs(device, stream, args.extra_reps)
     kzg_out = None if args.no_kzg else kzg_leg(device, args.extra_reps, not args.no_cpu_baseline)
     if kzg_out is not None:
-        kzg_out["context"] = "trusted setup loaded and one 6-blob verification run before the BLS legs (kzg_warm: node boot order)"
+        kzg_out["context"] = ("trusted setup loaded after the BLS legs (GPU_MAX_HW_QUEUES=%s: the KZG streams get hardware queues of their own)"
+                              % os.environ.get("GPU_MAX_HW_QUEUES"))
 
     cpu = None if args.no_cpu_baseline else cpu_baseline_oracle(pks, msgs, sigs, min(4096, S), min(512, S))
     line = {

@@ -53,24 +53,29 @@ namespace {
 // exceptional case ends at Z = 0 (sticky, tb_lean.h) and returns false:
 // k_set_hash_fix recomputes the set with the exact formulas.
 #define TB_PARK() asm volatile("" ::: "memory")
-__device__ TB_INLINE bool g2_clear_cofactor_lean(g2a& out, const g2j& p, g2a* park, g2a* keep) {
+// Round 6: the two [|x|] chains run with the running point in LDS
+// (tb_lean.h lds_pt: 288 B per lane) and their affine addend in global
+// memory (gpark, this set's 192-B slot of the caller's buffer); keep is the
+// set's output slot Q[i].
+__device__ TB_INLINE bool g2_clear_cofactor_lean(g2a& out, const g2j& p, const lean::lds_pt& P, g2a* gpark, g2a* keep) {
   g2a pa;
   if (!lean::to_aff(pa, p)) return false;
-  const g2j t1 = lean::mul_xabs_aff(pa, park);
-  pa = *park;
+  lean::mul_xabs_aff_lds(P, pa, gpark);  // t1 = [|x|]P in LDS
+  TB_PARK();
+  pa = *gpark;
   g2a ua, ea;
-  if (!lean::to_aff(ua, lean::madd(jac_neg(t1), lean::psi_aff(pa)))) return false;
+  if (!lean::to_aff(ua, lean::madd(jac_neg(P.get()), lean::psi_aff(pa)))) return false;
   *keep = ua;
   TB_PARK();
-  pa = *park;
+  pa = *gpark;
   if (!lean::to_aff(ea, lean::madd(g2_psi2(jac_dbl_i(jac_from_aff(pa))), lean::neg_aff(pa)))) return false;
   ua = *keep;
   *keep = ea;
   TB_PARK();
-  const g2j t3 = lean::mul_xabs_aff<true>(ua, park);
+  lean::mul_xabs_aff_lds<true>(P, ua, gpark);  // t3 = [|x| + 1]u in LDS
   TB_PARK();
   ea = *keep;
-  return lean::to_aff(out, lean::madd(jac_neg(t3), ea));
+  return lean::to_aff(out, lean::madd(jac_neg(P.get()), ea));
 }
 #undef TB_PARK
 
@@ -78,8 +83,8 @@ __device__ TB_INLINE bool g2_clear_cofactor_lean(g2a& out, const g2j& p, g2a* pa
 
 extern "C" __global__ void __launch_bounds__(TB_BLOCK, 2)
     k_set_hash_w2(const uint8_t* __restrict__ msgs, const uint32_t* __restrict__ msg_off, const uint8_t* __restrict__ dst,
-                  uint32_t dlen, uint32_t n, g2a* __restrict__ Q, uint8_t* __restrict__ skip) {
-  __shared__ g2a park[TB_BLOCK];  // 192 B per lane: 98 KB per CU at two waves per SIMD
+                  uint32_t dlen, uint32_t n, g2a* __restrict__ Q, uint8_t* __restrict__ skip, g2a* __restrict__ park) {
+  __shared__ uint4 Psh[TB_LDS_PT_UINT4 * TB_BLOCK];  // the chains' running point: 288 B per lane, 147 KB per CU at two waves per SIMD
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   xmd_ctx c;
@@ -100,7 +105,7 @@ extern "C" __global__ void __launch_bounds__(TB_BLOCK, 2)
 #endif
   const g2j p = iso_map_jac(e2p_add_aff_aff(q0, q1));
   g2a a;
-  if (!g2_clear_cofactor_lean(a, p, &park[threadIdx.x], &Q[i])) {
+  if (!g2_clear_cofactor_lean(a, p, lean::lds_pt{Psh + threadIdx.x}, &park[i], &Q[i])) {
     skip[i] = 2;  // k_set_hash_fix: the exact formulas (it rewrites Q[i])
     return;
   }

@@ -14,16 +14,20 @@ using namespace tb;
 extern "C" __global__ void __launch_bounds__(TB_BLOCK, 2)
     k_sig_check_w2(const uint8_t* __restrict__ sigs, uint32_t n, g2a* __restrict__ sig_aff, uint8_t* __restrict__ sig_use,
                    uint8_t* __restrict__ sig_code, uint32_t* __restrict__ n_bad, uint32_t skip_mode) {
-  __shared__ g2a park[TB_BLOCK];  // 192 B per lane
+  // round 6: the chain's running point in LDS (288 B per lane), Q parked in
+  // this set's own output slot sig_aff[i] (tb_lean.h lds_pt)
+  __shared__ uint4 Psh[TB_LDS_PT_UINT4 * TB_BLOCK];
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   g2a a;
   bool inf;
   int code = g2_decompress(a, inf, sigs + (size_t)i * 96);
   if (code == TB_SUCCESS && !inf) {
-    const g2j t = lean::mul_xabs_aff(a, &park[threadIdx.x]);
-    a = park[threadIdx.x];
-    if (!lean::psi_eq_neg(t, a)) code = TB_POINT_NOT_IN_GROUP;
+    const lean::lds_pt P{Psh + threadIdx.x};
+    lean::mul_xabs_aff_lds(P, a, &sig_aff[i]);
+    asm volatile("" ::: "memory");
+    a = sig_aff[i];
+    if (!lean::psi_eq_neg(P.get(), a)) code = TB_POINT_NOT_IN_GROUP;
   }
   const bool use = code == TB_SUCCESS && !inf;
   if (!use) {

@@ -50,13 +50,6 @@ int fail(int rc, const char* fmt, ...) {
 
 size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
 
-// Device allocations of the KZG context are rounded up to TKZG_ALLOC_ROUND
-// bytes (0: as requested; A/B of the allocation-order slowdown).
-#ifndef TKZG_ALLOC_ROUND
-#define TKZG_ALLOC_ROUND 0
-#endif
-size_t dev_round(size_t nb) { return TKZG_ALLOC_ROUND ? (nb + TKZG_ALLOC_ROUND - 1) / TKZG_ALLOC_ROUND * TKZG_ALLOC_ROUND : nb; }
-
 struct growbuf {
   void* p = nullptr;
   size_t cap = 0;
@@ -64,7 +57,7 @@ struct growbuf {
   int ensure(size_t bytes) {
     if (bytes <= cap) return 0;
     release();
-    const size_t nb = host ? (bytes < 65536 ? 65536 : bytes + bytes / 4) : dev_round(bytes < 65536 ? 65536 : bytes + bytes / 4);
+    const size_t nb = bytes < 65536 ? 65536 : bytes + bytes / 4;
     const hipError_t e = host ? hipHostMalloc(&p, nb, hipHostMallocDefault) : hipMalloc(&p, nb);
     if (e != hipSuccess) {
       p = nullptr;
@@ -402,7 +395,7 @@ extern "C" int tkzg_load_trusted_setup(const uint8_t* g1_monomial, size_t g1_mon
   // device: [lag | lag_inf | roots | g2 | g2_inf]  scratch: [bytes in | codes]
   const size_t persist = align16(N * sizeof(g1a)) + align16(N) + align16(N * sizeof(fr)) + align16(NG2 * sizeof(g2a)) + align16(NG2);
   void* p = nullptr;
-  KCHK(hipMalloc(&p, dev_round(persist)));
+  KCHK(hipMalloc(&p, persist));
   carve c{static_cast<uint8_t*>(p)};
   g.lag = c.take<g1a>(N);
   g.lag_inf = c.take<uint8_t>(N);

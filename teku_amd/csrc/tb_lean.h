@@ -68,6 +68,90 @@ __device__ TB_INLINE g2j mul_xabs_aff(const g2a& Q, g2a* park) {
   return r;
 }
 
+// ---------------------------------------------------------------------------
+// The same chains with the running point resident in LDS (round 6): 288 B
+// per lane (18 uint4; 147 KB per CU at two waves per SIMD), the formulas
+// read X, Y, Z when they use them and store each new coordinate once it is
+// final, so only the formula's temporaries and one Fp2 product's share the
+// 256 registers (the register-resident point spilled 16-18 scratch accesses
+// per doubling).  The affine addend waits in global memory (the caller's
+// 192-B slot), read once per addition.  Element q of lane l at
+// base[q * TB_BLOCK + l]: a wave's 16-byte accesses are consecutive.
+// Same formulas, in the same order, as jac_dbl_i and madd above.
+struct lds_pt {
+  uint4* p;  // &base[threadIdx.x]
+  __device__ TB_INLINE fp2 ld(int k) const {
+    fp2 r;
+    TB_UNROLL for (int j = 0; j < 3; j++) {
+      const uint4 a = p[(6 * k + j) * TB_BLOCK], b = p[(6 * k + 3 + j) * TB_BLOCK];
+      r.c0.l[4 * j] = a.x, r.c0.l[4 * j + 1] = a.y, r.c0.l[4 * j + 2] = a.z, r.c0.l[4 * j + 3] = a.w;
+      r.c1.l[4 * j] = b.x, r.c1.l[4 * j + 1] = b.y, r.c1.l[4 * j + 2] = b.z, r.c1.l[4 * j + 3] = b.w;
+    }
+    return r;
+  }
+  __device__ TB_INLINE void st(int k, const fp2& v) const {
+    TB_UNROLL for (int j = 0; j < 3; j++) {
+      p[(6 * k + j) * TB_BLOCK] = make_uint4(v.c0.l[4 * j], v.c0.l[4 * j + 1], v.c0.l[4 * j + 2], v.c0.l[4 * j + 3]);
+      p[(6 * k + 3 + j) * TB_BLOCK] = make_uint4(v.c1.l[4 * j], v.c1.l[4 * j + 1], v.c1.l[4 * j + 2], v.c1.l[4 * j + 3]);
+    }
+    asm volatile("" ::: "memory");  // later uses read LDS, not a forwarded register copy
+  }
+  __device__ TB_INLINE g2j get() const { return {ld(0), ld(1), ld(2)}; }
+  __device__ TB_INLINE void put(const g2j& v) const {
+    st(0, v.x);
+    st(1, v.y);
+    st(2, v.z);
+  }
+};
+#define TB_LDS_PT_UINT4 18  // uint4 per lane
+
+// jac_dbl_i (dbl-2009-l) on the LDS-resident point
+__device__ TB_INLINE void dbl_lds(const lds_pt& P) {
+  {
+    const fp2 y2 = fp2_dbl(P.ld(1));
+    P.st(2, M(y2, P.ld(2)));  // Z3 = (2Y) Z: Z dies
+  }
+  const fp2 B = S(P.ld(1));  // Y dies
+  const fp2 A = S(P.ld(0));
+  const fp2 C = S(B);
+  const fp2 D = fp2_dbl(fp2_sub(fp2_sub(S(fp2_add_nr(P.ld(0), B)), A), C));
+  const fp2 E = fp2_add_nr(fp2_dbl(A), A);  // < 4p: operand of the two products below only
+  const fp2 X3 = fp2_sub(S(E), fp2_dbl(D));
+  P.st(0, X3);
+  const fp2 C8 = fp2_dbl(fp2_dbl(fp2_dbl(C)));
+  P.st(1, fp2_sub(M(E, fp2_sub(D, X3)), C8));
+}
+
+// madd above on the LDS-resident point, q affine (finite)
+__device__ TB_INLINE void madd_lds(const lds_pt& P, const g2a& q) {
+  const fp2 Z1Z1 = S(P.ld(2));
+  const fp2 H = fp2_sub(M(q.x, Z1Z1), P.ld(0));
+  const fp2 r = fp2_dbl(fp2_sub(M(M(q.y, P.ld(2)), Z1Z1), P.ld(1)));
+  const fp2 HH = S(H);
+  P.st(2, fp2_sub(fp2_sub(S(fp2_add_nr(P.ld(2), H)), Z1Z1), HH));
+  const fp2 I = fp2_dbl(fp2_dbl(HH));
+  const fp2 J = M(H, I);
+  const fp2 V = M(P.ld(0), I);
+  const fp2 X3 = fp2_sub(fp2_sub(S(r), J), fp2_dbl(V));
+  const fp2 Y3 = fp2_sub(M(r, fp2_sub(V, X3)), fp2_dbl(M(P.ld(1), J)));
+  P.st(0, X3);
+  P.st(1, Y3);
+}
+
+// mul_xabs_aff with the running point in LDS (left there) and Q in global
+// memory at *gpark (written here)
+template <bool PLUS1 = false>
+__device__ TB_INLINE void mul_xabs_aff_lds(const lds_pt& P, const g2a& Q, g2a* gpark) {
+  *gpark = Q;
+  asm volatile("" ::: "memory");  // the additions reload Q from memory: no register copy across the loop
+  P.put(jac_from_aff(Q));
+  TB_NOUNROLL for (int k = 0; k < 6; k++) {
+    const int nd = k == 0 ? 1 : k == 1 ? 2 : k == 2 ? 3 : k == 3 ? 9 : k == 4 ? 32 : 16;
+    TB_NOUNROLL for (int i = 0; i < nd; i++) dbl_lds(P);
+    if (PLUS1 || k < 5) madd_lds(P, *gpark);
+  }
+}
+
 // affine form; false (o untouched) when Z = 0
 __device__ TB_INLINE bool to_aff(g2a& o, const g2j& p) {
   if (fp2_is_zero(p.z)) return false;

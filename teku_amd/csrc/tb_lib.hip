@@ -712,7 +712,9 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
     hipLaunchKernelGGL(k_set_hash_duo, dim3((2 * n + TB_BLOCK - 1) / TB_BLOCK), blk, 0, sh, b.msgs, b.msg_off, dst, dlen, n, Q, skip);
     hipLaunchKernelGGL(k_set_hash_fix, g, blk, 0, sh, b.msgs, b.msg_off, dst, dlen, n, Q, skip);
   } else if (n && w2(n)) {  // two waves per SIMD, then the exact formulas for the sets it flags (skip == 2)
-    hipLaunchKernelGGL(k_set_hash_w2, g, blk, 0, sh, b.msgs, b.msg_off, dst, dlen, n, Q, skip);
+    // the chains' affine addends wait in the line buffer (19,584 B per pair,
+    // unused until the line kernel, which runs after this stream joins)
+    hipLaunchKernelGGL(k_set_hash_w2, g, blk, 0, sh, b.msgs, b.msg_off, dst, dlen, n, Q, skip, (g2a*)(w + L.lines));
     hipLaunchKernelGGL(k_set_hash_fix, g, blk, 0, sh, b.msgs, b.msg_off, dst, dlen, n, Q, skip);
   } else if (n)
     hipLaunchKernelGGL(k_set_hash, g, blk, 0, sh, b.msgs, b.msg_off, dst, dlen, n, Q, skip);

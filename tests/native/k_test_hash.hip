@@ -48,9 +48,9 @@ extern "C" int tbls_test_hash_variant(const char* product_so, int variant, const
   if (!h) return -4;
   auto sym = [&](const char* name) { return dlsym(h, name); };
   const size_t mbytes = msg_off[n];
-  dev_mem dm, doff, ddst, dq, dskip, dh;
+  dev_mem dm, doff, ddst, dq, dskip, dh, dpark;
   if (dm.alloc(mbytes) || doff.alloc(4 * (n + 1)) || ddst.alloc(dlen) || dq.alloc(n * sizeof(tb::g2a)) || dskip.alloc(n) ||
-      dh.alloc(n * sizeof(tb::hrow_set)))
+      dh.alloc(n * sizeof(tb::hrow_set)) || dpark.alloc(n * sizeof(tb::g2a)))
     return -5;
   if ((mbytes && hipMemcpy(dm.p, msgs, mbytes, hipMemcpyHostToDevice) != hipSuccess) ||
       hipMemcpy(doff.p, msg_off, 4 * (n + 1), hipMemcpyHostToDevice) != hipSuccess ||
@@ -61,6 +61,7 @@ extern "C" int tbls_test_hash_variant(const char* product_so, int variant, const
   int ff = force_fix;
   const uint64_t* no_rand = nullptr;
   void* a_set[] = {&dm.p, &doff.p, &ddst.p, &d32, &n32, &dq.p, &dskip.p};
+  void* a_w2[] = {&dm.p, &doff.p, &ddst.p, &d32, &n32, &dq.p, &dskip.p, &dpark.p};  // k_set_hash_w2: + the chains' park buffer
   void* a_coop[] = {&dm.p, &doff.p, &ddst.p, &d32, &n32, &dq.p, &dskip.p, &no_rand};
   void* a_field[] = {&dm.p, &doff.p, &ddst.p, &d32, &n32, &dh.p};
   void* a_h[] = {&n32, &dh.p};
@@ -80,7 +81,7 @@ extern "C" int tbls_test_hash_variant(const char* product_so, int variant, const
     case 3: rc = launch(sym("k_set_hash_coop"), n32, 256, a_coop); break;
     case 4: rc = launch(sym("k_set_hash_wave"), n32, 128, a_set); break;
     case 5:
-      rc = launch(sym("k_set_hash_w2"), g, BLK, a_set);
+      rc = launch(sym("k_set_hash_w2"), g, BLK, a_w2);
       if (!rc && ff && hipMemset(dskip.p, 2, n) != hipSuccess) rc = -6;  // every set through the exact recomputation
       if (!rc) rc = launch(sym("k_set_hash_fix"), g, BLK, a_set);
       break;
