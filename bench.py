@@ -79,6 +79,14 @@ STAGE_KERNEL = {
     "miller": "k_miller_lines_w2 + k_miller_accs_lds",
     "fp12_prod": "k_fp12_prod_wave_seg + k_fp12_seg_combine_coop",
 }
+# Algorithmic HBM bytes per unit of the Miller stage: a
+# pair's G1 point (96 B) and G2 point (192 B) in, its share of the segment
+# outputs out (8 segments x 576 B per 16-pair group = 288 B), codes (3 B).
+# The split Miller loop adds the line table by design: 68 lines x 3 Fp2 =
+# 19,584 B per pair written by the line kernel and read once by the
+# accumulator (tb_lines.h).
+MILLER_ALG_BYTES_PER_PAIR = 96 + 192 + 288 + 3
+MILLER_LINE_BYTES_PER_PAIR = 19584
 STAGE_UNITS = {"pk_decompress": "keys", "set_pk": "sets", "set_sig": "sets", "set_hash": "sets", "g2_sum": "sets", "miller": "pairs", "fp12_prod": "pairs"}
 _MC = os.path.join(ROOT, "tools", "mul_counts.json")
 M_PER_UNIT = json.load(open(_MC)) if os.path.exists(_MC) else {}
@@ -144,6 +152,8 @@ def roofline_entry(stage_ms, S, device, ms_per_step):
         parts = [tj.get(k.strip(), {}).get("bytes_per_launch") for k in kernel.split("+")]
         traffic = sum(parts) if all(p is not None for p in parts) else None
     per_set = M_PER_UNIT.get("per_set_total")
+    alg = units[name] * MILLER_ALG_BYTES_PER_PAIR if name == "miller" else None
+    alg_lines = alg + 2 * units[name] * MILLER_LINE_BYTES_PER_PAIR if alg else None
     return {
         "bound": "valu-int (v_mad_u64_u32 issue)",
         "kernel": kernel,
@@ -154,6 +164,10 @@ def roofline_entry(stage_ms, S, device, ms_per_step):
         "peak_1wave": peak_mac_per_s(device, True) / 1e12,
         "frac_1wave": (achieved / peak_mac_per_s(device, True)) if achieved else None,
         "traffic": traffic,
+        "traffic_unit": "B per launch (profiles/pmc_traffic.json: FETCH_SIZE x 2 + WRITE_SIZE, this round's build)",
+        "algorithmic_bytes": alg,
+        "traffic_ratio": (traffic / alg) if traffic and alg else None,
+        "traffic_ratio_with_line_tables": (traffic / alg_lines) if traffic and alg_lines else None,
         "model": "SURVEY.md 8(d): Fp products per unit (tools/mul_counts.json) x 300 MAC",
         "units_per_launch": round(units[name]),
         "unit_of_work": STAGE_UNITS[name],

@@ -216,6 +216,60 @@ def test_async_final_pipelined_two_streams(hip):
     assert oks2.tolist() == [1, 0]
 
 
+def test_partials_alternating_streams(hip):
+    """Device-resident partials alternating two streams with no host wait
+    between them, each followed on its own stream by
+    tbls_dev_final_verify_async (the shape of a service with two batches
+    queued on a device; the shared workspace orders them by its last-use
+    event).  Valid and tampered batches alternate at a bucket-sum size (split
+    Miller loop, LDS accumulator) and a small one (coop kernels), so the
+    workspace is re-carved between sizes.  (Two workspace slots with batch
+    k+1's per-set stages under batch k's final exponentiation measured slower,
+    profiles/r06_ab_inflight.json.)"""
+    import torch
+
+    from teku_amd import synth
+
+    bls, native, L, _ = hip
+    dev = torch.device("cuda", 0)
+    u8 = lambda b: torch.frombuffer(bytearray(b), dtype=torch.uint8).to(dev)  # noqa: E731
+
+    def batch(n, seed, tamper):
+        pks, msgs, sigs = synth.single_signer(5000, n, seed=seed)
+        if tamper:
+            sigs = bytearray(sigs)
+            i = n // 2
+            sigs[96 * i : 96 * (i + 1)], sigs[96 * (i + 1) : 96 * (i + 2)] = sigs[96 * (i + 1) : 96 * (i + 2)], sigs[96 * i : 96 * (i + 1)]
+        t = dict(pks=u8(pks), msgs=u8(msgs), sigs=u8(bytes(sigs)), pk_off=torch.arange(0, n + 1, dtype=torch.int32, device=dev),
+                 msg_off=torch.arange(0, 32 * (n + 1), 32, dtype=torch.int32, device=dev),
+                 rand=torch.randint(1, 1 << 62, (n,), dtype=torch.int64, device=dev))
+        t["desc"] = native.TblsDevBatch(t["pks"].data_ptr(), t["pk_off"].data_ptr(), n, t["msgs"].data_ptr(), t["msg_off"].data_ptr(),
+                                        t["sigs"].data_ptr(), t["rand"].data_ptr(), n)
+        return t
+
+    big = [batch(40960, 7, False), batch(40960, 8, True)]
+    small = [batch(96, 9, False), batch(96, 10, True)]
+    streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+    recs = [torch.empty(native.PARTIAL_BYTES, dtype=torch.uint8, device=dev) for _ in range(2)]
+    # the expected verdicts: 1 for the valid batches, 0 for the tampered ones
+    plan = [big[0], big[1], big[0], big[1], small[0], big[1], small[1], big[0], big[0], small[1]]
+    want = [1, 0, 1, 0, 1, 0, 0, 1, 1, 0]
+    oks = torch.full((len(plan),), 7, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+    for k, b in enumerate(plan):
+        st = streams[k % 2]
+        native.check(L.tbls_dev_batch_partial(0, ctypes.byref(b["desc"]), st.cuda_stream, recs[k % 2].data_ptr()), "partial")
+        native.check(L.tbls_dev_final_verify_async(0, recs[k % 2].data_ptr(), 1, st.cuda_stream, oks[k : k + 1].data_ptr()), "final_async")
+    torch.cuda.synchronize()
+    assert oks.tolist() == want
+    # and back to one stream: the same slot each time, same verdicts
+    for k, b in enumerate(plan[:4]):
+        native.check(L.tbls_dev_batch_partial(0, ctypes.byref(b["desc"]), streams[0].cuda_stream, recs[0].data_ptr()), "partial")
+        native.check(L.tbls_dev_final_verify_async(0, recs[0].data_ptr(), 1, streams[0].cuda_stream, oks[k : k + 1].data_ptr()), "final_async")
+    torch.cuda.synchronize()
+    assert oks[:4].tolist() == want[:4]
+
+
 def test_hash_sign_keys_bit_exact(hip):
     bls, native, L, _ = hip
     for msg, dst in [(b"", O.ETH2_DST), (b"abc", O.ETH2_DST), (b"\x42" * 32, O.ETH2_DST), (b"abc", NUL_DST), (bytes(range(200)), O.ETH2_DST)]:
