@@ -59,6 +59,167 @@ extern "C" __global__ void __launch_bounds__(128)
 // ---------------------------------------------------------------------------
 #include "tb_cprog.h"
 
+// Phase timestamps of k_set_hash_coop (profiling builds only, -DTB_HASH_STAMPS,
+// tools/build_variant.py): thread 0 of set i writes wall_clock64() (100 MHz)
+// at the phase boundaries to g_hash_stamps[16 i + k]; tbls_debug_hash_stamps
+// copies them out (tools/hash_stamps_probe.py).
+#ifdef TB_HASH_STAMPS
+__device__ unsigned long long g_hash_stamps[16 * 4096];
+#define HSTAMP(k)                                                              \
+  do {                                                                         \
+    if (threadIdx.x == 0 && i < 4096) g_hash_stamps[16 * i + (k)] = wall_clock64(); \
+  } while (0)
+extern "C" int tbls_debug_hash_stamps(unsigned long long* out, unsigned n) {
+  if (n > 4096) n = 4096;
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_hash_stamps), (size_t)16 * n * sizeof(unsigned long long), 0, hipMemcpyDeviceToHost);
+}
+#else
+#define HSTAMP(k) ((void)0)
+#endif
+
+// expand_message_xmd / hash_to_field for the coop kernel with the padded
+// message blocks built as big-endian words in LDS by the whole workgroup, so
+// lane 0 only runs the 18 compressions (the byte-at-a-time assembly of
+// sha256_virtual, with its global loads of the message and DST bytes, took
+// most of the 156 us lane-0 phase at 128 sets: tools/hash_stamps_probe.py).
+//   b0 = H(Z_pad || msg || I2OSP(256, 2) || 0 || DST || len): Z_pad is the
+//        precomputed mid-state, xw0 holds the rest, padded (n0 blocks);
+//   b_i = H((b0 ^ b_{i-1}) || I2OSP(i, 1) || DST || len): xwi holds the
+//        padded message with the 32 x bytes and the index byte zero (ni
+//        blocks); x fills words 0-7 and i the top byte of word 8.
+// Same bytes as tb_h2c.h get_b0 / get_bi (RFC 9380 section 5.3.1).
+#define XW0_MAX 8  // blocks: msg + DST up to 495 bytes (else the byte path)
+#define XWI_MAX 5  // 34 + dlen + 9 <= 320 for dlen <= 255
+struct xmd_words {
+  uint32_t w0[16 * XW0_MAX];
+  uint32_t wi[16 * XWI_MAX];
+};
+
+__device__ TB_INLINE uint32_t xmd_byte0(const uint8_t* msg, uint32_t m, const uint8_t* dst, uint32_t dlen, uint32_t L, uint32_t i) {
+  if (i < L) {
+    if (i < m) return msg[i];
+    i -= m;
+    if (i == 0) return 0x01;
+    if (i < 3) return 0x00;
+    i -= 3;
+    return i < dlen ? dst[i] : dlen;
+  }
+  return i == L ? 0x80u : 0u;
+}
+__device__ TB_INLINE uint32_t xmd_bytei(const uint8_t* dst, uint32_t dlen, uint32_t L, uint32_t i) {
+  if (i < L) {
+    if (i < 33) return 0;  // x and the index byte
+    i -= 33;
+    return i < dlen ? dst[i] : dlen;
+  }
+  return i == L ? 0x80u : 0u;
+}
+// every thread of the block: fill X (n0 / ni blocks); returns false when the
+// message is too long for X (the caller takes hash_to_field_fp2)
+__device__ TB_INLINE bool xmd_words_fill(xmd_words& X, const uint8_t* msg, uint32_t m, const uint8_t* dst, uint32_t dlen, uint32_t& n0,
+                                         uint32_t& ni) {
+  const uint32_t L0 = m + 3 + dlen + 1, Li = 32 + 1 + dlen + 1;
+  n0 = (L0 + 9 + 63) / 64;
+  ni = (Li + 9 + 63) / 64;
+  if (n0 > XW0_MAX || ni > XWI_MAX) return false;
+  for (uint32_t t = threadIdx.x; t < 16 * (n0 + ni); t += blockDim.x) {
+    const bool first = t < 16 * n0;
+    const uint32_t wd = first ? t : t - 16 * n0, nb = first ? n0 : ni;
+    uint32_t v;
+    if (wd >= 16 * nb - 2) {  // the 64-bit length field
+      const uint64_t bits = (uint64_t)(first ? 64 + L0 : Li) * 8;
+      v = wd == 16 * nb - 2 ? (uint32_t)(bits >> 32) : (uint32_t)bits;
+    } else {
+      v = 0;
+      for (int by = 0; by < 4; by++)
+        v = (v << 8) | (first ? xmd_byte0(msg, m, dst, dlen, L0, 4 * wd + by) : xmd_bytei(dst, dlen, Li, 4 * wd + by));
+    }
+    (first ? X.w0 : X.wi)[wd] = v;
+  }
+  return true;
+}
+// lane 0: hash_to_field(msg, 2) from the prepared words
+__device__ TB_NOINLINE void hash_to_field_fp2_words(fp2& u0, fp2& u1, const xmd_words& X, uint32_t n0, uint32_t ni) {
+  uint32_t b0[8], blk[16];
+  TB_UNROLL for (int i = 0; i < 8; i++) b0[i] = SHA256_ZPAD_MID[i];
+  TB_NOUNROLL for (uint32_t b = 0; b < n0; b++) {
+    TB_UNROLL for (int k = 0; k < 16; k++) blk[k] = X.w0[16 * b + k];
+    sha256_compress(b0, blk);
+  }
+  uint32_t prev[8];
+  TB_UNROLL for (int i = 0; i < 8; i++) prev[i] = b0[i];
+  fp e[4];
+  TB_UNROLL for (int j = 0; j < 4; j++) {
+    uint32_t w[16];
+    TB_UNROLL for (int half = 0; half < 2; half++) {
+      const uint32_t idx = 2 * j + half + 1;
+      uint32_t st[8];
+      TB_UNROLL for (int i = 0; i < 8; i++) st[i] = SHA256_IV[i];
+      TB_UNROLL for (int k = 0; k < 8; k++) blk[k] = idx == 1 ? b0[k] : (b0[k] ^ prev[k]);
+      TB_UNROLL for (int k = 8; k < 16; k++) blk[k] = X.wi[k];
+      blk[8] |= idx << 24;
+      sha256_compress(st, blk);
+      TB_NOUNROLL for (uint32_t b = 1; b < ni; b++) {
+        TB_UNROLL for (int k = 0; k < 16; k++) blk[k] = X.wi[16 * b + k];
+        sha256_compress(st, blk);
+      }
+      TB_UNROLL for (int i = 0; i < 8; i++) {
+        prev[i] = st[i];
+        w[half * 8 + i] = st[i];
+      }
+    }
+    e[j] = fp_from_be512_words(w);
+  }
+  u0 = {e[0], e[1]};
+  u1 = {e[2], e[3]};
+}
+
+// Q0 + Q1 on E2' (madd-2007-bl, Z1 = 1) and the 3-isogeny (tb_h2c.h
+// e2p_add_aff_aff, iso_map_jac: the same formulas) as coop products on row 0,
+// instead of one lane's (119 us at 128 sets, tools/hash_stamps_probe.py).
+// Q0.x == Q1.x (doubling or infinity) returns false: lane 0 then runs the
+// exact one-lane formulas.  p, q: LDS (the row reads their words).
+__device__ TB_INLINE bool e2p_add_iso_row(g2j& out, const g2a& p, const g2a& q, crow::rowbuf& B, const coop::cctx& K) {
+  using namespace crow;
+  const c2 px = from_fp2(p.x), py = from_fp2(p.y), qx = from_fp2(q.x), qy = from_fp2(q.y);
+  const c2 H = norm(sub(qx, px));
+  if (is_zero(H.c0, B) && is_zero(H.c1, B)) return false;
+  const c2 dy = norm(sub(qy, py));
+  const c2 r = norm(add(dy, dy));
+  const c2 HH = sqr(H, K);
+  const c2 I = norm(add(add(HH, HH), add(HH, HH)));
+  const c2 J = mul(H, I, K), V = mul(px, I, K);
+  const c2 X = norm(sub(sub(sqr(r, K), J), add(V, V)));
+  const c2 pyJ = mul(py, J, K);
+  const c2 Y = norm(sub(mul(r, norm(sub(V, X)), K), add(pyJ, pyJ)));
+  const c2 Z = norm(add(H, H));
+  // 3-isogeny, Jacobian in and out (Z != 0 here)
+  const c2 z2 = sqr(Z, K), z4 = sqr(z2, K);
+  const c2 z6 = mul(z4, z2, K);
+  const c2 zp[3] = {z6, z4, z2};  // Z^(2(3-i)), i < 3
+  c2 nx = from_const2(ISO_XNUM[3]), ny = from_const2(ISO_YNUM[3]);
+  TB_UNROLL for (int i = 2; i >= 0; i--) {
+    nx = norm(add(mul(nx, X, K), mul(from_const2(ISO_XNUM[i]), zp[i], K)));
+    ny = norm(add(mul(ny, X, K), mul(from_const2(ISO_YNUM[i]), zp[i], K)));
+  }
+  const c2 dx = norm(add(mul(norm(add(X, mul(from_const2(ISO_XDEN[1]), z2, K))), X, K), mul(from_const2(ISO_XDEN[0]), z4, K)));
+  c2 dyv = norm(add(X, mul(from_const2(ISO_YDEN[2]), z2, K)));
+  dyv = norm(add(mul(dyv, X, K), mul(from_const2(ISO_YDEN[1]), z4, K)));
+  dyv = norm(add(mul(dyv, X, K), mul(from_const2(ISO_YDEN[0]), z6, K)));
+  const c2 dy2 = sqr(dyv, K), dxdy = mul(dx, dyv, K);
+  const c2 oz = mul(Z, dxdy, K);
+  const c2 ox = mul(nx, mul(dyv, dxdy, K), K);
+  const c2 dx2 = sqr(dx, K);
+  const c2 oy = mul(mul(Y, ny, K), mul(mul(dx2, dx, K), dy2, K), K);
+  const fp2 fx = to_fp2(ox, B), fy = to_fp2(oy, B), fz = to_fp2(oz, B);
+  if (dig() == 0) {
+    out.x = fx;
+    out.y = fy;
+    out.z = fz;
+  }
+  return true;
+}
+
 struct hcoop_lds {
   cdig S[CF_NSLOT];
   uint16_t tab[CF_TAB_N];
@@ -69,6 +230,7 @@ struct hcoop_lds {
   fp res[6];
   g2a qa;  // the affine H(m) before [r] (rand != nullptr)
   int ok;
+  xmd_words X;
 };
 
 extern "C" __global__ void __launch_bounds__(256)
@@ -78,26 +240,42 @@ extern "C" __global__ void __launch_bounds__(256)
   const uint32_t i = blockIdx.x;
   if (i >= n) return;
   tb_latency_prio();
+  HSTAMP(0);
   const coop::cctx K = coop::cctx_load();
   const int g = crow::row(), d = crow::dig();
   for (int j = threadIdx.x; j < CF_TAB_N; j += blockDim.x) L.tab[j] = CF_TAB[j];
   for (int j = threadIdx.x; j < CF_NSLOT * 16; j += blockDim.x) (&L.S[0][0])[j] = 0;
+  uint32_t n0, ni;
+  const uint32_t mlen = msg_off[i + 1] - msg_off[i];
+  const bool words = xmd_words_fill(L.X, msgs + msg_off[i], mlen, dst, dlen, n0, ni);
+  __syncthreads();
   if (threadIdx.x == 0) {
-    xmd_ctx c;
-    c.msg = msgs + msg_off[i];
-    c.mlen = msg_off[i + 1] - msg_off[i];
-    c.dst = dst;
-    c.dlen = dlen;
-    hash_to_field_fp2(L.u[0], L.u[1], c);
+    if (words) {
+      hash_to_field_fp2_words(L.u[0], L.u[1], L.X, n0, ni);
+    } else {
+      xmd_ctx c;
+      c.msg = msgs + msg_off[i];
+      c.mlen = mlen;
+      c.dst = dst;
+      c.dlen = dlen;
+      hash_to_field_fp2(L.u[0], L.u[1], c);
+    }
   }
   __syncthreads();
+  HSTAMP(1);
   if (g < 2) {
     const g2a q = crow::sswu(L.u[g], L.rb[g], K);
     if (d == 0) L.qm[g] = q;
   }
   __syncthreads();
-  if (threadIdx.x == 0) L.J = iso_map_jac(e2p_add_aff_aff(L.qm[0], L.qm[1]));
+  HSTAMP(2);
+  {
+    bool done = true;
+    if (g == 0) done = e2p_add_iso_row(L.J, L.qm[0], L.qm[1], L.rb[0], K);
+    if (threadIdx.x == 0 && !done) L.J = iso_map_jac(e2p_add_aff_aff(L.qm[0], L.qm[1]));
+  }
   __syncthreads();
+  HSTAMP(3);
   // slots: the point (Jacobian, Fp2 coordinates) and the psi constants
   if (g < 6) {
     const fp* jw = g < 2 ? &L.J.x.c0 : (g < 4 ? &L.J.y.c0 : &L.J.z.c0);
@@ -108,12 +286,15 @@ extern "C" __global__ void __launch_bounds__(256)
     L.S[slot][d] = coop::cfrom_words(cw);
   }
   __syncthreads();
+  HSTAMP(4);
   for (int k = 0; k < CF_NLEVEL; k++) crow::level<2, 2, CF_AMAX, CF_BMAX, CF_QMAX * CF_OMAX>(L.S, L.tab, CF_TYPE_OFF[CF_SEQ[k]], K);
   if (g < 6) {
     const fp v = crow::to_fp(L.S[CF_S_RX0 + g][d], L.rb[g].d, &L.rb[g].f);
     if (d == 0) L.res[g] = v;
   }
+  HSTAMP(5);
   __syncthreads();
+  HSTAMP(6);
   if (threadIdx.x == 0) {
     const fp2 X = {L.res[0], L.res[1]}, Y = {L.res[2], L.res[3]}, Z = {L.res[4], L.res[5]};
     g2a a;
@@ -122,6 +303,7 @@ extern "C" __global__ void __launch_bounds__(256)
       ok = jac_to_aff(a, g2_clear_cofactor(L.J));
     } else {
       const fp2 zi = fp2_inv(Z);
+      HSTAMP(8);
       a.x = fp2_mul(X, zi);
       a.y = fp2_mul(Y, zi);
     }
@@ -135,6 +317,7 @@ extern "C" __global__ void __launch_bounds__(256)
     L.ok = ok ? 1 : 0;
     skip[i] = ok ? 0 : 1;
   }
+  HSTAMP(7);
   // Multi-key batches (tb_lib.hip launch_partial, r on G2): the set's
   // randomizer multiplies H(m) here instead of the aggregate key (e(apk,
   // [r] H) = e([r] apk, H)), on row 0 with coop mixed additions -- the hash

@@ -8,7 +8,7 @@ k_set_hash is its one-wave A/B twin), k_set_hash_duo + k_set_hash_fix
 k_set_hash_quad + k_set_hash_fix (1,025 - 8,192), the row pipeline k_hrow_*
 (513 - 1,024) and k_set_hash_coop (<= 512; k_set_hash_wave is its
 fall-back).  Each one runs here on the same 640
-messages -- empty, 200-byte, random lengths up to 256 bytes -- under the
+messages -- empty, 200-byte, 768-byte, random lengths up to 256 bytes -- under the
 Ethereum POP DST and the NUL DST (BLSTest.java:375-391), through the test
 library's hook (tests/native/k_test_hash.hip), which launches the PRODUCT
 library's kernels, and its compressed H(m) is compared byte for byte with the
@@ -38,7 +38,8 @@ VARIANTS = {0: "k_set_hash", 2: "k_hrow_*", 3: "k_set_hash_coop", 4: "k_set_hash
 
 def messages():
     rng = random.Random(2024)
-    ms = [b"", bytes(200), bytes(range(200)), b"abc", bytes([0xFF]) * 256]
+    # 768 bytes: past k_set_hash_coop's LDS message words (XW0_MAX blocks), its byte path
+    ms = [b"", bytes(200), bytes(range(200)), b"abc", bytes([0xFF]) * 256, bytes(range(256)) * 3]
     while len(ms) < 640:
         ms.append(bytes(rng.getrandbits(8) for _ in range(rng.choice([0, 1, 31, 32, 33, 55, 56, 63, 64, 65, 119, 120, 200, 256]))))
     return ms
