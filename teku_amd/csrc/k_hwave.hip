@@ -263,9 +263,12 @@ extern "C" __global__ void __launch_bounds__(256)
   }
   __syncthreads();
   HSTAMP(1);
-  if (g < 2) {
-    const g2a q = crow::sswu(L.u[g], L.rb[g], K);
-    if (d == 0) L.qm[g] = q;
+  // map m on row 4 m: the first row of waves 0 and 1, each the only active
+  // row of its wave, so the row inversion's divsteps run on the scalar unit
+  if (g == 0 || g == 4) {
+    const int m = g >> 2;
+    const g2a q = crow::sswu<true>(L.u[m], L.rb[g], K);
+    if (d == 0) L.qm[m] = q;
   }
   __syncthreads();
   HSTAMP(2);
@@ -295,17 +298,28 @@ extern "C" __global__ void __launch_bounds__(256)
   HSTAMP(5);
   __syncthreads();
   HSTAMP(6);
+  // (X : Y : Z) -> affine on row 0: Z^-1 by the row (crow::inv, tb_cinv.h),
+  // two coop products (round 5: lane 0's fp2_inv, 118 us at 128 sets)
+  const bool zinf = fp2_is_zero(fp2{L.res[4], L.res[5]});
+  if (g == 0 && !zinf) {
+    const fp2* R2 = reinterpret_cast<const fp2*>(L.res);  // X, Y, Z (LDS: the row reads their words)
+    const crow::c2 zi = crow::inv<true>(crow::from_fp2(R2[2]), L.rb[0], K);
+    const fp2 ax = crow::to_fp2(crow::mul(crow::from_fp2(R2[0]), zi, K), L.rb[0]);
+    const fp2 ay = crow::to_fp2(crow::mul(crow::from_fp2(R2[1]), zi, K), L.rb[0]);
+    if (d == 0) {
+      L.qa.x = ax;
+      L.qa.y = ay;
+    }
+  }
+  __syncthreads();
+  HSTAMP(8);
   if (threadIdx.x == 0) {
-    const fp2 X = {L.res[0], L.res[1]}, Y = {L.res[2], L.res[3]}, Z = {L.res[4], L.res[5]};
     g2a a;
     bool ok = true;
-    if (fp2_is_zero(Z)) {
+    if (zinf) {
       ok = jac_to_aff(a, g2_clear_cofactor(L.J));
     } else {
-      const fp2 zi = fp2_inv(Z);
-      HSTAMP(8);
-      a.x = fp2_mul(X, zi);
-      a.y = fp2_mul(Y, zi);
+      a = L.qa;
     }
     if (!ok) {
       a.x = fp2_zero();
@@ -330,7 +344,7 @@ extern "C" __global__ void __launch_bounds__(256)
     if (g == 0 && L.ok && r > 1) {
       const crow::c2 one2 = {crow::from_const(R1), coop::c32(0)};
       const coop::cj2 t = coop::mul_u64_aff(crow::from_fp2(L.qa.x), crow::from_fp2(L.qa.y), r, one2, K);
-      const crow::c2 zi = crow::inv(t.z, L.rb[0], K);
+      const crow::c2 zi = crow::inv<true>(t.z, L.rb[0], K);
       const crow::c2 zi2 = crow::sqr(zi, K);
       const crow::c2 zi3 = crow::mul(zi2, zi, K);
       const crow::c2 ax = crow::mul(t.x, zi2, K), ay = crow::mul(t.y, zi3, K);

@@ -162,7 +162,10 @@ extern "C" __global__ void __launch_bounds__(128)
     const c32 zc = cacc.z;
     const c32 v1[1] = {coop::cmul(t.z, zc, K)};
     crow::to_fp_n<1>(v1, M.zb1, &M.inv);
-    if (d == 0) M.inv = fp_inv(M.inv);
+    {
+      const fp z = cinv::inv_row_lane0(M.inv, M.zb1[0]);  // the row's inversion (tb_cinv.h)
+      if (d == 0) M.inv = z;
+    }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     const c32 iv = crow::from_fp(M.inv);
@@ -400,7 +403,10 @@ __device__ TB_INLINE void ka_tree(ka_set& S, int rows, int q, int d, const coop:
 __device__ TB_INLINE void ka_affine(const coop::cj1& t, int32_t (*zb)[16], fp& inv, fp* out, int d, const coop::cctx& K) {
   const c32 v1[1] = {t.z};
   crow::to_fp_n<1>(v1, zb, &inv);
-  if (d == 0) inv = fp_inv(inv);
+  {
+    const fp z = cinv::inv_row_lane0(inv, zb[0]);  // the row's inversion (tb_cinv.h)
+    if (d == 0) inv = z;
+  }
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
   const c32 i1 = crow::from_fp(inv);

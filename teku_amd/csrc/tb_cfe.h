@@ -16,6 +16,7 @@
 // of a lone lane's Fp product plus its sums (10-14k cycles).
 // The easy part's Fp12 inversion stays on one lane (fp12_inv, tb_tower.h).
 #pragma once
+#include "tb_cinv.h"
 #include "tb_coop.h"
 #include "tb_fp12_wave.h"
 
@@ -281,7 +282,10 @@ __device__ TB_INLINE void inv(cdig* dst, const cdig* x, cfe_lds& L, const cfe_re
   __syncthreads();
   if (g == 0) L.prod[2][d] = creduce64((c64)L.prod[0][d] + (c64)L.prod[1][d], R.K.plo[0]);
   __syncthreads();
-  if (threadIdx.x == 0) L.tmp[0] = fp_inv(coop::cdigits_to_fp(L.prod[2]));
+  if (g == 0) {  // n^-1 by row 0 (tb_cinv.h; prod[3] is its lane buffer)
+    const fp z = cinv::inv_row_lane0<true>(coop::cdigits_to_fp(L.prod[2]), L.prod[3]);
+    if (d == 0) L.tmp[0] = z;
+  }
   __syncthreads();
   // w = conj2(v) / n: coordinates 0, 1 (rows 0, 1), zero elsewhere
   const c32 ninv = coop::cfrom_words(L.tmp[0].l);

@@ -14,6 +14,7 @@
 // (creduce64) into its slot.  The slot values stay |v| < 2.6 p, the operand
 // sums below 2^395 (the generators cap sum |coef| of an operand at 4096).
 #pragma once
+#include "tb_cinv.h"
 #include "tb_coop.h"
 #include "tb_cpoint.h"
 #include "tb_fp12_wave.h"
@@ -101,14 +102,14 @@ __device__ TB_INLINE fp2 to_fp2(const c2& a, rowbuf& B) {
   return r;
 }
 
-// a^-1 in Fp2: conj(a) / N(a), the Fp inversion on the row's lane 0
+// a^-1 in Fp2: conj(a) / N(a), the Fp inversion by the whole row (tb_cinv.h;
+// round 5 ran fp_inv on the row's lane 0: ~105 us at 128 sets)
+// (U: the row is the only active row of its wave, tb_cinv.h)
+template <bool U = false>
 __device__ TB_INLINE c2 inv(const c2& a, rowbuf& B, const cctx& K) {
   const fp n = to_fp(norm2(a, K), B.d, &B.f);
-#if defined(TB_ROW_INV_INLINE)  // k_hrow.hip: keep the kernel's 256-register bound
-  if (dig() == 0) B.f = fp_inv_body(n);
-#else
-  if (dig() == 0) B.f = fp_inv(n);
-#endif
+  const fp z = cinv::inv_row_lane0<U>(n, B.d);
+  if (dig() == 0) B.f = z;
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
   const c32 ni = from_fp(B.f);
@@ -121,6 +122,7 @@ __device__ TB_INLINE c2 inv(const c2& a, rowbuf& B, const cctx& K) {
 // chains; the canonical tests (exceptional tv, squareness, delta = 0, chi = 1,
 // sgn0) go through the row buffer.  Returns the affine point in [0, 2p).
 // u_in: LDS (the row reads its words)
+template <bool U = false>
 __device__ TB_INLINE g2a sswu(const fp2& u_in, rowbuf& B, const cctx& K) {
   const c2 u = from_fp2(u_in);
   const c2 A = from_const2(SSWU_A), Bc = from_const2(SSWU_B);
@@ -130,7 +132,7 @@ __device__ TB_INLINE g2a sswu(const fp2& u_in, rowbuf& B, const cctx& K) {
   const bool exc = fp2_is_zero(tvf);
   const c2 one2 = {from_const(R1), c32(0)};
   const c2 tvs = exc ? one2 : tv;
-  const c2 ti = inv(tvs, B, K);
+  const c2 ti = inv<U>(tvs, B, K);
   c2 x1 = mul(from_const2(SSWU_MINUS_B_OVER_A), norm(add(one2, ti)), K);
   if (exc) x1 = from_const2(SSWU_B_OVER_ZA);
   const c2 gx1 = norm(add(mul(norm(add(sqr(x1, K), A)), x1, K), Bc));

@@ -112,6 +112,7 @@ extern "C" __global__ void __launch_bounds__(64) k_test_wave_timing(const uint8_
 // lane-cooperative kernels (tests/native/k_test_coop.hip, its own TU)
 extern "C" __global__ void k_test_coop_mul(const uint8_t* in, uint8_t* out, uint32_t n);
 extern "C" __global__ void k_test_coop_timing(const uint8_t* in, uint8_t* out);
+extern "C" __global__ void k_test_coop_inv(const uint8_t* in, uint8_t* out, uint32_t n);
 extern "C" __global__ void k_test_final_exp_coop(const uint8_t* in, uint8_t* out);
 extern "C" __global__ void k_test_cfe_ops(const uint8_t* in, uint8_t* out);
 
@@ -119,6 +120,7 @@ extern "C" __global__ void k_test_cfe_ops(const uint8_t* in, uint8_t* out);
 #define TOP_CFE_OPS 46
 #define TOP_COOP_MUL 43
 #define TOP_COOP_TIMING 44
+#define TOP_COOP_INV 47
 #define TOP_FINAL_EXP_WAVE 29
 #define TOP_MILLER_WAVE 31
 #define TOP_MILLER_PROG 40  // tb_testops.h uses 1..35
@@ -149,6 +151,8 @@ extern "C" int tbls_test_ops(int op, const uint8_t* in, uint8_t* out, size_t n) 
       hipLaunchKernelGGL(k_test_coop_mul, dim3((uint32_t)((n + 3) / 4)), dim3(64), 0, 0, din, dout, (uint32_t)n);
     else if (op == TOP_COOP_TIMING)
       hipLaunchKernelGGL(k_test_coop_timing, dim3(1), dim3(64), 0, 0, din, dout);
+    else if (op == TOP_COOP_INV)
+      hipLaunchKernelGGL(k_test_coop_inv, dim3((uint32_t)((n + 3) / 4)), dim3(64), 0, 0, din, dout, (uint32_t)n);
     else if (op == TOP_CLEAR_COF_PROG)
       hipLaunchKernelGGL(k_test_clear_cof_prog, dim3((uint32_t)n), dim3(64), 0, 0, din, dout);
     else if (test_op_in_a(op))

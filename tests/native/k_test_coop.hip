@@ -4,6 +4,7 @@
 #include "../../teku_amd/csrc/tb_kdecl.h"
 #include "tb_testops.h"
 #include "../../teku_amd/csrc/tb_cfe.h"
+#include "../../teku_amd/csrc/tb_cinv.h"
 
 using namespace tb;
 
@@ -163,5 +164,30 @@ extern "C" __global__ void __launch_bounds__(256) k_test_cfe_ops(const uint8_t* 
     t[0] = (uint64_t)(c[1] - c[0]);
     t[1] = (uint64_t)(c[2] - c[1]);
     t[2] = (uint64_t)(c[3] - c[2]);
+  }
+}
+
+// the row inversion (tb_cinv.h): one inversion per 16-lane row, record = a
+// (48 B), out = a^-1 (48 B) at +0; record 0's row also times one row
+// inversion and one lone-lane fp_inv (clock64 cycles, u64 at +48 / +56)
+extern "C" __global__ void __launch_bounds__(64) k_test_coop_inv(const uint8_t* in, uint8_t* out, uint32_t n) {
+  __shared__ int32_t D[4][16];
+  const uint32_t row = threadIdx.x >> 4, rec = blockIdx.x * 4 + row;
+  const bool live = rec < n;
+  const fp a = tio_fp(in + (size_t)(live ? rec : 0) * TB_TEST_IN);  // every lane decodes the same record
+  const long long t0 = clock64();
+  const fp z = cinv::inv_row_lane0(a, D[row]);
+  const long long t1 = clock64();
+  fp y = a;
+  if (rec == 0 && (threadIdx.x & 15) == 0) y = fp_inv(a);
+  const long long t2 = clock64();
+  if (live && (threadIdx.x & 15) == 0) {
+    tio_put_fp(out + (size_t)rec * TB_TEST_OUT, z);
+    if (rec == 0) {
+      uint64_t* o = reinterpret_cast<uint64_t*>(out + 48);
+      o[0] = (uint64_t)(t1 - t0);
+      o[1] = (uint64_t)(t2 - t1);
+      tio_put_fp(out + 64, y);
+    }
   }
 }

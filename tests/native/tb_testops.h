@@ -8,6 +8,7 @@
 // affine points x||y.
 #pragma once
 #include "../../teku_amd/csrc/tb_stages.h"
+#include "../../teku_amd/csrc/tb_cinv.h"
 
 namespace tb {
 
@@ -52,6 +53,9 @@ enum {
   TOP_CLEAR_COF_NX = 36,
   // the subgroup check with the branch-free [|x|] (g2_in_group_nx): u32 verdict
   TOP_G2_IN_GROUP_NX = 37,
+  // the row inversion (tb_cinv.h) -- host emulation only (the GPU form is the
+  // per-row k_test_coop_inv, op 47)
+  TOP_FP_INV_ROW = 38,
 };
 
 #define TB_TEST_IN 1536
@@ -147,6 +151,11 @@ TB_HD TB_INLINE bool test_op_a(int op, const uint8_t* in, uint8_t* out) {
     case TOP_FP_INV:
       tio_put_fp(out, fp_inv(tio_fp(in)));
       break;
+#if !defined(__HIPCC__)
+    case TOP_FP_INV_ROW:
+      tio_put_fp(out, cinv::inv_row_lane0(tio_fp(in), nullptr));
+      break;
+#endif
     case TOP_FP2_MUL:
       tio_put_fp2(out, fp2_mul(tio_fp2(in), tio_fp2(in + 96)));
       break;

@@ -17,7 +17,7 @@ TEST_OUT = 640
 OPS = dict(
     FP_MUL=1, FP_INV=2, FP2_MUL=3, FP2_SQRT=4, FP12_MUL=5, FP12_CYC_SQR=6, FP12_FROB=7, FINAL_EXP=8,
     MILLER=9, G1_DECOMP=10, G2_DECOMP=11, HASH_TO_G2=12, G1_IN_GROUP=13, G2_IN_GROUP=14, SSWU=15,
-    ISO=16, CLEAR_COF=17, FP12_SQR=18, FP12_INV=19, HASH_TO_FIELD=20, FP_SQR=21, FP_ADD=22, FP_SUB=23, FINAL_EXP_WAVE=29, MILLER2=30, MILLER_WAVE=31, MILLER_PROG=40, CLEAR_COF_PROG=41, WAVE_TIMING=42, COOP_MUL=43, COOP_TIMING=44, FINAL_EXP_COOP=45, CFE_OPS=46,
+    ISO=16, CLEAR_COF=17, FP12_SQR=18, FP12_INV=19, HASH_TO_FIELD=20, FP_SQR=21, FP_ADD=22, FP_SUB=23, FINAL_EXP_WAVE=29, MILLER2=30, MILLER_WAVE=31, MILLER_PROG=40, CLEAR_COF_PROG=41, WAVE_TIMING=42, COOP_MUL=43, COOP_TIMING=44, COOP_INV=47, FP_INV_ROW=38, FINAL_EXP_COOP=45, CFE_OPS=46,
     FP_MUL_RAW=32, FP_SQR_RAW=33, FP2_MUL_RAW=34, FP2_SQR_RAW=35, CLEAR_COF_NX=36, G2_IN_GROUP_NX=37, STAGE_PK=24, STAGE_SET_PK=25, STAGE_SET_SIG=26, STAGE_SET_HASH=27, G2_JADD=28,
 )
 

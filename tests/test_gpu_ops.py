@@ -215,6 +215,22 @@ def test_coop_mul_and_timing(run):
     assert int.from_bytes(o[160:208], "big") == a * pow(b, 64, O.P) % O.P
 
 
+def test_coop_row_inversion(run):
+    """tb_cinv.h on the GPU: one Bernstein-Yang inversion per 16-lane row
+    equals pow(a, -1, p) (0 -> 0), short inputs included; record 0's row also
+    times one row inversion against the lone-lane fp_inv (printed) and checks
+    that fp_inv agrees."""
+    rng = _rng()
+    A = [rng.randrange(O.P) for _ in range(100)] + [0, 1, 2, O.P - 1, O.P - 2, 1 << 380]
+    A += [rng.randrange(1 << rng.randrange(1, 381)) for _ in range(30)]
+    out = run("COOP_INV", [enc_fp(a) for a in A])
+    assert [dec_fp(x[:48]) for x in out] == [pow(a, -1, O.P) if a else 0 for a in A]
+    o = out[0]
+    cyc = [int.from_bytes(o[48 + 8 * i : 56 + 8 * i], "little") for i in range(2)]
+    print("\nFp inversion cycles: coop row %d, lone-lane fp_inv %d" % tuple(cyc))
+    assert int.from_bytes(o[64:112], "big") == pow(A[0], -1, O.P)
+
+
 def test_cfe_ops(run):
     """Single lane-cooperative Fp12 ops (tb_cfe.h) vs the oracle: product,
     cyclotomic squaring (on f^((p^6-1)(p^2+1))), Frobenius, conjugation."""

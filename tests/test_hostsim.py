@@ -39,6 +39,18 @@ def test_fp(run):
     assert [dec_fp(x) for x in run("FP_SUB", recs)] == [(a - b) % O.P for a, b in zip(A, B)]
 
 
+def test_fp_inv_row(run):
+    """tb_cinv.h: the coop-row Bernstein-Yang inversion (host emulation of the
+    16 lanes) against pow(a, -1, p), and against the lone-lane fp_inv; 0 -> 0."""
+    rng = random.Random(11)
+    A = [rng.randrange(O.P) for _ in range(300)] + [0, 1, 2, 3, O.P - 1, O.P - 2, (O.P - 1) // 2, 1 << 380, (1 << 381) % O.P]
+    A += [rng.randrange(1 << rng.randrange(1, 381)) for _ in range(60)]  # short values: long runs of zero bits
+    recs = [enc_fp(a) for a in A]
+    got = [dec_fp(x) for x in run("FP_INV_ROW", recs)]
+    assert got == [pow(a, -1, O.P) if a else 0 for a in A]
+    assert got == [dec_fp(x) for x in run("FP_INV", recs)]
+
+
 def test_tower(run):
     rng = random.Random(6)
     rf2 = lambda: (rng.randrange(O.P), rng.randrange(O.P))  # noqa: E731

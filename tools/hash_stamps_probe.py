@@ -14,7 +14,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-PHASES = ["start->field (lane 0: expand_message_xmd, hash_to_field)", "field->sswu (rows 0-1: two SSWU maps)",
+PHASES = ["start->field (lane 0: expand_message_xmd, hash_to_field)", "field->sswu (rows 0 and 4: two SSWU maps)",
           "sswu->iso (lane 0: E2' addition + 3-isogeny)", "iso->slots (slot setup)", "slots->levels (cofactor program)",
           "levels->to_fp (barrier)", "to_fp->end (lane 0: affine conversion)"]
 
@@ -44,7 +44,7 @@ def main():
             tot.append((t[7] - t[0]) / 100.0)
             inv.append((buf[16 * i + 8] - t[6]) / 100.0)
     out = {"n": n, "reps": reps, "phase_us_median": {p: statistics.median(v) for p, v in per.items()}, "total_us_median": statistics.median(tot),
-           "to_fp->after fp2_inv (lane 0)": statistics.median(inv)}
+           "to_fp->affine (row 0: row inversion + 2 coop products)": statistics.median(inv)}
     print(json.dumps(out, indent=1), flush=True)
 
 
