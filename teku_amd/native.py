@@ -8,6 +8,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import sys
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -210,6 +211,11 @@ def _preload_process_hip_runtime():
     and RTLD_GLOBAL, makes every later request resolve to that one copy: this
     library's soname request matches it, and torch's own load finds the same
     file already mapped.  A process without torch keeps the system runtime.
+    The library is built against /opt/rocm's HIP: torch's copy is taken only
+    when its ROCm major version (the "+rocmX.Y" of torch's package version,
+    read from its metadata, nothing loaded) equals the build's (/opt/rocm/.info/
+    version), or when torch is already imported (its runtime is then the
+    process's in any case); otherwise the system runtime stays.
     TBLS_HIP_PRELOAD=0 disables this (diagnostics)."""
     if os.environ.get("TBLS_HIP_PRELOAD", "1") == "0" or _loaded_hip_runtimes():
         return
@@ -221,9 +227,33 @@ def _preload_process_hip_runtime():
         spec = None
     if spec is None or not spec.origin:
         return
+    if "torch" not in sys.modules and not _same_rocm_major():
+        return
     rt = os.path.join(os.path.dirname(spec.origin), "lib", "libamdhip64.so")
     if os.path.exists(rt):
         ctypes.CDLL(rt, mode=ctypes.RTLD_GLOBAL)
+
+
+def _rocm_major(version: str):
+    """Major version from "7.2.0" or a "+rocm7.0" local version tag (None if absent)."""
+    import re
+
+    m = re.search(r"(?:rocm)?(\d+)\.\d+", version.split("+rocm", 1)[1] if "+rocm" in version else version)
+    return int(m.group(1)) if m else None
+
+
+def _same_rocm_major() -> bool:
+    """torch's ROCm major version equals /opt/rocm's (the build's)."""
+    try:
+        import importlib.metadata
+
+        t = importlib.metadata.version("torch")
+        tv = _rocm_major(t) if "+rocm" in t else None  # a CUDA or CPU build of torch: no HIP runtime to share
+        with open(os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), ".info", "version")) as f:
+            sv = _rocm_major(f.read().strip())
+    except (OSError, ImportError, ValueError):
+        return False
+    return tv is not None and tv == sv
 
 
 def load_library(path: str = LIB_PATH):
