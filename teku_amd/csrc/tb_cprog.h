@@ -173,17 +173,41 @@ __device__ TB_INLINE g2a sswu(const fp2& u_in, rowbuf& B, const cctx& K) {
 }
 
 // ---- level programs ---------------------------------------------------------
-// sum of the terms [b, e) of a level's entry list: coef * S[slot][d]
-__device__ TB_INLINE c64 psum(const cdig* S, const uint16_t* ent, int b, int e, int maxlen) {
+// sum of the terms [b, e) of a level's entry list: coef * S[slot][d].  All
+// MAXLEN entries are loaded at once (past e: slot 0, coefficient 0), then all
+// their slot values, then the multiply-adds: two LDS latencies per sum
+// instead of two per term (the loop that stopped at e chained them: ~60 % of
+// a level's 4.6k cycles in k_set_hash_coop's cofactor program, 302 levels).
+template <int MAXLEN>
+__device__ TB_INLINE c64 psum(const cdig* S, const uint16_t* ent, int b, int e) {
   const int d = dig();
-  c64 acc = 0;
-  for (int t = 0; t < maxlen; t++) {
-    if (b + t >= e) break;
-    const uint32_t slot = ent[2 * (b + t)];
-    const int32_t cf = (int16_t)ent[2 * (b + t) + 1];
-    acc += coop::mulw(S[slot][d], cf);
+  uint32_t sl[MAXLEN];
+  int32_t cf[MAXLEN];
+  TB_UNROLL for (int t = 0; t < MAXLEN; t++) {
+    const bool v = b + t < e;
+    const int i = v ? b + t : 0;
+    const uint32_t s0 = ent[2 * i];
+    const int32_t c0 = (int16_t)ent[2 * i + 1];
+    sl[t] = v ? s0 : 0u;
+    cf[t] = v ? c0 : 0;
   }
+  c32 x[MAXLEN];
+  TB_UNROLL for (int t = 0; t < MAXLEN; t++) x[t] = S[sl[t]][d];
+  c64 acc = 0;
+  TB_UNROLL for (int t = 0; t < MAXLEN; t++) acc += coop::mulw(x[t], cf[t]);
   return acc;
+}
+
+// pr[0..N) = xa[k] xb[k], the N products interleaved
+template <int N, int KP>
+__device__ TB_INLINE void cmul_first(c32 (&pr)[KP], const c32 (&xa)[KP], const c32 (&xb)[KP], const cctx& K) {
+  c32 a[N], b[N], r[N];
+  TB_UNROLL for (int k = 0; k < N; k++) {
+    a[k] = xa[k];
+    b[k] = xb[k];
+  }
+  coop::cmul_n<N>(r, a, b, K);
+  TB_UNROLL for (int k = 0; k < N; k++) pr[k] = r[k];
 }
 
 // one level of a generated program on 16 rows (tables in LDS at tab + off)
@@ -199,18 +223,31 @@ __device__ TB_INLINE void level(cdig* S, const uint16_t* tab, int off, const cct
   const uint16_t* obeg = qbeg + nq + 1;
   const uint16_t* odst = obeg + no + 1;
   const uint16_t* ent = odst + no;
-  c32 pr[KP];
+  c32 pr[KP], xa[KP], xb[KP];
   TB_UNROLL for (int k = 0; k < KP; k++) {
+    xa[k] = 0;
+    xb[k] = 0;
     if (16 * k < np) {  // uniform: skip whole rounds with no product
       const int t = g + 16 * k;
       c64 sa = 0, sb = 0;
       if (t < np) {
-        sa = psum(S, ent, abeg[t], abeg[t + 1], AMAX);
-        sb = psum(S, ent, bbeg[t], bbeg[t + 1], BMAX);
+        sa = psum<AMAX>(S, ent, abeg[t], abeg[t + 1]);
+        sb = psum<BMAX>(S, ent, bbeg[t], bbeg[t + 1]);
       }
-      pr[k] = coop::cmul(coop::cnorm64(sa), coop::cnorm64(sb), K);
+      xa[k] = coop::cnorm64(sa);
+      xb[k] = coop::cnorm64(sb);
     }
   }
+  // a row's products of all active rounds interleaved (two: 1,136 cycles
+  // against 2 x 1,069 one after the other, tests/test_gpu_ops.py timing)
+  const int nr = (np + 15) / 16;  // uniform
+  if (nr == 1) pr[0] = coop::cmul(xa[0], xb[0], K);
+  if constexpr (KP >= 2)
+    if (nr == 2) cmul_first<2>(pr, xa, xb, K);
+  if constexpr (KP >= 3)
+    if (nr == 3) cmul_first<3>(pr, xa, xb, K);
+  if constexpr (KP >= 4)
+    if (nr == 4) cmul_first<4>(pr, xa, xb, K);
   TB_UNROLL for (int k = 0; k < KP; k++) {
     const int t = g + 16 * k;
     if (16 * k < np && t < np) S[pout[t]][d] = pr[k];
@@ -222,7 +259,7 @@ __device__ TB_INLINE void level(cdig* S, const uint16_t* tab, int off, const cct
     out[k] = 0;
     if (16 * k < no && o < no) {
       const int j0 = obeg[o], j1 = obeg[o + 1];
-      out[k] = coop::creduce64(psum(S, ent, qbeg[j0], qbeg[j1], OTERMS), K.plo[0]);
+      out[k] = coop::creduce64(psum<OTERMS>(S, ent, qbeg[j0], qbeg[j1]), K.plo[0]);
     }
   }
   __syncthreads();

@@ -40,16 +40,24 @@ __device__ TB_INLINE void cs_term_pos(c13& a, const fp& v, uint32_t m) {
   TB_UNROLL for (int i = 0; i < 12; i++) a.c[i] = (uint64_t)v.l[i] * m + a.c[i];
 }
 
-// acc += sum over entries [b, e) of coef * S[slot] (carry-save columns)
+// acc += sum over entries [b, e) of coef * S[slot] (carry-save columns).
+// Every entry and slot value up to MAXLEN is loaded first (past e: entry 0,
+// never added), then the terms are added: the LDS latencies overlap instead
+// of one entry -> value -> multiply-add round trip per term.
 template <int MAXLEN, int NSLOT>
 __device__ TB_INLINE void mp_csum(c13& acc, const fp* S, const uint16_t* ent, int b, int e) {
+  uint32_t sl[MAXLEN], m[MAXLEN];
   TB_UNROLL for (int t = 0; t < MAXLEN; t++) {
-    if (b + t < e) {
-      const uint32_t slot = ent[2 * (b + t)];
-      const int c = (int16_t)ent[2 * (b + t) + 1];
-      cs_term_pos(acc, S[c < 0 ? NSLOT + slot : slot], (uint32_t)(c < 0 ? -c : c));
-    }
+    const int i = b + t < e ? b + t : 0;
+    const uint32_t slot = ent[2 * i];
+    const int c = (int16_t)ent[2 * i + 1];
+    sl[t] = c < 0 ? NSLOT + slot : slot;
+    m[t] = (uint32_t)(c < 0 ? -c : c);
   }
+  fp v[MAXLEN];
+  TB_UNROLL for (int t = 0; t < MAXLEN; t++) v[t] = S[sl[t]];
+  TB_UNROLL for (int t = 0; t < MAXLEN; t++)
+    if (b + t < e) cs_term_pos(acc, v[t], m[t]);
 }
 
 // negated copies of slots [0, NSLOT) after an initialization (whole workgroup)
