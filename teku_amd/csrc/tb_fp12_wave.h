@@ -103,14 +103,31 @@ __device__ TB_INLINE u13 cs_norm(const c13& a) {
 
 // acc += (x & 1 ? -src[x >> 1] : src[x >> 1]) over the entries [b, e) (at most
 // MAXLEN; unrolled and predicated so the LDS reads issue early)
+#ifndef TB_WCS_PIPE
+#define TB_WCS_PIPE 1
+#endif
 template <int MAXLEN>
 __device__ TB_INLINE void w_cs_sum(c13& acc, const fp* src, const uint16_t* ent, int b, int e) {
+#if !TB_WCS_PIPE  // A/B: one term after another
   TB_UNROLL for (int t = 0; t < MAXLEN; t++) {
     if (b + t < e) {
       const uint32_t x = ent[b + t];
       cs_term(acc, src[x >> 1], 1u, (x & 1u) != 0);
     }
   }
+  return;
+#endif
+  // every entry, then every value, loaded before the first term is added
+  // (entries past e read entry 0 and are not added): the LDS latencies
+  // overlap instead of chaining entry -> value -> add per term
+  if constexpr (MAXLEN == 0) return;
+  constexpr int N = MAXLEN > 0 ? MAXLEN : 1;
+  uint32_t x[N];
+  TB_UNROLL for (int t = 0; t < MAXLEN; t++) x[t] = ent[b + t < e ? b + t : 0];
+  fp v[N];
+  TB_UNROLL for (int t = 0; t < MAXLEN; t++) v[t] = src[x[t] >> 1];
+  TB_UNROLL for (int t = 0; t < MAXLEN; t++)
+    if (b + t < e) cs_term(acc, v[t], 1u, (x[t] & 1u) != 0);
 }
 
 // Montgomery product of two 13-limb values < 2^406 (output < 2p)

@@ -424,6 +424,15 @@ static int line_group(uint32_t n_main) {
   return 1;
 }
 
+// Values per wave of the unsegmented product levels (k_fp12_prod_wave): a
+// wave multiplies its chunk one value after another, so small batches (the
+// latency path) take 4 (256 pairs: 4 levels of 3 products, against 2 levels
+// of 15 with 16); larger unsegmented batches keep TB_PROD_CHUNK.
+#ifndef TB_PROD_SMALL_MAX
+#define TB_PROD_SMALL_MAX 4096u
+#endif
+static uint32_t prod_chunk(const pair_plan& pp) { return !pp.seg() && pp.n_f() <= TB_PROD_SMALL_MAX ? 4u : TB_PROD_CHUNK; }
+
 struct ws_layout {
   size_t pk_aff, pk_code, P, Q, skip, set_code, sig_code, f, fpart, fpart2, segv, n_bad, result;
   size_t sig_aff, sig_use, msm_cnt, msm_off, msm_cur, msm_idx, msm_sum, mlist, mcnt, lines, hrow, total;
@@ -433,7 +442,8 @@ struct ws_layout {
     const uint32_t n = pp.n, np = pp.n_pairs, nf = pp.n_f();
     const bool msm = pp.msm;
     // first product level; segmented: nseg rows of the last segment's width
-    nb_f = (nf + TB_PROD_CHUNK - 1) / TB_PROD_CHUNK + pp.nseg * ((pp.n_groups() + pp.n_xwave + TB_PROD_CHUNK - 1) / TB_PROD_CHUNK);
+    const uint32_t pc = prod_chunk(pp);
+    nb_f = (nf + pc - 1) / pc + pp.nseg * ((pp.n_groups() + pp.n_xwave + TB_PROD_CHUNK - 1) / TB_PROD_CHUNK);
     size_t o = 0;
     pk_aff = o;   o = align_up(o + (size_t)K * sizeof(g1a));
     pk_code = o;  o = align_up(o + K);
@@ -456,7 +466,7 @@ struct ws_layout {
     lines = o;    o = align_up(o + (size_t)pp.line_pairs() * TB_LINE_BYTES_PER_PAIR);
     f = o;        o = align_up(o + (size_t)(nf ? nf : 1) * sizeof(fp12));
     fpart = o;    o = align_up(o + (size_t)nb_f * sizeof(fp12));
-    fpart2 = o;   o = align_up(o + (size_t)((nb_f + TB_PROD_CHUNK - 1) / TB_PROD_CHUNK + pp.nseg) * sizeof(fp12));
+    fpart2 = o;   o = align_up(o + (size_t)((nb_f + pc - 1) / pc + pp.nseg) * sizeof(fp12));
     segv = o;     o = align_up(o + (size_t)pp.nseg * sizeof(fp12));
     n_bad = o;    o = align_up(o + 4);
     result = o;   o = align_up(o + 4);
@@ -804,9 +814,9 @@ int launch_partial(dev_ctx& c, const tbls_dev_batch& b, hipStream_t s, void* par
                          0u, (fp12*)partial_out);
     } else
     for (;;) {
-      const uint32_t nout = (cnt + TB_PROD_CHUNK - 1) / TB_PROD_CHUNK;
+      const uint32_t pc = prod_chunk(pp), nout = (cnt + pc - 1) / pc;
       fp12* dstp = nout == 1 ? (fp12*)partial_out : (fp12*)(w + ((lvl & 1) ? L.fpart2 : L.fpart));
-      hipLaunchKernelGGL(k_fp12_prod_wave, dim3(nout), dim3(64), 0, s, src, cnt, TB_PROD_CHUNK, dstp);
+      hipLaunchKernelGGL(k_fp12_prod_wave, dim3(nout), dim3(64), 0, s, src, cnt, pc, dstp);
       if (nout == 1) break;
       src = dstp;
       cnt = nout;
