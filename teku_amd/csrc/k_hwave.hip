@@ -290,7 +290,7 @@ extern "C" __global__ void __launch_bounds__(256)
   }
   __syncthreads();
   HSTAMP(4);
-  for (int k = 0; k < CF_NLEVEL; k++) crow::level<2, 2, CF_AMAX, CF_BMAX, CF_QMAX * CF_OMAX>(L.S, L.tab, CF_TYPE_OFF[CF_SEQ[k]], K);
+  for (int k = 0; k < CF_NLEVEL; k++) crow::level<2, 2, CF_AMAX, CF_BMAX, CF_QMAX * CF_OMAX, true>(L.S, L.tab, CF_TYPE_OFF[CF_SEQ[k]], K);
   if (g < 6) {
     const fp v = crow::to_fp(L.S[CF_S_RX0 + g][d], L.rb[g].d, &L.rb[g].f);
     if (d == 0) L.res[g] = v;

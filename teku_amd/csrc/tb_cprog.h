@@ -210,8 +210,12 @@ __device__ TB_INLINE void cmul_first(c32 (&pr)[KP], const c32 (&xa)[KP], const c
   TB_UNROLL for (int k = 0; k < N; k++) pr[k] = r[k];
 }
 
-// one level of a generated program on 16 rows (tables in LDS at tab + off)
-template <int KP, int KO, int AMAX, int BMAX, int OTERMS>
+// one level of a generated program on 16 rows (tables in LDS at tab + off).
+// NOALIAS: no output slot of a level is a term of another output's sum in
+// that level (tests/test_level_tables.py checks the cofactor program's
+// tables), so a row stores its outputs without waiting for the other rows'
+// output sums.
+template <int KP, int KO, int AMAX, int BMAX, int OTERMS, bool NOALIAS = false>
 __device__ TB_INLINE void level(cdig* S, const uint16_t* tab, int off, const cctx& K) {
   const int g = row(), d = dig();
   const uint16_t* H = tab + off;
@@ -262,7 +266,7 @@ __device__ TB_INLINE void level(cdig* S, const uint16_t* tab, int off, const cct
       out[k] = coop::creduce64(psum<OTERMS>(S, ent, qbeg[j0], qbeg[j1]), K.plo[0]);
     }
   }
-  __syncthreads();
+  if constexpr (!NOALIAS) __syncthreads();
   TB_UNROLL for (int k = 0; k < KO; k++) {
     const int o = g + 16 * k;
     if (16 * k < no && o < no) S[odst[o]][d] = out[k];

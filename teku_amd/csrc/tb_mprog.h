@@ -101,19 +101,16 @@ __device__ TB_INLINE void wprog_level(fp* S, u13* part, const uint16_t* tab, int
     part[l] = cs_norm(acc);
   }
   __syncthreads();
-  fp r;
-  int dst = 0;
+  // the outputs read only part[], so a lane may store its output while
+  // others still sum theirs: no barrier between the two
   if (l < no) {
     u13 acc;
     TB_UNROLL for (int i = 0; i < 13; i++) acc.l[i] = 0;
     const int j0 = obeg[l], j1 = obeg[l + 1];
     TB_UNROLL for (int j = 0; j < OMAX; j++)
       if (j0 + j < j1) u13_add(acc, part[j0 + j]);
-    r = reduce13(acc);
-    dst = odst[l];
-  }
-  __syncthreads();
-  if (l < no) {
+    const fp r = reduce13(acc);
+    const int dst = odst[l];
     S[dst] = r;
     S[NSLOT + dst] = fp_neg2p(r);
   }
