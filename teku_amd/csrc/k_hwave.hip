@@ -220,6 +220,99 @@ __device__ TB_INLINE bool e2p_add_iso_row(g2j& out, const g2a& p, const g2a& q, 
   return true;
 }
 
+// The two SSWU maps with the inversion off the exponentiations' path
+// (tb_cprog.h crow::sswu restated over three phases and two rows per map):
+// x1 = (-B/A)(1 + 1/tv) = X1n / tv with X1n = (-B/A)(tv + 1), so
+// gx1 = G / tv^3 with G = X1n (X1n^2 + A tv^2) + B tv^3, and
+// sqrt(N(gx1)) = sqrt(N(G) N(tv)) / N(tv)^2: row A (4 m: rows 0 and 4)
+// starts the first square-root exponentiation on N(G) N(tv) at once while
+// row B (8 + 4 m) inverts N(tv) (tb_cinv.h) and forms x1, gx1, x2, gx2 and
+// N(tv)^-2 beside it; then row A finishes as crow::sswu does, with
+// g1 = (N(G) N(tv))^((p+1)/4) N(tv)^-2, which squares to +-N(gx1) exactly
+// as crow::sswu's g1.  tv = 0 (the exceptional case) takes X1n = B/(Z A),
+// tv = 1, as crow::sswu.
+struct sswu_sh {
+  cdig zu2[2], tv[2], x1n[2], ntv, x1[2], x2[2], gx1[2], gx2[2], in2, n;
+};
+__device__ TB_INLINE void sswu_p1(sswu_sh& W, const fp2& u_in, crow::rowbuf& B, const coop::cctx& K) {  // row A
+  using namespace crow;
+  const int d = dig();
+  const c2 u = from_fp2(u_in);
+  const c2 A = from_const2(SSWU_A), Bc = from_const2(SSWU_B);
+  const c2 zu2 = mul(from_const2(SSWU_Z), sqr(u, K), K);
+  const c2 tv = norm(add(sqr(zu2, K), zu2));
+  const bool exc = fp2_is_zero(to_fp2(tv, B));
+  const c2 one2 = {from_const(R1), c32(0)};
+  const c2 tvs = exc ? one2 : tv;
+  const c2 x1n = exc ? from_const2(SSWU_B_OVER_ZA) : mul(from_const2(SSWU_MINUS_B_OVER_A), norm(add(tvs, one2)), K);
+  const c2 t2 = sqr(tvs, K);
+  const c2 t3 = mul(t2, tvs, K);
+  const c2 G = norm(add(mul(norm(add(sqr(x1n, K), mul(A, t2, K))), x1n, K), mul(Bc, t3, K)));
+  const c32 ntv = coop::cnorm(norm2(tvs, K));
+  W.zu2[0][d] = zu2.c0, W.zu2[1][d] = zu2.c1;
+  W.tv[0][d] = tvs.c0, W.tv[1][d] = tvs.c1;
+  W.x1n[0][d] = x1n.c0, W.x1n[1][d] = x1n.c1;
+  W.ntv[d] = ntv;
+  W.n[d] = coop::cmul(coop::cnorm(norm2(G, K)), ntv, K);
+}
+__device__ TB_INLINE void sswu_p2b(sswu_sh& W, crow::rowbuf& B, const coop::cctx& K) {  // row B, beside row A's first exponentiation
+  using namespace crow;
+  const int d = dig();
+  const c2 A = from_const2(SSWU_A), Bc = from_const2(SSWU_B);
+  const fp nt = to_fp(W.ntv[d], B.d, &B.f);
+  const fp zi = cinv::inv_row_lane0<true>(nt, B.d);
+  if (d == 0) B.f = zi;
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  const c32 in = from_fp(B.f);
+  __builtin_amdgcn_wave_barrier();
+  const c2 tvs = {W.tv[0][d], W.tv[1][d]}, x1n = {W.x1n[0][d], W.x1n[1][d]}, zu2 = {W.zu2[0][d], W.zu2[1][d]};
+  const c2 ti = mul_fp({tvs.c0, -tvs.c1}, in, K);  // 1 / tv
+  const c2 x1 = mul(x1n, ti, K);
+  const c2 gx1 = norm(add(mul(norm(add(sqr(x1, K), A)), x1, K), Bc));
+  const c2 x2 = mul(zu2, x1, K);
+  const c2 gx2 = norm(add(mul(norm(add(sqr(x2, K), A)), x2, K), Bc));
+  W.x1[0][d] = x1.c0, W.x1[1][d] = x1.c1;
+  W.x2[0][d] = x2.c0, W.x2[1][d] = x2.c1;
+  W.gx1[0][d] = gx1.c0, W.gx1[1][d] = gx1.c1;
+  W.gx2[0][d] = gx2.c0, W.gx2[1][d] = gx2.c1;
+  W.in2[d] = coop::cmul(in, in, K);
+}
+__device__ TB_INLINE g2a sswu_p3(const sswu_sh& W, const fp2& u_in, const coop::c32& g1p, crow::rowbuf& B, const coop::cctx& K) {  // row A
+  using namespace crow;
+  const int d = dig();
+  const c2 u = from_fp2(u_in);
+  const c2 x1 = {W.x1[0][d], W.x1[1][d]}, x2 = {W.x2[0][d], W.x2[1][d]};
+  const c2 gx1 = {W.gx1[0][d], W.gx1[1][d]}, gx2 = {W.gx2[0][d], W.gx2[1][d]};
+  const c32 g1 = coop::cmul(g1p, W.in2[d], K);
+  const c32 n1 = coop::cnorm(norm2(gx1, K));
+  const bool sq1 = eq(coop::cmul(g1, g1, K), n1, B);
+  const c32 nu = coop::cnorm(norm2(u, K));
+  const c32 c = coop::cmul(coop::cmul(coop::cmul(nu, nu, K), nu, K), from_const(SQRT_MINUS_125), K);
+  const c32 g2 = coop::cmul(c, g1, K);
+  const c2 x = sq1 ? x1 : x2, gx = sq1 ? gx1 : gx2;
+  const c32 gam = sq1 ? g1 : g2;
+  const c32 half = from_const(FP_HALF);
+  c32 delta = coop::cmul(coop::cnorm(gx.c0 + gam), half, K);
+  if (is_zero(delta, B)) delta = coop::cmul(coop::cnorm(gx.c0 - gam), half, K);
+  c32 sr;
+  {
+    c32 a1[1] = {delta}, r1[1];
+    coop::cpow_win_n<1>(r1, a1, EXPW_PM3D4_FIRST, EXPW_PM3D4, EXPW_PM3D4_N, K);
+    sr = r1[0];
+  }
+  const c32 sd = coop::cmul(sr, delta, K);
+  const c32 chi = coop::cmul(sr, sd, K);
+  const c32 hs = coop::cmul(coop::cmul(gx.c1, sr, K), half, K);
+  const bool pos = eq(chi, from_const(R1), B);
+  const c2 y = pos ? c2{sd, hs} : c2{-hs, sd};
+  g2a q;
+  q.x = to_fp2(x, B);
+  q.y = to_fp2(y, B);
+  if (fp2_sgn0(u_in) != fp2_sgn0(q.y)) q.y = fp2_neg(q.y);
+  return q;
+}
+
 struct hcoop_lds {
   cdig S[CF_NSLOT];
   uint16_t tab[CF_TAB_N];
@@ -231,6 +324,7 @@ struct hcoop_lds {
   g2a qa;  // the affine H(m) before [r] (rand != nullptr)
   int ok;
   xmd_words X;
+  sswu_sh W[2];
 };
 
 extern "C" __global__ void __launch_bounds__(256)
@@ -263,11 +357,23 @@ extern "C" __global__ void __launch_bounds__(256)
   }
   __syncthreads();
   HSTAMP(1);
-  // map m on row 4 m: the first row of waves 0 and 1, each the only active
-  // row of its wave, so the row inversion's divsteps run on the scalar unit
+  // map m on rows 4 m (A) and 8 + 4 m (B): the first rows of the four
+  // waves, each the only active row of its wave (the row inversion's
+  // divsteps then run on the scalar unit)
+  if (g == 0 || g == 4) sswu_p1(L.W[g >> 2], L.u[g >> 2], L.rb[g], K);
+  __syncthreads();
+  coop::c32 g1p = 0;
+  if (g == 0 || g == 4) {
+    coop::c32 a1[1] = {L.W[g >> 2].n[d]}, r1[1];
+    coop::cpow_win_n<1>(r1, a1, EXPW_SQRT_FIRST, EXPW_SQRT, EXPW_SQRT_N, K);
+    g1p = r1[0];
+  } else if (g == 8 || g == 12) {
+    sswu_p2b(L.W[(g - 8) >> 2], L.rb[g], K);
+  }
+  __syncthreads();
   if (g == 0 || g == 4) {
     const int m = g >> 2;
-    const g2a q = crow::sswu<true>(L.u[m], L.rb[g], K);
+    const g2a q = sswu_p3(L.W[m], L.u[m], g1p, L.rb[g], K);
     if (d == 0) L.qm[m] = q;
   }
   __syncthreads();
