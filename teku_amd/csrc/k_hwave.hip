@@ -175,47 +175,86 @@ __device__ TB_NOINLINE void hash_to_field_fp2_words(fp2& u0, fp2& u1, const xmd_
 }
 
 // Q0 + Q1 on E2' (madd-2007-bl, Z1 = 1) and the 3-isogeny (tb_h2c.h
-// e2p_add_aff_aff, iso_map_jac: the same formulas) as coop products on row 0,
-// instead of one lane's (119 us at 128 sets, tools/hash_stamps_probe.py).
-// Q0.x == Q1.x (doubling or infinity) returns false: lane 0 then runs the
-// exact one-lane formulas.  p, q: LDS (the row reads their words).
-__device__ TB_INLINE bool e2p_add_iso_row(g2j& out, const g2a& p, const g2a& q, crow::rowbuf& B, const coop::cctx& K) {
+// e2p_add_aff_aff, iso_map_jac: the same formulas) as coop products on the
+// four rows of wave 0, instead of one lane's (119 us at 128 sets,
+// tools/hash_stamps_probe.py): row 0 forms Q0 + Q1 = (X, Y, Z) and Z^2, Z^4,
+// Z^6; then row r evaluates one of the isogeny's four polynomials -- Nx, Ny,
+// Dx, Dy, each ((a3 X + a2) X + a1) X + a0 with a_i a constant times a power
+// of Z (Dx, of degree 2: a3 = 0, a2 = 1) -- and row 0 combines them.  Q0.x
+// == Q1.x (doubling or infinity) returns false: lane 0 then runs the exact
+// one-lane formulas.  p, q: LDS (the rows read their words).  Every row of
+// wave 0 calls it.
+struct iso_sh {
+  cdig X[2], Y[2], Z[2], zp[3][2], P[4][2];
+  int exc;
+};
+__device__ TB_INLINE void st2(cdig (&dst)[2], const crow::c2& v, int d) {
+  dst[0][d] = v.c0;
+  dst[1][d] = v.c1;
+}
+__device__ TB_INLINE crow::c2 ld2(const cdig (&src)[2], int d) { return {src[0][d], src[1][d]}; }
+__device__ TB_INLINE void wave_sync() {
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+}
+__device__ TB_INLINE bool e2p_add_iso_rows(g2j& out, const g2a& p, const g2a& q, crow::rowbuf* rb, iso_sh& W, const coop::cctx& K) {
   using namespace crow;
-  const c2 px = from_fp2(p.x), py = from_fp2(p.y), qx = from_fp2(q.x), qy = from_fp2(q.y);
-  const c2 H = norm(sub(qx, px));
-  if (is_zero(H.c0, B) && is_zero(H.c1, B)) return false;
-  const c2 dy = norm(sub(qy, py));
-  const c2 r = norm(add(dy, dy));
-  const c2 HH = sqr(H, K);
-  const c2 I = norm(add(add(HH, HH), add(HH, HH)));
-  const c2 J = mul(H, I, K), V = mul(px, I, K);
-  const c2 X = norm(sub(sub(sqr(r, K), J), add(V, V)));
-  const c2 pyJ = mul(py, J, K);
-  const c2 Y = norm(sub(mul(r, norm(sub(V, X)), K), add(pyJ, pyJ)));
-  const c2 Z = norm(add(H, H));
-  // 3-isogeny, Jacobian in and out (Z != 0 here)
-  const c2 z2 = sqr(Z, K), z4 = sqr(z2, K);
-  const c2 z6 = mul(z4, z2, K);
-  const c2 zp[3] = {z6, z4, z2};  // Z^(2(3-i)), i < 3
-  c2 nx = from_const2(ISO_XNUM[3]), ny = from_const2(ISO_YNUM[3]);
-  TB_UNROLL for (int i = 2; i >= 0; i--) {
-    nx = norm(add(mul(nx, X, K), mul(from_const2(ISO_XNUM[i]), zp[i], K)));
-    ny = norm(add(mul(ny, X, K), mul(from_const2(ISO_YNUM[i]), zp[i], K)));
+  const int g = row(), d = dig();
+  if (g == 0) {
+    const c2 px = from_fp2(p.x), py = from_fp2(p.y), qx = from_fp2(q.x), qy = from_fp2(q.y);
+    const c2 H = norm(sub(qx, px));
+    const bool exc = is_zero(H.c0, rb[0]) && is_zero(H.c1, rb[0]);
+    if (d == 0) W.exc = exc ? 1 : 0;
+    if (!exc) {
+      const c2 dy = norm(sub(qy, py));
+      const c2 r = norm(add(dy, dy));
+      const c2 HH = sqr(H, K);
+      const c2 I = norm(add(add(HH, HH), add(HH, HH)));
+      const c2 J = mul(H, I, K), V = mul(px, I, K);
+      const c2 X = norm(sub(sub(sqr(r, K), J), add(V, V)));
+      const c2 pyJ = mul(py, J, K);
+      const c2 Y = norm(sub(mul(r, norm(sub(V, X)), K), add(pyJ, pyJ)));
+      const c2 Z = norm(add(H, H));
+      const c2 z2 = sqr(Z, K), z4 = sqr(z2, K);
+      st2(W.X, X, d);
+      st2(W.Y, Y, d);
+      st2(W.Z, Z, d);
+      st2(W.zp[0], z2, d);
+      st2(W.zp[1], z4, d);
+      st2(W.zp[2], mul(z4, z2, K), d);
+    }
   }
-  const c2 dx = norm(add(mul(norm(add(X, mul(from_const2(ISO_XDEN[1]), z2, K))), X, K), mul(from_const2(ISO_XDEN[0]), z4, K)));
-  c2 dyv = norm(add(X, mul(from_const2(ISO_YDEN[2]), z2, K)));
-  dyv = norm(add(mul(dyv, X, K), mul(from_const2(ISO_YDEN[1]), z4, K)));
-  dyv = norm(add(mul(dyv, X, K), mul(from_const2(ISO_YDEN[0]), z6, K)));
-  const c2 dy2 = sqr(dyv, K), dxdy = mul(dx, dyv, K);
-  const c2 oz = mul(Z, dxdy, K);
-  const c2 ox = mul(nx, mul(dyv, dxdy, K), K);
-  const c2 dx2 = sqr(dx, K);
-  const c2 oy = mul(mul(Y, ny, K), mul(mul(dx2, dx, K), dy2, K), K);
-  const fp2 fx = to_fp2(ox, B), fy = to_fp2(oy, B), fz = to_fp2(oz, B);
-  if (dig() == 0) {
-    out.x = fx;
-    out.y = fy;
-    out.z = fz;
+  wave_sync();
+  if (W.exc) return false;
+  // row g: polynomial g of Nx, Ny, Dx, Dy
+  const c2 X = ld2(W.X, d), z2 = ld2(W.zp[0], d), z4 = ld2(W.zp[1], d), z6 = ld2(W.zp[2], d);
+  const c2 one2 = {from_const(R1), c32(0)};
+  const bool dxr = g == 2;
+  const uint32_t(*C)[2][12] = g == 0 ? ISO_XNUM : g == 1 ? ISO_YNUM : g == 2 ? ISO_XDEN : ISO_YDEN;
+  const uint32_t(*C3)[2][12] = g == 2 ? ISO_YDEN : C;  // (Dx has no a3: read a valid entry, then take 0)
+  const c2 w2 = dxr ? one2 : z2, w1 = dxr ? z2 : z4, w0 = dxr ? z4 : z6;
+  const c2 a2 = mul(from_const2(C[2]), w2, K), a1 = mul(from_const2(C[1]), w1, K), a0 = mul(from_const2(C[0]), w0, K);
+  c2 acc = from_const2(C3[3]);
+  if (dxr) acc = {c32(0), c32(0)};
+  acc = norm(add(mul(acc, X, K), a2));
+  acc = norm(add(mul(acc, X, K), a1));
+  acc = norm(add(mul(acc, X, K), a0));
+  st2(W.P[g], acc, d);
+  wave_sync();
+  if (g == 0) {
+    const c2 nx = ld2(W.P[0], d), ny = ld2(W.P[1], d), dx = ld2(W.P[2], d), dyv = ld2(W.P[3], d);
+    const c2 Y = ld2(W.Y, d), Z = ld2(W.Z, d);
+    const c2 dy2 = sqr(dyv, K), dxdy = mul(dx, dyv, K);
+    const c2 oz = mul(Z, dxdy, K);
+    const c2 ox = mul(nx, mul(dyv, dxdy, K), K);
+    const c2 dx2 = sqr(dx, K);
+    const c2 oy = mul(mul(Y, ny, K), mul(mul(dx2, dx, K), dy2, K), K);
+    const fp2 fx = to_fp2(ox, rb[0]), fy = to_fp2(oy, rb[0]), fz = to_fp2(oz, rb[0]);
+    if (d == 0) {
+      out.x = fx;
+      out.y = fy;
+      out.z = fz;
+    }
   }
   return true;
 }
@@ -325,6 +364,7 @@ struct hcoop_lds {
   int ok;
   xmd_words X;
   sswu_sh W[2];
+  iso_sh I;
 };
 
 extern "C" __global__ void __launch_bounds__(256)
@@ -380,7 +420,7 @@ extern "C" __global__ void __launch_bounds__(256)
   HSTAMP(2);
   {
     bool done = true;
-    if (g == 0) done = e2p_add_iso_row(L.J, L.qm[0], L.qm[1], L.rb[0], K);
+    if (g < 4) done = e2p_add_iso_rows(L.J, L.qm[0], L.qm[1], L.rb, L.I, K);
     if (threadIdx.x == 0 && !done) L.J = iso_map_jac(e2p_add_aff_aff(L.qm[0], L.qm[1]));
   }
   __syncthreads();
