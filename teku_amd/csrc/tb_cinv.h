@@ -21,7 +21,8 @@
 //   [f, g] <- T [f, g] / 2^30,   [d, e] <- (T [d, e] + [md, me] M) / 2^30
 // with md, me making the low 30 bits vanish.  37 batches = 1,110 divsteps
 // >= floor((49 * 382 + 57) / 17) = 1,104, the divstep bound for inputs below
-// 2^382 (x < 2p): then g = 0, f = +-1 and x^-1 = +-d.  |d| grows by at most
+// 2^382 (x < 2p): then g = 0, f = +-1 and x^-1 = +-d.  With U (one row per
+// wave) the loop stops at the first batch that leaves every limb of g zero.  |d| grows by at most
 // M per batch (|T| rows sum to <= 2^30): |d| < 38 M < 2^387, within the 16
 // limbs.  x = 0 gives d = 0 (the result 0, as fp_inv).
 // Output: the Montgomery inverse, x R in -> x^-1 R out (R = 2^406): the
@@ -110,6 +111,9 @@ TBC_FN c32 from_next(c32 x) { return coop::dpp_<0x101>(x); }  // row_shl:1: lane
 TBC_FN c32 tab(const int32_t* t) { return t[coop::lane16()]; }
 TBC_FN c64 split_lo(c64 x) { return coop::lane16() == 15 ? x : x - ((x >> 30) << 30); }  // lane 15 keeps the top
 TBC_FN c64 split_hi(c64 x) { return coop::lane16() == 15 ? (c64)0 : x >> 30; }
+// every limb of x zero on the active lanes (U: the row is the wave's only
+// active row, so the ballot is the row's)
+TBC_FN bool row_zero_u(c32 x) { return __ballot(x != 0) == 0; }
 #else
 template <bool U>
 inline uint32_t uni(uint32_t x) {
@@ -136,6 +140,11 @@ inline c64 split_hi(const c64& x) {
   c64 r;
   for (int j = 0; j < 16; j++) r.v[j] = j == 15 ? 0 : x.v[j] >> 30;
   return r;
+}
+inline bool row_zero_u(const c32& x) {
+  for (int j = 0; j < 16; j++)
+    if (x.v[j] != 0) return false;
+  return true;
 }
 #endif
 
@@ -196,6 +205,11 @@ TBC_FN fp inv_row_lane0(const fp& a, int32_t* buf) {
     g = shift30(cg);
     d = shift30(cd);
     e = shift30(ce);
+    // variable time (U only): once every limb of g is zero, g = 0 and the
+    // remaining batches would leave d and f as they are (md = 0, f' = f).
+    // Limbs of a zero g in another form only delay the exit.
+    if constexpr (U)
+      if (row_zero_u(g)) break;
   }
   d = d + tab(P30X64);  // d + 64 p > 0
   int32_t dl[16], fl[16];

@@ -153,7 +153,7 @@ TB_HD TB_INLINE bool test_op_a(int op, const uint8_t* in, uint8_t* out) {
       break;
 #if !defined(__HIPCC__)
     case TOP_FP_INV_ROW:
-      tio_put_fp(out, cinv::inv_row_lane0(tio_fp(in), nullptr));
+      tio_put_fp(out, cinv::inv_row_lane0<true>(tio_fp(in), nullptr));  // with the early exit
       break;
 #endif
     case TOP_FP2_MUL:
